@@ -1,0 +1,54 @@
+import importlib
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(REPO, "tests", "golden")
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) — run via gpurun")
+
+
+def load_pkg():
+    """The product package lives in the directory ``nice-slam_amd`` (not a valid identifier)."""
+    return importlib.import_module("nice-slam_amd")
+
+
+@pytest.fixture(scope="session")
+def pkg():
+    return load_pkg()
+
+
+@pytest.fixture(scope="session")
+def tiny():
+    with np.load(os.path.join(GOLDEN, "tiny_scene.npz")) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(scope="session")
+def room0():
+    with np.load(os.path.join(GOLDEN, "room0_color.npz")) as z:
+        return {k: z[k] for k in z.files}
+
+
+def sd_from(tiny):
+    import torch
+    return {k[3:]: torch.from_numpy(v) for k, v in tiny.items() if k.startswith("sd.")}
+
+
+def grids_from(tiny):
+    import torch
+    return {k: torch.from_numpy(tiny[k]) for k in ("grid_coarse", "grid_middle", "grid_fine", "grid_color")}
+
+
+def rel_l2(a, b):
+    a = np.asarray(a, dtype=np.float64).ravel()
+    b = np.asarray(b, dtype=np.float64).ravel()
+    den = np.linalg.norm(b)
+    return float(np.linalg.norm(a - b) / (den if den > 0 else 1.0))
