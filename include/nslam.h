@@ -1,0 +1,135 @@
+/*
+ * nslam.h — C-ABI of libnslam.so, the MI355X (gfx950) hot path of NICE-SLAM's volumetric renderer.
+ *
+ * The reference (LongruiDong/nice-slam) is pure PyTorch; it has no native/FFI boundary.  Each
+ * entry point below replaces a specific piece of the reference's Python hot path (file:line are
+ * relative to the reference checkout), and is bound from Python by ctypes in
+ * nice-slam_amd/_lib.py (see INTEGRATION.md for the binding a maintainer would add).
+ *
+ * Contract (all entry points):
+ *   - every pointer is a DEVICE pointer owned by the caller (PyTorch caching allocator);
+ *   - work is enqueued on `stream` (a hipStream_t passed as void*); nothing synchronises;
+ *   - no globals, no persistent allocations: re-entrant across threads/processes (the reference
+ *     runs tracker, mapper and coarse mapper concurrently on one GPU, src/NICE_SLAM.py:288-307);
+ *   - return 0 on success, a negative NSLAM_E* code on bad arguments, or NSLAM_EHIP - hipError
+ *     when a launch fails.  nslam_strerror() maps codes to text.
+ *
+ * Grid layout: a feature grid is the reference's [1, C=32, Z, Y, X] float32 tensor stored
+ * channels-last, i.e. physically [Z][Y][X][32] (torch.channels_last_3d); one trilinear corner
+ * is one 128-byte row.
+ */
+#ifndef NSLAM_H
+#define NSLAM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NSLAM_C_DIM 32
+#define NSLAM_HIDDEN 32
+#define NSLAM_EMB 93
+
+enum {
+  NSLAM_OK = 0,
+  NSLAM_EINVAL = -1,       /* bad pointer / size / enum */
+  NSLAM_EUNSUPPORTED = -2, /* configuration outside the NICE-SLAM path (e.g. S > 256) */
+  NSLAM_EWORKSPACE = -3,   /* workspace too small */
+  NSLAM_EHIP = -1000       /* NSLAM_EHIP - hipError_t */
+};
+
+enum { NSLAM_STAGE_COARSE = 0, NSLAM_STAGE_MIDDLE = 1, NSLAM_STAGE_FINE = 2, NSLAM_STAGE_COLOR = 3 };
+enum { NSLAM_DEC_COARSE = 0, NSLAM_DEC_MIDDLE = 1, NSLAM_DEC_FINE = 2, NSLAM_DEC_COLOR = 3 };
+
+/* One feature grid (src/NICE_SLAM.py:192-250) with the bound it is normalised against
+ * (decoder.bound, src/NICE_SLAM.py:152-157; the coarse decoder uses bound*2). */
+typedef struct nslam_grid {
+  const float* data; /* channels-last [Z][Y][X][32]; NULL when the stage does not read it */
+  float* grad;       /* same layout, accumulated with atomics; NULL = no grid gradient      */
+  int32_t dims[3];   /* Z, Y, X (= D, H, W of F.grid_sample)                                 */
+  int32_t pad_;
+  double lo[3];      /* x, y, z lower bound (float64, as the reference)                      */
+  double hi[3];      /* x, y, z upper bound                                                  */
+} nslam_grid;
+
+/* Where a decoder's parameter gradients go: `base` is a flat float32 buffer and the offsets are
+ * element offsets of each parameter in it (natural row-major [out][in] layout, i.e. the layout
+ * of nn.Linear.weight).  base == NULL: no parameter gradients for this decoder. */
+typedef struct nslam_dec_grad {
+  float* base;
+  int64_t w[5], b[5];   /* pts_linears.i.weight / .bias                       */
+  int64_t wc[5], bc[5]; /* fc_c.i.weight / .bias (unused for the coarse MLP)  */
+  int64_t wo, bo;       /* output_linear.weight / .bias                       */
+  int64_t B;            /* embedder._B [3][93] (unused for the coarse MLP)    */
+} nslam_dec_grad;
+
+/* Point query: NICE.forward + Renderer.eval_points
+ * (src/conv_onet/models/decoder.py:168-342, src/utils/Renderer.py:23-61). */
+typedef struct nslam_query_cfg {
+  int32_t stage;            /* NSLAM_STAGE_*                                             */
+  int32_t need_pts_grad;    /* backward: write d loss / d pts                             */
+  double bound_lo[3];       /* OOB test bound (strict <, >), Renderer.py:43-46            */
+  double bound_hi[3];
+  nslam_grid grid[4];       /* indexed by NSLAM_DEC_*                                     */
+  const float* packed[4];   /* packed decoder weights (nslam_pack_layout), NULL if unused */
+  nslam_dec_grad dgrad[4];  /* parameter-gradient destinations                            */
+} nslam_query_cfg;
+
+/* ---- packing ------------------------------------------------------------------------------
+ * Decoder weights are re-laid-out into MFMA fragment order by the caller (a gather with the
+ * index map described here).  kind 0 = MLP with Fourier embedding and `nc` feature blocks
+ * (middle/color nc=1, fine nc=2); kind 1 = MLP_no_xyz (coarse).  Writes up to `n` int32 values:
+ *   out[0] = total packed floats, out[1] = offset of the vector section, out[2] = fwd frag count,
+ *   out[3] = bwd frag count.  Returns the number of values written or <0. */
+int nslam_pack_layout(int kind, int nc, int32_t* out, int n);
+
+/* ---- sampler: src/utils/Renderer.py:82-174 (perturb=0, N_importance=0) ---------------------
+ * z_vals[N][S0+S1] (float64) for rays_o/rays_d [N][3] float32 and gt_depth [N] float32
+ * (NULL = no depth: S1 is forced to 0 and near = 0.01).  t_strat = torch.linspace(0,1,S0)
+ * (float32), t_surf = torch.linspace(0,1,S1).double() — passed in so the sampler uses the very
+ * values the reference uses.  ws must hold nslam_workspace_size(NSLAM_WS_SAMPLER, N) bytes. */
+int nslam_sample_rays(const float* rays_o, const float* rays_d, const float* gt_depth, int64_t n_rays,
+                      const double* bound_lo, const double* bound_hi, /* HOST pointers, 3 each */
+                      const float* t_strat, int32_t s0, const double* t_surf, int32_t s1,
+                      int32_t lindisp, double* z_vals, void* ws, size_t ws_bytes, void* stream);
+
+/* ---- fused point query ------------------------------------------------------------------------
+ * raw[M][4] float32 for pts[M][3] float64 (Renderer.eval_points incl. `ret[~mask,3]=100`). */
+int nslam_query_fwd(const nslam_query_cfg* cfg, const double* pts, int64_t n_pts, float* raw, void* stream);
+
+/* Backward of nslam_query_fwd for cotangent g_raw[M][4]: accumulates grid gradients into
+ * cfg->grid[i].grad (atomics, caller zero-initialises), parameter gradients into cfg->dgrad[i]
+ * (atomics, caller zero-initialises) and writes g_pts[M][3] float64 when cfg->need_pts_grad. */
+int nslam_query_bwd(const nslam_query_cfg* cfg, const double* pts, int64_t n_pts, const float* g_raw,
+                    double* g_pts, void* stream);
+
+/* ---- compositing: raw2outputs_nerf_color, src/common.py:204-245 (occupancy mode) ------------ */
+int nslam_composite_fwd(const float* raw, const double* z_vals, int64_t n_rays, int32_t n_samples,
+                        double* depth, double* var, float* color, void* stream);
+/* g_raw[N][S][4] from cotangents g_depth[N], g_var[N] (float64), g_color[N][3] (float32);
+ * any cotangent pointer may be NULL (= zeros). */
+int nslam_composite_bwd(const float* raw, const double* z_vals, int64_t n_rays, int32_t n_samples,
+                        const double* g_depth, const double* g_var, const float* g_color, float* g_raw,
+                        void* stream);
+
+/* ---- standalone trilinear lookup (F.grid_sample 5-D, bilinear, border, align_corners=True;
+ *      the op of src/conv_onet/models/decoder.py:173-174) ----------------------------------------
+ * coords[M][3] float32 normalised (x,y,z in [-1,1]); out[M][32]. */
+int nslam_grid_sample_fwd(const float* grid, const int32_t* dims, const float* coords, int64_t n,
+                          float* out, void* stream);
+/* grad_grid (atomics, may be NULL) and grad_coords[M][3] (may be NULL) from grad_out[M][32]. */
+int nslam_grid_sample_bwd(const float* grid, const int32_t* dims, const float* coords, int64_t n,
+                          const float* grad_out, float* grad_grid, float* grad_coords, void* stream);
+
+enum { NSLAM_WS_SAMPLER = 0 };
+size_t nslam_workspace_size(int which, int64_t n);
+
+const char* nslam_strerror(int code);
+int nslam_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NSLAM_H */

@@ -1,0 +1,16 @@
+"""nice-slam_amd — NICE-SLAM's volumetric-rendering hot path on MI355X (gfx950).
+
+Host code mirrors the reference's API (src/common.py, src/conv_onet/models/decoder.py,
+src/utils/Renderer.py, Tracker.optimize_cam_in_batch, Mapper.optimize_map); the compute runs in
+hand-written HIP kernels in libnslam.so (csrc/), bound through the C-ABI of include/nslam.h.
+The directory name is not a Python identifier: import with importlib.import_module("nice-slam_amd").
+"""
+import sys as _sys
+
+from . import _lib, common, decoder, ops, packing, renderer  # noqa: F401
+from .decoder import NICE, MLP, MLP_no_xyz  # noqa: F401
+from .renderer import Renderer  # noqa: F401
+
+_sys.modules.setdefault("nice_slam_amd", _sys.modules[__name__])
+
+__all__ = ["NICE", "MLP", "MLP_no_xyz", "Renderer", "common", "decoder", "ops", "packing", "renderer"]

@@ -1,0 +1,120 @@
+"""ctypes binding of libnslam.so (include/nslam.h).
+
+The product path calls the HIP kernels only through this module.  There is no CPU fallback:
+if the shared library is missing, or a tensor is not on a HIP device, the call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libnslam.so")
+
+NSLAM_OK = 0
+STAGES = {"coarse": 0, "middle": 1, "fine": 2, "color": 3}
+DEC_COARSE, DEC_MIDDLE, DEC_FINE, DEC_COLOR = 0, 1, 2, 3
+
+c_float_p = ctypes.POINTER(ctypes.c_float)
+
+
+class NslamGrid(ctypes.Structure):
+    _fields_ = [
+        ("data", ctypes.c_void_p),
+        ("grad", ctypes.c_void_p),
+        ("dims", ctypes.c_int32 * 3),
+        ("pad_", ctypes.c_int32),
+        ("lo", ctypes.c_double * 3),
+        ("hi", ctypes.c_double * 3),
+    ]
+
+
+class NslamDecGrad(ctypes.Structure):
+    _fields_ = [
+        ("base", ctypes.c_void_p),
+        ("w", ctypes.c_int64 * 5),
+        ("b", ctypes.c_int64 * 5),
+        ("wc", ctypes.c_int64 * 5),
+        ("bc", ctypes.c_int64 * 5),
+        ("wo", ctypes.c_int64),
+        ("bo", ctypes.c_int64),
+        ("B", ctypes.c_int64),
+    ]
+
+
+class NslamQueryCfg(ctypes.Structure):
+    _fields_ = [
+        ("stage", ctypes.c_int32),
+        ("need_pts_grad", ctypes.c_int32),
+        ("bound_lo", ctypes.c_double * 3),
+        ("bound_hi", ctypes.c_double * 3),
+        ("grid", NslamGrid * 4),
+        ("packed", ctypes.c_void_p * 4),
+        ("dgrad", NslamDecGrad * 4),
+    ]
+
+
+# every symbol include/nslam.h declares (tests check that the library exports all of them)
+EXPORTS = (
+    "nslam_pack_layout", "nslam_sample_rays", "nslam_query_fwd", "nslam_query_bwd",
+    "nslam_composite_fwd", "nslam_composite_bwd", "nslam_grid_sample_fwd", "nslam_grid_sample_bwd",
+    "nslam_workspace_size", "nslam_strerror", "nslam_abi_version",
+)
+
+_lib = None
+
+
+def lib():
+    """Load libnslam.so once (fails loudly when it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
+                               "(make -C nice-slam_amd/csrc); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i32, i64, sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
+        dp = ctypes.POINTER(ctypes.c_double)
+        L.nslam_pack_layout.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int32), ctypes.c_int]
+        L.nslam_sample_rays.argtypes = [vp, vp, vp, i64, dp, dp, vp, i32, vp, i32, i32, vp, vp, sz, vp]
+        L.nslam_query_fwd.argtypes = [ctypes.POINTER(NslamQueryCfg), vp, i64, vp, vp]
+        L.nslam_query_bwd.argtypes = [ctypes.POINTER(NslamQueryCfg), vp, i64, vp, vp, vp]
+        L.nslam_composite_fwd.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp]
+        L.nslam_composite_bwd.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, vp]
+        L.nslam_grid_sample_fwd.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), vp, i64, vp, vp]
+        L.nslam_grid_sample_bwd.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), vp, i64, vp, vp, vp, vp]
+        L.nslam_workspace_size.argtypes = [ctypes.c_int, i64]
+        L.nslam_workspace_size.restype = sz
+        L.nslam_strerror.argtypes = [ctypes.c_int]
+        L.nslam_strerror.restype = ctypes.c_char_p
+        L.nslam_abi_version.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != NSLAM_OK:
+        msg = lib().nslam_strerror(rc).decode()
+        raise RuntimeError(f"{what} failed: rc={rc} ({msg})")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None → NULL); refuses host tensors (no CPU fallback)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("nice-slam_amd kernels run on the HIP device only; got a CPU tensor")
+    return t.data_ptr()
+
+
+def stream_ptr(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def pack_layout(kind: int, nc: int = 1):
+    out = (ctypes.c_int32 * 4)()
+    n = lib().nslam_pack_layout(kind, nc, out, 4)
+    if n != 4:
+        raise RuntimeError(f"nslam_pack_layout({kind},{nc}) failed: {n}")
+    return {"total": out[0], "vec": out[1], "nf": out[2], "nb": out[3]}

@@ -1,0 +1,307 @@
+// nslam_dev.h — device-side building blocks shared by the gfx950 kernels of libnslam.so.
+//
+// Conventions (CDNA4, wave64, v_mfma_f32_32x32x2_f32):
+//   A "feature tile" is 32 features x 32 points held as one f32x16 accumulator in the MFMA C/D
+//   layout: lane l = (h = l>>5, p = l&31) holds point p, register r holds feature
+//   F(r,h) = (r&3) + 8*(r>>2) + 4*h.  Because the B operand of step s of a 32x32x2 MFMA is
+//   "row k = l>>5, column j = l&31", register s of a feature tile IS the B operand of step s when
+//   the K order of that step is {F(s,0), F(s,1)}.  So a layer Y = W*X chains tile -> tile with no
+//   data movement: A of step s in lane l is W[l&31][F(s, l>>5)] (pre-packed "fragment", 16
+//   floats per lane, 4 x dwordx4), B is X.reg[s].  The transposed product W^T*dY (backward)
+//   uses the same scheme with fragments W[F(s,l>>5)][l&31].
+//   Weight gradients sum over POINTS, so both operands are moved through LDS as [point][feature]
+//   images (row pitch 33 floats: conflict-free ds_write_b32 of the C layout and ds_read_b32 of
+//   the A/B layout).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nslam.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define NSLAM_FRAG 1024  // floats per packed fragment block (16 steps x 64 lanes)
+#define TPITCH 33        // LDS row pitch of a transposed tile [32 points][33]
+#define TILE_FLOATS (32 * TPITCH)
+
+// ------------------------------------------------------------------------------------------
+// pack layouts (single source of truth; exported to the host through nslam_pack_layout)
+// ------------------------------------------------------------------------------------------
+struct XyzPack {  // MLP with Fourier embedding (decoder.py:91-203); nc = feature blocks (1|2)
+  int nc;
+  __host__ __device__ constexpr int nf() const { return 10 + 5 * nc; }
+  __host__ __device__ constexpr int L0() const { return 0; }   // 3 blocks (emb 96)
+  __host__ __device__ constexpr int L1() const { return 3; }
+  __host__ __device__ constexpr int L2() const { return 4; }
+  __host__ __device__ constexpr int L3() const { return 5; }   // 4 blocks (emb 96 | h2 32)
+  __host__ __device__ constexpr int L4() const { return 9; }
+  __host__ __device__ constexpr int FC(int i, int c) const { return 10 + i * nc + c; }
+  __host__ __device__ constexpr int L0T() const { return nf(); }       // 3 blocks
+  __host__ __device__ constexpr int L1T() const { return nf() + 3; }
+  __host__ __device__ constexpr int L2T() const { return nf() + 4; }
+  __host__ __device__ constexpr int L3T() const { return nf() + 5; }   // 4 blocks
+  __host__ __device__ constexpr int L4T() const { return nf() + 9; }
+  __host__ __device__ constexpr int FCT(int i) const { return nf() + 10 + i; }  // feature block 0
+  __host__ __device__ constexpr int nfrag() const { return nf() + 15; }
+  __host__ __device__ constexpr int V() const { return nfrag() * NSLAM_FRAG; }
+  __host__ __device__ constexpr int Bias(int i) const { return V() + 32 * i; }
+  __host__ __device__ constexpr int BiasC(int i) const { return V() + 160 + 32 * i; }
+  __host__ __device__ constexpr int Wo() const { return V() + 320; }  // [4][32]
+  __host__ __device__ constexpr int Bo() const { return V() + 448; }  // [4]
+  __host__ __device__ constexpr int FB() const { return V() + 452; }  // [3][96]
+  __host__ __device__ constexpr int total() const { return V() + 740; }
+};
+
+struct NoXyzPack {  // MLP_no_xyz (decoder.py:206-274), coarse level
+  __host__ __device__ constexpr int L0() const { return 0; }
+  __host__ __device__ constexpr int L1() const { return 1; }
+  __host__ __device__ constexpr int L2() const { return 2; }
+  __host__ __device__ constexpr int L3() const { return 3; }  // 2 blocks (c | h2)
+  __host__ __device__ constexpr int L4() const { return 5; }
+  __host__ __device__ constexpr int nf() const { return 6; }
+  __host__ __device__ constexpr int L0T() const { return 6; }
+  __host__ __device__ constexpr int L1T() const { return 7; }
+  __host__ __device__ constexpr int L2T() const { return 8; }
+  __host__ __device__ constexpr int L3T() const { return 9; }  // 2 blocks
+  __host__ __device__ constexpr int L4T() const { return 11; }
+  __host__ __device__ constexpr int nfrag() const { return 12; }
+  __host__ __device__ constexpr int V() const { return nfrag() * NSLAM_FRAG; }
+  __host__ __device__ constexpr int Bias(int i) const { return V() + 32 * i; }
+  __host__ __device__ constexpr int Wo() const { return V() + 160; }
+  __host__ __device__ constexpr int Bo() const { return V() + 288; }
+  __host__ __device__ constexpr int total() const { return V() + 292; }
+};
+
+// ------------------------------------------------------------------------------------------
+// MFMA tile helpers
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int fidx(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) z[r] = 0.f;
+  return z;
+}
+
+// acc += Wblock * X   (frag: packed [lane][16])
+__device__ __forceinline__ void gemm_acc(f32x16& acc, const float* __restrict__ frag, const f32x16& x,
+                                         int lane) {
+  const f32x4* f = reinterpret_cast<const f32x4*>(frag) + lane * 4;
+  const f32x4 a0 = f[0], a1 = f[1], a2 = f[2], a3 = f[3];
+  acc = mfma32(a0[0], x[0], acc);
+  acc = mfma32(a0[1], x[1], acc);
+  acc = mfma32(a0[2], x[2], acc);
+  acc = mfma32(a0[3], x[3], acc);
+  acc = mfma32(a1[0], x[4], acc);
+  acc = mfma32(a1[1], x[5], acc);
+  acc = mfma32(a1[2], x[6], acc);
+  acc = mfma32(a1[3], x[7], acc);
+  acc = mfma32(a2[0], x[8], acc);
+  acc = mfma32(a2[1], x[9], acc);
+  acc = mfma32(a2[2], x[10], acc);
+  acc = mfma32(a2[3], x[11], acc);
+  acc = mfma32(a3[0], x[12], acc);
+  acc = mfma32(a3[1], x[13], acc);
+  acc = mfma32(a3[2], x[14], acc);
+  acc = mfma32(a3[3], x[15], acc);
+}
+
+// feature-tile view of a natural [32] vector: v[F(r,h)]
+__device__ __forceinline__ f32x16 vec_tile(const float* __restrict__ v, int lane) {
+  const int h = lane >> 5;
+  f32x16 t;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x4 q = *reinterpret_cast<const f32x4*>(v + 8 * i + 4 * h);
+    t[4 * i + 0] = q[0];
+    t[4 * i + 1] = q[1];
+    t[4 * i + 2] = q[2];
+    t[4 * i + 3] = q[3];
+  }
+  return t;
+}
+
+__device__ __forceinline__ f32x16 relu16(const f32x16& a) {
+  f32x16 o;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) o[r] = a[r] > 0.f ? a[r] : 0.f;
+  return o;
+}
+
+__device__ __forceinline__ uint32_t mask16(const f32x16& a) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) m |= (a[r] > 0.f ? 1u : 0u) << r;
+  return m;
+}
+
+__device__ __forceinline__ f32x16 apply_mask(const f32x16& g, uint32_t m) {
+  f32x16 o;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) o[r] = ((m >> r) & 1u) ? g[r] : 0.f;
+  return o;
+}
+
+// store a C-layout tile as a [point][feature] LDS image (pitch 33)
+__device__ __forceinline__ void tstore(float* s, const f32x16& v, int lane) {
+  const int p = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) s[p * TPITCH + fidx(r, h)] = v[r];
+}
+
+__device__ __forceinline__ float xor32(float v) { return __shfl_xor(v, 32, 64); }
+__device__ __forceinline__ double xor32d(double v) { return __shfl_xor(v, 32, 64); }
+
+// ------------------------------------------------------------------------------------------
+// trilinear corners (F.grid_sample 5-D, bilinear, padding 'border', align_corners=True)
+// ------------------------------------------------------------------------------------------
+struct Corners {
+  int32_t row[8];  // corner row index (z*H + y)*W + x; 0 when the corner is out of range
+  float w[8];      // weight ((wx*wy)*wz); exactly 0 for out-of-range corners
+  float f0[3], f1[3];  // (lo-side, hi-side) linear factors per axis x,y,z
+  float gmul[3];   // d(unnormalised)/d(normalised) incl. the clip gate: 0 or (n-1)/2
+  uint32_t ok;     // bit k: corner k is inside the grid (torch's within_bounds_3d)
+};
+
+// normalised coordinate of axis a (decoder.py:169 → common.py:269-284), float64 then .float()
+__device__ __forceinline__ float norm_coord(double p, double lo, double hi) {
+  const double ext = hi - lo;
+  return (float)(((p - lo) / ext) * 2.0 - 1.0);
+}
+
+// grid_sampler_compute_source_index with its gradient gate, per axis
+__device__ __forceinline__ float unnorm_clip(float c, int n, float& gmul) {
+  float u = ((c + 1.f) / 2.f) * (float)(n - 1);
+  gmul = (float)(n - 1) / 2.f;
+  if (u <= 0.f) {
+    u = 0.f;
+    gmul = 0.f;
+  } else if (u >= (float)(n - 1)) {
+    u = (float)(n - 1);
+    gmul = 0.f;
+  }
+  return u;
+}
+
+// nc3 = normalised (x,y,z); dims = Z,Y,X
+__device__ __forceinline__ void make_corners(Corners& c, const float nc3[3], const int32_t dims[3]) {
+  const int n[3] = {dims[2], dims[1], dims[0]};  // x→W, y→H, z→D
+  int i0[3];
+  bool hi_ok[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const float u = unnorm_clip(nc3[a], n[a], c.gmul[a]);
+    const float fl = floorf(u);
+    i0[a] = (int)fl;
+    c.f1[a] = u - fl;                      // (ix - ix_tnw)
+    c.f0[a] = (float)(i0[a] + 1) - u;      // (ix_bse - ix)
+    hi_ok[a] = (i0[a] + 1) <= n[a] - 1;
+  }
+  c.ok = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int dx = k & 1, dy = (k >> 1) & 1, dz = k >> 2;
+    const bool ok = (!dx || hi_ok[0]) && (!dy || hi_ok[1]) && (!dz || hi_ok[2]);
+    c.ok |= (ok ? 1u : 0u) << k;
+    const float w = ((dx ? c.f1[0] : c.f0[0]) * (dy ? c.f1[1] : c.f0[1])) * (dz ? c.f1[2] : c.f0[2]);
+    c.w[k] = ok ? w : 0.f;
+    c.row[k] = ok ? ((i0[2] + dz) * n[1] + (i0[1] + dy)) * n[0] + (i0[0] + dx) : 0;
+  }
+}
+
+// gather this lane's 16 channels (F(r,h) layout) of the trilinear feature
+__device__ __forceinline__ f32x16 gather_tile(const float* __restrict__ grid, const Corners& c, int lane) {
+  const int h = lane >> 5;
+  f32x16 acc = zero16();
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const f32x4* row = reinterpret_cast<const f32x4*>(grid + (size_t)c.row[k] * NSLAM_C_DIM + 4 * h);
+    const f32x4 v0 = row[0], v1 = row[2], v2 = row[4], v3 = row[6];
+    const float w = c.w[k];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc[j] += v0[j] * w;
+      acc[4 + j] += v1[j] * w;
+      acc[8 + j] += v2[j] * w;
+      acc[12 + j] += v3[j] * w;
+    }
+  }
+  return acc;
+}
+
+// d out / d (normalised coords) for cotangent tile g (this lane's 16 channels; caller adds the
+// other half with xor32 and multiplies by gmul)
+__device__ __forceinline__ void coord_grad_partial(const float* __restrict__ grid, const Corners& c,
+                                                   const f32x16& g, int lane, float out[3]) {
+  const int h = lane >> 5;
+  out[0] = out[1] = out[2] = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    __builtin_amdgcn_sched_barrier(0);  // keep the 8 corner reads from being hoisted together
+    const f32x4* row = reinterpret_cast<const f32x4*>(grid + (size_t)c.row[k] * NSLAM_C_DIM + 4 * h);
+    const f32x4 v0 = row[0], v1 = row[2], v2 = row[4], v3 = row[6];
+    float dot = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      dot += v0[j] * g[j];
+      dot += v1[j] * g[4 + j];
+      dot += v2[j] * g[8 + j];
+      dot += v3[j] * g[12 + j];
+    }
+    if (!((c.ok >> k) & 1u)) dot = 0.f;  // out-of-range corner contributes nothing
+    const int dx = k & 1, dy = (k >> 1) & 1, dz = k >> 2;
+    const float fx = dx ? c.f1[0] : c.f0[0], fy = dy ? c.f1[1] : c.f0[1], fz = dz ? c.f1[2] : c.f0[2];
+    const float sx = dx ? 1.f : -1.f, sy = dy ? 1.f : -1.f, sz = dz ? 1.f : -1.f;
+    out[0] += sx * (fy * fz) * dot;
+    out[1] += sy * (fx * fz) * dot;
+    out[2] += sz * (fx * fy) * dot;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// accurate, branch-free sin/cos for the Fourier features (args up to ~1e5 rad; decoder.py:30)
+// Reduction x - k*pi/2 in float64 (two-part pi/2, FMA), then float32 minimax polynomials on
+// [-pi/4, pi/4].  Max error ~1 ulp (the reference's torch.sin is a <=1-ulp Sleef/libm sinf).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void reduce_pio2(float x, float& r, int& q) {
+  const double xd = (double)x;
+  const double k = rint(xd * 0.63661977236758134308);
+  double rd = fma(-k, 1.5707963267948966192, xd);
+  rd = fma(-k, 6.1232339957367660e-17, rd);
+  r = (float)rd;
+  q = ((int)k) & 3;
+}
+__device__ __forceinline__ float sin_poly(float r) {
+  const float r2 = r * r;
+  float p = fmaf(r2, -1.9515295891e-4f, 8.3321608736e-3f);
+  p = fmaf(r2, p, -1.6666654611e-1f);
+  return fmaf(r * r2, p, r);
+}
+__device__ __forceinline__ float cos_poly(float r) {
+  const float r2 = r * r;
+  float p = fmaf(r2, 2.443315711809948e-5f, -1.388731625493765e-3f);
+  p = fmaf(r2, p, 4.166664568298827e-2f);
+  return fmaf(r2 * r2, p, fmaf(-0.5f, r2, 1.f));
+}
+__device__ __forceinline__ float fsin(float x) {
+  float r;
+  int q;
+  reduce_pio2(x, r, q);
+  const float s = sin_poly(r), c = cos_poly(r);
+  const float v = (q & 1) ? c : s;
+  return (q & 2) ? -v : v;
+}
+__device__ __forceinline__ float fcos(float x) {
+  float r;
+  int q;
+  reduce_pio2(x, r, q);
+  const float s = sin_poly(r), c = cos_poly(r);
+  const float v = (q & 1) ? s : c;
+  return ((q + 1) & 2) ? -v : v;
+}

@@ -1,0 +1,766 @@
+// nslam_query.hip — fused point query for gfx950: normalise → trilinear gather (channels-last
+// grids) → Fourier embedding → tiny MLP decoders on MFMA (v_mfma_f32_32x32x2_f32) → stage
+// combiner → OOB logit, and its recompute-backward.
+//
+// Replaces, per point: Renderer.eval_points (src/utils/Renderer.py:23-61), NICE.forward
+// (src/conv_onet/models/decoder.py:312-342), MLP / MLP_no_xyz forward (decoder.py:177-203,
+// 262-274), sample_grid_feature (decoder.py:168-175, F.grid_sample) and the autograd backward of
+// all of them (Tracker.py:125, Mapper.py:503).
+//
+// Work decomposition: one wave = one tile of 32 points.  Each lane pair (l, l+32) owns one point;
+// the half h = l>>5 gathers/holds the 16 feature channels F(r,h) of that point (nslam_dev.h).
+#include "nslam_dev.h"
+
+namespace {
+
+struct QueryKArgs {
+  nslam_query_cfg c;
+  const double* pts;
+  int64_t n;
+  float* raw;          // fwd output [n][4]
+  const float* g_raw;  // bwd input  [n][4]
+  double* g_pts;       // bwd output [n][3]
+};
+
+// ------------------------------------------------------------------------------------------
+// per-point context
+// ------------------------------------------------------------------------------------------
+struct Pt {
+  double p[3];
+  float x[3];  // p.float() (decoder.py:189)
+  bool valid;
+  bool inside;
+};
+
+__device__ __forceinline__ Pt load_point(const QueryKArgs& a, int64_t idx) {
+  Pt q;
+  q.valid = idx < a.n;
+  const int64_t i = q.valid ? idx : 0;  // invalid tail lanes compute on a real point, write nothing
+  q.p[0] = a.pts[i * 3 + 0];
+  q.p[1] = a.pts[i * 3 + 1];
+  q.p[2] = a.pts[i * 3 + 2];
+  bool in = true;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    q.x[k] = (float)q.p[k];
+    in = in && (q.p[k] < a.c.bound_hi[k]) && (q.p[k] > a.c.bound_lo[k]);  // Renderer.py:43-46
+  }
+  q.inside = in;
+  return q;
+}
+
+__device__ __forceinline__ void grid_corners(Corners& cr, const nslam_grid& g, const Pt& q) {
+  float nc3[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) nc3[k] = norm_coord(q.p[k], g.lo[k], g.hi[k]);
+  make_corners(cr, nc3, g.dims);
+}
+
+// ------------------------------------------------------------------------------------------
+// Fourier embedding (decoder.py:26-30): block b, reg r of lane (h,p) is dim k = 32b + F(r,h)
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float fourier_arg(const float x[3], float b0, float b1, float b2) {
+  return fmaf(x[2], b2, fmaf(x[1], b1, x[0] * b0));
+}
+
+template <bool COS>
+__device__ __forceinline__ f32x16 emb_tile(const float* __restrict__ B, const float x[3], int b, int lane) {
+  const int h = lane >> 5;
+  f32x16 e;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    // bound the interleaving of the float64 range reductions (register pressure)
+    __builtin_amdgcn_sched_barrier(0);
+    const int k = 32 * b + 8 * i + 4 * h;
+    const f32x4 B0 = *reinterpret_cast<const f32x4*>(B + k);
+    const f32x4 B1 = *reinterpret_cast<const f32x4*>(B + 96 + k);
+    const f32x4 B2 = *reinterpret_cast<const f32x4*>(B + 192 + k);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float t = fourier_arg(x, B0[j], B1[j], B2[j]);
+      e[4 * i + j] = COS ? fcos(t) : fsin(t);
+    }
+  }
+  return e;
+}
+
+// ------------------------------------------------------------------------------------------
+// LDS helpers for weight gradients (wave-private scratch, WG = 1 wave in the backward kernel)
+// ------------------------------------------------------------------------------------------
+struct Scratch {
+  float* sA;    // [32][33] transposed cotangent tile
+  float* sX;    // [32][33] transposed input tile
+  float* gtab;  // [32][4]  per-point output cotangents
+  float* xtab;  // [32][3]  per-point x (float)
+  int* crow;    // [32][8]
+  float* cw;    // [32][8]
+};
+
+__device__ __forceinline__ void lds_sync() { __syncthreads(); }
+
+// dW[o][kofs + k] += sum_p sA[p][o] * sX[p][k]   for k < kvalid
+__device__ __forceinline__ void dw_block(float* __restrict__ dst, int ldk, int kofs, int kvalid, const Scratch& S,
+                                         int lane) {
+  const int h = lane >> 5, j = lane & 31;
+  f32x16 acc = zero16();
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc = mfma32(S.sA[(2 * s + h) * TPITCH + j], S.sX[(2 * s + h) * TPITCH + j], acc);
+  if (j < kvalid) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) unsafeAtomicAdd(dst + fidx(r, h) * ldk + kofs + j, acc[r]);
+  }
+}
+
+// db[o] += sum_p sA[p][o]
+__device__ __forceinline__ void db_vec(float* __restrict__ dst, const Scratch& S, int lane) {
+  const int h = lane >> 5, o = lane & 31;
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) s += S.sA[(2 * t + h) * TPITCH + o];
+  s += xor32(s);
+  if (h == 0) unsafeAtomicAdd(dst + o, s);
+}
+
+// sA <- d ; then per input tile: sX <- x ; dW += ...
+__device__ __forceinline__ void wg_begin(const f32x16& d, const Scratch& S, int lane) { tstore(S.sA, d, lane); }
+__device__ __forceinline__ void wg_block(float* __restrict__ dW, int ldk, int kofs, int kvalid, const f32x16& x,
+                                         const Scratch& S, int lane) {
+  tstore(S.sX, x, lane);
+  lds_sync();
+  dw_block(dW, ldk, kofs, kvalid, S, lane);
+  lds_sync();
+}
+__device__ __forceinline__ void wg_end(float* __restrict__ db, const Scratch& S, int lane) {
+  lds_sync();
+  db_vec(db, S, lane);
+  lds_sync();
+}
+
+// ------------------------------------------------------------------------------------------
+// MLP with Fourier embedding (decoder.py:177-203): forward
+//   layer-3's embedding product is formed right after layer 0, so the 48-register embedding
+//   dies early (the MFMA work is unchanged).
+// ------------------------------------------------------------------------------------------
+template <int NC>
+__device__ __forceinline__ f32x16 fc_branch(const float* __restrict__ pk, const XyzPack& L, int i,
+                                            const f32x16 (&cin)[NC], int lane) {
+  f32x16 z = vec_tile(pk + L.BiasC(i), lane);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) gemm_acc(z, pk + L.FC(i, c) * NSLAM_FRAG, cin[c], lane);
+  return z;
+}
+
+template <int NC, bool KEEP>
+__device__ __forceinline__ f32x16 xyz_forward(const float* __restrict__ pk, const f32x16 (&cin)[NC],
+                                              const float x[3], int lane, uint32_t m[5], f32x16* hs) {
+  const XyzPack L{NC};
+  f32x16 a = vec_tile(pk + L.Bias(0), lane);
+  f32x16 a3 = vec_tile(pk + L.Bias(3), lane);
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    const f32x16 e = emb_tile<false>(pk + L.FB(), x, b, lane);
+    gemm_acc(a, pk + (L.L0() + b) * NSLAM_FRAG, e, lane);
+    gemm_acc(a3, pk + (L.L3() + b) * NSLAM_FRAG, e, lane);
+  }
+  m[0] = mask16(a);
+  f32x16 h = relu16(a) + fc_branch<NC>(pk, L, 0, cin, lane);
+  if (KEEP) hs[0] = h;
+  a = vec_tile(pk + L.Bias(1), lane);
+  gemm_acc(a, pk + L.L1() * NSLAM_FRAG, h, lane);
+  m[1] = mask16(a);
+  h = relu16(a) + fc_branch<NC>(pk, L, 1, cin, lane);
+  if (KEEP) hs[1] = h;
+  a = vec_tile(pk + L.Bias(2), lane);
+  gemm_acc(a, pk + L.L2() * NSLAM_FRAG, h, lane);
+  m[2] = mask16(a);
+  h = relu16(a) + fc_branch<NC>(pk, L, 2, cin, lane);
+  if (KEEP) hs[2] = h;
+  gemm_acc(a3, pk + (L.L3() + 3) * NSLAM_FRAG, h, lane);
+  m[3] = mask16(a3);
+  h = relu16(a3) + fc_branch<NC>(pk, L, 3, cin, lane);
+  if (KEEP) hs[3] = h;
+  a = vec_tile(pk + L.Bias(4), lane);
+  gemm_acc(a, pk + L.L4() * NSLAM_FRAG, h, lane);
+  m[4] = mask16(a);
+  h = relu16(a) + fc_branch<NC>(pk, L, 4, cin, lane);
+  return h;
+}
+
+// output_linear row j: sum_f Wo[j][f] h4[f] + bo[j]  (complete in both halves)
+__device__ __forceinline__ float out_row(const float* __restrict__ Wo, const float* __restrict__ bo, int j,
+                                         const f32x16& h4, int lane) {
+  const f32x16 w = vec_tile(Wo + 32 * j, lane);
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) s += w[r] * h4[r];
+  return (s + xor32(s)) + bo[j];
+}
+
+// ------------------------------------------------------------------------------------------
+// MLP with Fourier embedding: backward (forward recomputed first).
+//   gall[GOFS + j], j < NOUT : cotangents of the decoder outputs (per point, both halves)
+//   dc : out, d/d(feature block 0) (C layout);  gx : out, d/dx through the embedding (if EMBG)
+// Parameter gradients (WG) go through LDS transposes + MFMA over the 32 points and are added
+// with atomics shaped as two 128-B row segments.
+// ------------------------------------------------------------------------------------------
+template <int NC, bool WG>
+__device__ __forceinline__ void fc_bwd(const float* __restrict__ pk, const XyzPack& L, int i,
+                                       const f32x16 (&cin)[NC], const f32x16& dh, const nslam_dec_grad& dg,
+                                       const Scratch& S, int lane, f32x16& dc) {
+  gemm_acc(dc, pk + L.FCT(i) * NSLAM_FRAG, dh, lane);  // dz_i = dh_i
+  if (WG) {
+    wg_begin(dh, S, lane);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) wg_block(dg.base + dg.wc[i], 32 * NC, 32 * c, 32, cin[c], S, lane);
+    wg_end(dg.base + dg.bc[i], S, lane);
+  }
+}
+
+template <int NC, int NOUT, int GOFS, bool WG, bool EMBG>
+__device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const f32x16 (&cin)[NC],
+                                             const float x[3], const float (&gall)[4], const nslam_dec_grad& dg,
+                                             const Scratch& S, int lane, f32x16& dc, float gx[3]) {
+  const XyzPack L{NC};
+  const int h = lane >> 5;
+  uint32_t m[5];
+  f32x16 hs[4];
+  const f32x16 h4 = xyz_forward<NC, WG>(pk, cin, x, lane, m, hs);
+
+  // output layer: dh4 = Wo^T g
+  f32x16 dh = zero16();
+#pragma unroll
+  for (int j = 0; j < NOUT; ++j) {
+    const f32x16 w = vec_tile(pk + L.Wo() + 32 * j, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dh[r] += w[r] * gall[GOFS + j];
+  }
+  if (WG) {
+    tstore(S.sX, h4, lane);
+    lds_sync();
+    const int f = lane & 31;
+#pragma unroll
+    for (int j = 0; j < NOUT; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const int p = 2 * t + h;
+        s += S.gtab[p * 4 + GOFS + j] * S.sX[p * TPITCH + f];
+      }
+      s += xor32(s);
+      if (h == 0) unsafeAtomicAdd(dg.base + dg.wo + 32 * j + f, s);
+      if (lane == 0) {
+        float sb = 0.f;
+        for (int p = 0; p < 32; ++p) sb += S.gtab[p * 4 + GOFS + j];
+        unsafeAtomicAdd(dg.base + dg.bo + j, sb);
+      }
+    }
+    lds_sync();
+  }
+  dc = zero16();
+  const float* FB = pk + L.FB();
+
+  // layer 4
+  fc_bwd<NC, WG>(pk, L, 4, cin, dh, dg, S, lane, dc);
+  f32x16 da = apply_mask(dh, m[4]);
+  if (WG) {
+    wg_begin(da, S, lane);
+    wg_block(dg.base + dg.w[4], 32, 0, 32, hs[3], S, lane);
+    wg_end(dg.base + dg.b[4], S, lane);
+  }
+  dh = zero16();
+  gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
+  // layer 3 (input = [emb | h2])
+  fc_bwd<NC, WG>(pk, L, 3, cin, dh, dg, S, lane, dc);
+  const f32x16 da3 = apply_mask(dh, m[3]);
+  if (WG) {
+    wg_begin(da3, S, lane);
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+      wg_block(dg.base + dg.w[3], 125, 32 * b, b < 2 ? 32 : 29, emb_tile<false>(FB, x, b, lane), S, lane);
+    wg_block(dg.base + dg.w[3], 125, 93, 32, hs[2], S, lane);
+    wg_end(dg.base + dg.b[3], S, lane);
+  }
+  dh = zero16();
+  gemm_acc(dh, pk + (L.L3T() + 3) * NSLAM_FRAG, da3, lane);
+  // layer 2
+  fc_bwd<NC, WG>(pk, L, 2, cin, dh, dg, S, lane, dc);
+  da = apply_mask(dh, m[2]);
+  if (WG) {
+    wg_begin(da, S, lane);
+    wg_block(dg.base + dg.w[2], 32, 0, 32, hs[1], S, lane);
+    wg_end(dg.base + dg.b[2], S, lane);
+  }
+  dh = zero16();
+  gemm_acc(dh, pk + L.L2T() * NSLAM_FRAG, da, lane);
+  // layer 1
+  fc_bwd<NC, WG>(pk, L, 1, cin, dh, dg, S, lane, dc);
+  da = apply_mask(dh, m[1]);
+  if (WG) {
+    wg_begin(da, S, lane);
+    wg_block(dg.base + dg.w[1], 32, 0, 32, hs[0], S, lane);
+    wg_end(dg.base + dg.b[1], S, lane);
+  }
+  dh = zero16();
+  gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
+  // layer 0 (input = emb)
+  fc_bwd<NC, WG>(pk, L, 0, cin, dh, dg, S, lane, dc);
+  da = apply_mask(dh, m[0]);
+  if (WG) {
+    wg_begin(da, S, lane);
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+      wg_block(dg.base + dg.w[0], 93, 32 * b, b < 2 ? 32 : 29, emb_tile<false>(FB, x, b, lane), S, lane);
+    wg_end(dg.base + dg.b[0], S, lane);
+  }
+
+  // Fourier features: de_b = L3T_b da3 + L0T_b da0 ; G = de * cos(theta)
+  gx[0] = gx[1] = gx[2] = 0.f;
+  if (EMBG) {
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      f32x16 de = zero16();
+      gemm_acc(de, pk + (L.L3T() + b) * NSLAM_FRAG, da3, lane);
+      gemm_acc(de, pk + (L.L0T() + b) * NSLAM_FRAG, da, lane);
+      const f32x16 cs = emb_tile<true>(FB, x, b, lane);
+      f32x16 G;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = 32 * b + 8 * i + 4 * h;
+        const f32x4 B0 = *reinterpret_cast<const f32x4*>(FB + k);
+        const f32x4 B1 = *reinterpret_cast<const f32x4*>(FB + 96 + k);
+        const f32x4 B2 = *reinterpret_cast<const f32x4*>(FB + 192 + k);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float gk = de[4 * i + j] * cs[4 * i + j];
+          G[4 * i + j] = gk;
+          gx[0] += gk * B0[j];
+          gx[1] += gk * B1[j];
+          gx[2] += gk * B2[j];
+        }
+      }
+      if (WG) {  // dB[j][k] += sum_p x_j[p] G[k][p]
+        tstore(S.sA, G, lane);
+        lds_sync();
+        const int jj = lane & 31;
+        const int jc = jj < 3 ? jj : 0;
+        f32x16 acc = zero16();
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+          const int p = 2 * s + h;
+          const float xv = jj < 3 ? S.xtab[p * 3 + jc] : 0.f;
+          acc = mfma32(S.sA[p * TPITCH + jj], xv, acc);
+        }
+        if (jj < 3) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int k = 32 * b + fidx(r, h);
+            if (k < NSLAM_EMB) unsafeAtomicAdd(dg.base + dg.B + jj * NSLAM_EMB + k, acc[r]);
+          }
+        }
+        lds_sync();
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) gx[k] += xor32(gx[k]);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// MLP_no_xyz (coarse, decoder.py:262-274): forward / backward
+// ------------------------------------------------------------------------------------------
+template <bool KEEP>
+__device__ __forceinline__ f32x16 noxyz_forward(const float* __restrict__ pk, const f32x16& c, int lane,
+                                                uint32_t m[5], f32x16* hs) {
+  const NoXyzPack L;
+  f32x16 a = vec_tile(pk + L.Bias(0), lane);
+  gemm_acc(a, pk + L.L0() * NSLAM_FRAG, c, lane);
+  f32x16 a3 = vec_tile(pk + L.Bias(3), lane);
+  gemm_acc(a3, pk + L.L3() * NSLAM_FRAG, c, lane);
+  m[0] = mask16(a);
+  f32x16 h = relu16(a);
+  if (KEEP) hs[0] = h;
+  a = vec_tile(pk + L.Bias(1), lane);
+  gemm_acc(a, pk + L.L1() * NSLAM_FRAG, h, lane);
+  m[1] = mask16(a);
+  h = relu16(a);
+  if (KEEP) hs[1] = h;
+  a = vec_tile(pk + L.Bias(2), lane);
+  gemm_acc(a, pk + L.L2() * NSLAM_FRAG, h, lane);
+  m[2] = mask16(a);
+  h = relu16(a);
+  if (KEEP) hs[2] = h;
+  gemm_acc(a3, pk + (L.L3() + 1) * NSLAM_FRAG, h, lane);
+  m[3] = mask16(a3);
+  h = relu16(a3);
+  if (KEEP) hs[3] = h;
+  a = vec_tile(pk + L.Bias(4), lane);
+  gemm_acc(a, pk + L.L4() * NSLAM_FRAG, h, lane);
+  m[4] = mask16(a);
+  return relu16(a);
+}
+
+template <bool WG>
+__device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, const f32x16& c, float g,
+                                               const nslam_dec_grad& dg, const Scratch& S, int lane, f32x16& dc) {
+  const NoXyzPack L;
+  const int h = lane >> 5;
+  uint32_t m[5];
+  f32x16 hs[4];
+  const f32x16 h4 = noxyz_forward<WG>(pk, c, lane, m, hs);
+  f32x16 dh;
+  {
+    const f32x16 w = vec_tile(pk + L.Wo(), lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dh[r] = w[r] * g;
+  }
+  if (WG) {
+    tstore(S.sX, h4, lane);
+    lds_sync();
+    const int f = lane & 31;
+    float s = 0.f;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int p = 2 * t + h;
+      s += S.gtab[p * 4 + 3] * S.sX[p * TPITCH + f];
+    }
+    s += xor32(s);
+    if (h == 0) unsafeAtomicAdd(dg.base + dg.wo + f, s);
+    if (lane == 0) {
+      float sb = 0.f;
+      for (int p = 0; p < 32; ++p) sb += S.gtab[p * 4 + 3];
+      unsafeAtomicAdd(dg.base + dg.bo, sb);
+    }
+    lds_sync();
+  }
+  dc = zero16();
+  // layer 4
+  f32x16 da = apply_mask(dh, m[4]);
+  if (WG) {
+    wg_begin(da, S, lane);
+    wg_block(dg.base + dg.w[4], 32, 0, 32, hs[3], S, lane);
+    wg_end(dg.base + dg.b[4], S, lane);
+  }
+  dh = zero16();
+  gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
+  // layer 3 (input = [c | h2])
+  da = apply_mask(dh, m[3]);
+  if (WG) {
+    wg_begin(da, S, lane);
+    wg_block(dg.base + dg.w[3], 64, 0, 32, c, S, lane);
+    wg_block(dg.base + dg.w[3], 64, 32, 32, hs[2], S, lane);
+    wg_end(dg.base + dg.b[3], S, lane);
+  }
+  gemm_acc(dc, pk + L.L3T() * NSLAM_FRAG, da, lane);
+  dh = zero16();
+  gemm_acc(dh, pk + (L.L3T() + 1) * NSLAM_FRAG, da, lane);
+  // layer 2
+  da = apply_mask(dh, m[2]);
+  if (WG) {
+    wg_begin(da, S, lane);
+    wg_block(dg.base + dg.w[2], 32, 0, 32, hs[1], S, lane);
+    wg_end(dg.base + dg.b[2], S, lane);
+  }
+  dh = zero16();
+  gemm_acc(dh, pk + L.L2T() * NSLAM_FRAG, da, lane);
+  // layer 1
+  da = apply_mask(dh, m[1]);
+  if (WG) {
+    wg_begin(da, S, lane);
+    wg_block(dg.base + dg.w[1], 32, 0, 32, hs[0], S, lane);
+    wg_end(dg.base + dg.b[1], S, lane);
+  }
+  dh = zero16();
+  gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
+  // layer 0 (input = c)
+  da = apply_mask(dh, m[0]);
+  if (WG) {
+    wg_begin(da, S, lane);
+    wg_block(dg.base + dg.w[0], 32, 0, 32, c, S, lane);
+    wg_end(dg.base + dg.b[0], S, lane);
+  }
+  gemm_acc(dc, pk + L.L0T() * NSLAM_FRAG, da, lane);
+}
+
+// ------------------------------------------------------------------------------------------
+// grid gradient scatter (atomics shaped as two 128-B row segments per wave-instruction) and
+// coordinate gradient through the trilinear weights
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void scatter_grid_grad(float* __restrict__ grad, const Corners& cr, const f32x16& dc, bool valid,
+                                  const Scratch& S, int lane) {
+  const int h = lane >> 5, p = lane & 31;
+  tstore(S.sA, dc, lane);
+  if (h == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      S.crow[p * 8 + k] = cr.row[k];
+      S.cw[p * 8 + k] = valid ? cr.w[k] : 0.f;
+    }
+  }
+  lds_sync();
+  for (int j = 0; j < 16; ++j) {
+    const int pp = 2 * j + h;
+    const float v = S.sA[pp * TPITCH + p];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float w = S.cw[pp * 8 + k];
+      if (w != 0.f) unsafeAtomicAdd(grad + (size_t)S.crow[pp * 8 + k] * NSLAM_C_DIM + p, w * v);
+    }
+  }
+  lds_sync();
+}
+
+__device__ __forceinline__ void coord_grad(const nslam_grid& g, const Corners& cr, const f32x16& dc, int lane,
+                                           double gp[3]) {
+  float part[3];
+  coord_grad_partial(g.data, cr, dc, lane, part);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float gn = (part[k] + xor32(part[k])) * cr.gmul[k];
+    gp[k] += ((double)gn * 2.0) / (g.hi[k] - g.lo[k]);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------------------------
+template <int STAGE>
+__global__ __launch_bounds__(256, 2) void k_query_fwd(QueryKArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tile * 32 >= a.n) return;  // wave-uniform
+  const int h = lane >> 5;
+  const Pt q = load_point(a, tile * 32 + (lane & 31));
+  float out[4] = {0.f, 0.f, 0.f, 0.f};
+  uint32_t m[5];
+  if (STAGE == NSLAM_STAGE_COARSE) {
+    Corners cr;
+    grid_corners(cr, a.c.grid[NSLAM_DEC_COARSE], q);
+    const f32x16 c = gather_tile(a.c.grid[NSLAM_DEC_COARSE].data, cr, lane);
+    const float* pk = a.c.packed[NSLAM_DEC_COARSE];
+    const NoXyzPack L;
+    const f32x16 h4 = noxyz_forward<false>(pk, c, lane, m, nullptr);
+    out[3] = out_row(pk + L.Wo(), pk + L.Bo(), 0, h4, lane);
+  } else {
+    Corners cr;
+    grid_corners(cr, a.c.grid[NSLAM_DEC_MIDDLE], q);
+    const f32x16 cm[1] = {gather_tile(a.c.grid[NSLAM_DEC_MIDDLE].data, cr, lane)};
+    {
+      const float* pk = a.c.packed[NSLAM_DEC_MIDDLE];
+      const XyzPack L{1};
+      const f32x16 h4 = xyz_forward<1, false>(pk, cm, q.x, lane, m, nullptr);
+      out[3] = out_row(pk + L.Wo(), pk + L.Bo(), 0, h4, lane);
+    }
+    if (STAGE >= NSLAM_STAGE_FINE) {
+      grid_corners(cr, a.c.grid[NSLAM_DEC_FINE], q);
+      const f32x16 cf[2] = {gather_tile(a.c.grid[NSLAM_DEC_FINE].data, cr, lane), cm[0]};
+      const float* pk = a.c.packed[NSLAM_DEC_FINE];
+      const XyzPack L{2};
+      const f32x16 h4 = xyz_forward<2, false>(pk, cf, q.x, lane, m, nullptr);
+      out[3] = out_row(pk + L.Wo(), pk + L.Bo(), 0, h4, lane) + out[3];  // fine_occ + middle_occ
+    }
+    if (STAGE == NSLAM_STAGE_COLOR) {
+      grid_corners(cr, a.c.grid[NSLAM_DEC_COLOR], q);
+      const f32x16 cc[1] = {gather_tile(a.c.grid[NSLAM_DEC_COLOR].data, cr, lane)};
+      const float* pk = a.c.packed[NSLAM_DEC_COLOR];
+      const XyzPack L{1};
+      const f32x16 h4 = xyz_forward<1, false>(pk, cc, q.x, lane, m, nullptr);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) out[j] = out_row(pk + L.Wo(), pk + L.Bo(), j, h4, lane);
+    }
+  }
+  if (!q.inside) out[3] = 100.f;  // Renderer.py:57
+  if (h == 0 && q.valid) {
+    f32x4 v;
+    v[0] = out[0];
+    v[1] = out[1];
+    v[2] = out[2];
+    v[3] = out[3];
+    *reinterpret_cast<f32x4*>(a.raw + (tile * 32 + (lane & 31)) * 4) = v;
+  }
+}
+
+// One backward launch per decoder: the decoder's forward is recomputed, its parameter / grid
+// gradients are accumulated, and its share of d/dpts is added into g_pts (launches on one stream
+// are ordered, each point is owned by one lane pair: plain read-modify-write, no atomics).
+//   DEC: NSLAM_DEC_*;  FIRST: this launch initialises g_pts instead of adding.
+template <int DEC, bool WG, bool PG, bool FIRST>
+__global__ __launch_bounds__(64, 2) void k_dec_bwd(QueryKArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  Scratch S;
+  S.sA = lds;
+  S.sX = lds + TILE_FLOATS;
+  S.gtab = lds + 2 * TILE_FLOATS;
+  S.xtab = S.gtab + 32 * 4;
+  S.crow = reinterpret_cast<int*>(S.xtab + 32 * 3);
+  S.cw = reinterpret_cast<float*>(S.crow + 32 * 8);
+
+  const int lane = threadIdx.x;
+  const int64_t tile = blockIdx.x;
+  const int h = lane >> 5, p = lane & 31;
+  const int64_t idx = tile * 32 + p;
+  const Pt q = load_point(a, idx);
+  float g[4] = {0.f, 0.f, 0.f, 0.f};
+  if (q.valid) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(a.g_raw + idx * 4);
+    g[0] = v[0];
+    g[1] = v[1];
+    g[2] = v[2];
+    g[3] = q.inside ? v[3] : 0.f;  // ret[~mask,3]=100 blocks the occupancy gradient
+  }
+  if (WG) {
+    if (h == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) S.gtab[p * 4 + j] = g[j];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) S.xtab[p * 3 + j] = q.x[j];
+    }
+    lds_sync();
+  }
+  const nslam_grid& gr = a.c.grid[DEC];
+  const nslam_dec_grad& dg = a.c.dgrad[DEC];
+  const float* pk = a.c.packed[DEC];
+  Corners cr;
+  grid_corners(cr, gr, q);
+  f32x16 dc;
+  float gx[3] = {0.f, 0.f, 0.f};
+  if (DEC == NSLAM_DEC_COARSE) {
+    const f32x16 c = gather_tile(gr.data, cr, lane);
+    noxyz_backward<WG>(pk, c, g[3], dg, S, lane, dc);
+  } else if (DEC == NSLAM_DEC_FINE) {
+    Corners cm;
+    grid_corners(cm, a.c.grid[NSLAM_DEC_MIDDLE], q);
+    // the middle feature enters the fine decoder under torch.no_grad (decoder.py:184-187)
+    const f32x16 cf[2] = {gather_tile(gr.data, cr, lane), gather_tile(a.c.grid[NSLAM_DEC_MIDDLE].data, cm, lane)};
+    xyz_backward<2, 1, 3, WG, PG || WG>(pk, cf, q.x, g, dg, S, lane, dc, gx);
+  } else {
+    const f32x16 c[1] = {gather_tile(gr.data, cr, lane)};
+    if (DEC == NSLAM_DEC_COLOR)  // the colour decoder's 4th output is overwritten by the combiner
+      xyz_backward<1, 3, 0, WG, PG || WG>(pk, c, q.x, g, dg, S, lane, dc, gx);
+    else
+      xyz_backward<1, 1, 3, WG, PG || WG>(pk, c, q.x, g, dg, S, lane, dc, gx);
+  }
+  if (gr.grad) scatter_grid_grad(gr.grad, cr, dc, q.valid, S, lane);
+  if (PG) {
+    double gp[3] = {(double)gx[0], (double)gx[1], (double)gx[2]};
+    coord_grad(gr, cr, dc, lane, gp);
+    if (h == 0 && q.valid) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) a.g_pts[idx * 3 + k] = FIRST ? gp[k] : a.g_pts[idx * 3 + k] + gp[k];
+    }
+  }
+}
+
+constexpr size_t kBwdLds = (2 * TILE_FLOATS + 32 * 4 + 32 * 3 + 32 * 8 * 2) * sizeof(float);
+
+bool grid_ok(const nslam_grid& g) {
+  return g.data && g.dims[0] > 0 && g.dims[1] > 0 && g.dims[2] > 0 && (((uintptr_t)g.data) & 15) == 0;
+}
+
+int check_cfg(const nslam_query_cfg* c, bool bwd) {
+  if (!c || c->stage < 0 || c->stage > 3) return NSLAM_EINVAL;
+  const int st = c->stage;
+  bool need[4] = {st == NSLAM_STAGE_COARSE, st != NSLAM_STAGE_COARSE, st >= NSLAM_STAGE_FINE,
+                  st == NSLAM_STAGE_COLOR};
+  for (int d = 0; d < 4; ++d) {
+    if (!need[d]) continue;
+    if (!grid_ok(c->grid[d]) || !c->packed[d]) return NSLAM_EINVAL;
+    if ((((uintptr_t)c->packed[d]) & 15) != 0) return NSLAM_EINVAL;
+  }
+  (void)bwd;
+  return NSLAM_OK;
+}
+
+int hip_status() {
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? NSLAM_OK : NSLAM_EHIP - (int)e;
+}
+
+}  // namespace
+
+extern "C" int nslam_query_fwd(const nslam_query_cfg* cfg, const double* pts, int64_t n_pts, float* raw,
+                               void* stream) {
+  const int rc = check_cfg(cfg, false);
+  if (rc) return rc;
+  if (n_pts < 0 || (n_pts > 0 && (!pts || !raw))) return NSLAM_EINVAL;
+  if (n_pts == 0) return NSLAM_OK;
+  QueryKArgs a{*cfg, pts, n_pts, raw, nullptr, nullptr};
+  const int64_t tiles = (n_pts + 31) / 32;
+  const dim3 grid((unsigned)((tiles + 3) / 4)), block(256);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  switch (cfg->stage) {
+    case NSLAM_STAGE_COARSE: hipLaunchKernelGGL(k_query_fwd<NSLAM_STAGE_COARSE>, grid, block, 0, s, a); break;
+    case NSLAM_STAGE_MIDDLE: hipLaunchKernelGGL(k_query_fwd<NSLAM_STAGE_MIDDLE>, grid, block, 0, s, a); break;
+    case NSLAM_STAGE_FINE: hipLaunchKernelGGL(k_query_fwd<NSLAM_STAGE_FINE>, grid, block, 0, s, a); break;
+    default: hipLaunchKernelGGL(k_query_fwd<NSLAM_STAGE_COLOR>, grid, block, 0, s, a); break;
+  }
+  return hip_status();
+}
+
+template <int DEC, bool WG, bool PG>
+void launch_dec_bwd(const QueryKArgs& a, bool first, dim3 grid, hipStream_t s) {
+  if (first)
+    hipLaunchKernelGGL((k_dec_bwd<DEC, WG, PG, true>), grid, dim3(64), kBwdLds, s, a);
+  else
+    hipLaunchKernelGGL((k_dec_bwd<DEC, WG, PG, false>), grid, dim3(64), kBwdLds, s, a);
+}
+
+template <int DEC>
+void dispatch_dec_bwd(const QueryKArgs& a, bool first, dim3 grid, hipStream_t s) {
+  const bool wg = a.c.dgrad[DEC].base != nullptr;
+  const bool pg = a.c.need_pts_grad != 0;
+  if (wg && pg) launch_dec_bwd<DEC, true, true>(a, first, grid, s);
+  else if (wg) launch_dec_bwd<DEC, true, false>(a, first, grid, s);
+  else if (pg) launch_dec_bwd<DEC, false, true>(a, first, grid, s);
+  else launch_dec_bwd<DEC, false, false>(a, first, grid, s);
+}
+
+extern "C" int nslam_query_bwd(const nslam_query_cfg* cfg, const double* pts, int64_t n_pts, const float* g_raw,
+                               double* g_pts, void* stream) {
+  const int rc = check_cfg(cfg, true);
+  if (rc) return rc;
+  if (n_pts < 0 || (n_pts > 0 && (!pts || !g_raw))) return NSLAM_EINVAL;
+  if (cfg->need_pts_grad && n_pts > 0 && !g_pts) return NSLAM_EINVAL;
+  if (n_pts == 0) return NSLAM_OK;
+  QueryKArgs a{*cfg, pts, n_pts, nullptr, g_raw, g_pts};
+  const dim3 grid((unsigned)((n_pts + 31) / 32));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  switch (cfg->stage) {
+    case NSLAM_STAGE_COARSE:
+      dispatch_dec_bwd<NSLAM_DEC_COARSE>(a, true, grid, s);
+      break;
+    case NSLAM_STAGE_MIDDLE:
+      dispatch_dec_bwd<NSLAM_DEC_MIDDLE>(a, true, grid, s);
+      break;
+    case NSLAM_STAGE_FINE:
+      dispatch_dec_bwd<NSLAM_DEC_MIDDLE>(a, true, grid, s);
+      dispatch_dec_bwd<NSLAM_DEC_FINE>(a, false, grid, s);
+      break;
+    default:
+      dispatch_dec_bwd<NSLAM_DEC_MIDDLE>(a, true, grid, s);
+      dispatch_dec_bwd<NSLAM_DEC_FINE>(a, false, grid, s);
+      dispatch_dec_bwd<NSLAM_DEC_COLOR>(a, false, grid, s);
+      break;
+  }
+  return hip_status();
+}
+
+extern "C" int nslam_pack_layout(int kind, int nc, int32_t* out, int n) {
+  if (!out || n < 4) return NSLAM_EINVAL;
+  if (kind == 0) {
+    if (nc != 1 && nc != 2) return NSLAM_EINVAL;
+    const XyzPack L{nc};
+    out[0] = L.total();
+    out[1] = L.V();
+    out[2] = L.nf();
+    out[3] = L.nfrag() - L.nf();
+  } else if (kind == 1) {
+    const NoXyzPack L;
+    out[0] = L.total();
+    out[1] = L.V();
+    out[2] = L.nf();
+    out[3] = L.nfrag() - L.nf();
+  } else {
+    return NSLAM_EINVAL;
+  }
+  return 4;
+}

@@ -1,0 +1,270 @@
+"""torch.autograd operators over libnslam.so (HIP, gfx950).  No CPU fallback.
+
+  sample_z        — Renderer.render_batch_ray's sampler (src/utils/Renderer.py:82-170), no grad
+  query_points    — NICE.forward + eval_points (decoder.py:168-342, Renderer.py:23-61), fwd+bwd
+  composite       — raw2outputs_nerf_color (src/common.py:204-245, occupancy), fwd+bwd
+  grid_sample     — F.grid_sample(bilinear, border, align_corners=True) on a channels-last grid
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+
+from . import _lib
+from ._lib import check, lib, ptr, stream_ptr
+
+_DEC_FOR_STAGE = {
+    "coarse": ("coarse",),
+    "middle": ("middle",),
+    "fine": ("middle", "fine"),
+    "color": ("middle", "fine", "color"),
+}
+_DEC_ID = {"coarse": _lib.DEC_COARSE, "middle": _lib.DEC_MIDDLE, "fine": _lib.DEC_FINE, "color": _lib.DEC_COLOR}
+_GRID_KEYS = ("grid_coarse", "grid_middle", "grid_fine", "grid_color")
+
+
+def channels_last(g: torch.Tensor) -> torch.Tensor:
+    """[1,C,Z,Y,X] grid as physically [Z][Y][X][C] (no copy when it already is)."""
+    if g.dim() != 5 or g.shape[0] != 1 or g.shape[1] != 32:
+        raise ValueError(f"feature grid must be [1,32,Z,Y,X], got {tuple(g.shape)}")
+    if g.dtype != torch.float32:
+        raise ValueError("feature grids are float32")
+    if not g.is_contiguous(memory_format=torch.channels_last_3d):
+        g = g.contiguous(memory_format=torch.channels_last_3d)
+    return g
+
+
+def _bound_list(b):
+    b = b.detach().to("cpu", torch.float64)
+    return [float(v) for v in b[:, 0]], [float(v) for v in b[:, 1]]
+
+
+# ----------------------------------------------------------------------------------------------
+# sampler
+# ----------------------------------------------------------------------------------------------
+_T_CACHE = {}
+
+
+def _t_tables(device, s0, s1):
+    key = (str(device), s0, s1)
+    if key not in _T_CACHE:
+        ts = torch.linspace(0.0, 1.0, s0).to(device)
+        tu = torch.linspace(0.0, 1.0, max(s1, 1)).double().to(device)
+        _T_CACHE[key] = (ts, tu)
+    return _T_CACHE[key]
+
+
+def sample_z(rays_o, rays_d, gt_depth, bound, n_strat, n_surf, lindisp=False):
+    """z_vals [N, n_strat(+n_surf)] float64 (surface samples only when gt_depth is given)."""
+    ro = rays_o.detach().float().contiguous()
+    rd = rays_d.detach().float().contiguous()
+    n = ro.shape[0]
+    s1 = n_surf if gt_depth is not None else 0
+    z = torch.empty(n, n_strat + s1, dtype=torch.float64, device=ro.device)
+    if n == 0:
+        return z
+    gt = gt_depth.detach().float().reshape(-1).contiguous() if gt_depth is not None else None
+    ts, tu = _t_tables(ro.device, n_strat, n_surf)
+    lo, hi = _bound_list(bound)
+    L = lib()
+    wsb = L.nslam_workspace_size(0, n)
+    ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=ro.device)
+    rc = L.nslam_sample_rays(ptr(ro), ptr(rd), ptr(gt), n, (ctypes.c_double * 3)(*lo), (ctypes.c_double * 3)(*hi),
+                             ptr(ts), n_strat, ptr(tu), s1, int(bool(lindisp)), ptr(z), ptr(ws), wsb,
+                             stream_ptr(ro.device))
+    check(rc, "nslam_sample_rays")
+    return z
+
+
+# ----------------------------------------------------------------------------------------------
+# fused point query
+# ----------------------------------------------------------------------------------------------
+class QueryMeta:
+    """Non-tensor configuration of one query call."""
+
+    def __init__(self, stage, decs, packers, dec_bounds, oob_bound, n_params):
+        self.stage = stage
+        self.decs = decs                # tuple of decoder names used by the stage
+        self.packers = packers          # name → DecoderPacker
+        self.dec_bounds = dec_bounds    # name → ([lo]*3, [hi]*3) normalisation bound
+        self.oob_bound = oob_bound      # ([lo]*3, [hi]*3) or None (= no OOB test)
+        self.n_params = n_params        # name → number of parameter tensors
+
+
+def _fill_cfg(meta, grids, packed, dgrads, need_pts_grad):
+    cfg = _lib.NslamQueryCfg()
+    cfg.stage = _lib.STAGES[meta.stage]
+    cfg.need_pts_grad = int(bool(need_pts_grad))
+    if meta.oob_bound is None:
+        lo, hi = [-math.inf] * 3, [math.inf] * 3
+    else:
+        lo, hi = meta.oob_bound
+    for k in range(3):
+        cfg.bound_lo[k], cfg.bound_hi[k] = lo[k], hi[k]
+    for name in meta.decs:
+        d = _DEC_ID[name]
+        g, gg = grids[d]
+        cfg.grid[d].data = g.data_ptr()
+        cfg.grid[d].grad = gg.data_ptr() if gg is not None else None
+        cfg.grid[d].dims[0], cfg.grid[d].dims[1], cfg.grid[d].dims[2] = g.shape[2], g.shape[3], g.shape[4]
+        blo, bhi = meta.dec_bounds[name]
+        for k in range(3):
+            cfg.grid[d].lo[k], cfg.grid[d].hi[k] = blo[k], bhi[k]
+        cfg.packed[d] = packed[name].data_ptr()
+        cfg.dgrad[d] = meta.packers[name].grad_struct(dgrads.get(name))
+    # the fine decoder also reads the middle grid (no gradient through it)
+    if "fine" in meta.decs and "middle" not in meta.decs:
+        raise ValueError("fine stage needs the middle decoder/grid")
+    return cfg
+
+
+class _Query(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, meta, pts, g_coarse, g_middle, g_fine, g_color, *params):
+        pts = pts.detach().to(torch.float64).contiguous()
+        grids_in = (g_coarse, g_middle, g_fine, g_color)
+        grids = [channels_last(g.detach()) if g is not None else None for g in grids_in]
+        packed, off = {}, 0
+        for name in meta.decs:
+            n = meta.n_params[name]
+            packed[name] = meta.packers[name].pack(params[off:off + n])
+            off += n
+        raw = torch.empty(pts.shape[0], 4, dtype=torch.float32, device=pts.device)
+        cfg = _fill_cfg(meta, [(g, None) if g is not None else (None, None) for g in grids], packed, {}, False)
+        check(lib().nslam_query_fwd(ctypes.byref(cfg), ptr(pts), pts.shape[0], ptr(raw), stream_ptr(pts.device)),
+              "nslam_query_fwd")
+        ctx.meta = meta
+        ctx.packed = packed
+        ctx.grids = grids
+        ctx.save_for_backward(pts)
+        return raw
+
+    @staticmethod
+    def backward(ctx, g_raw):
+        meta = ctx.meta
+        (pts,) = ctx.saved_tensors
+        g_raw = g_raw.contiguous().float()
+        need = ctx.needs_input_grad
+        need_pts = bool(need[1])
+        grid_grads = [None] * 4
+        pairs = []
+        for d in range(4):
+            g = ctx.grids[d]
+            if g is not None and need[2 + d]:
+                grid_grads[d] = torch.zeros_like(g, memory_format=torch.channels_last_3d)
+            pairs.append((g, grid_grads[d]) if g is not None else (None, None))
+        dgrads, off, pidx = {}, 0, 6
+        for name in meta.decs:
+            n = meta.n_params[name]
+            if any(need[pidx + off + i] for i in range(n)):
+                dgrads[name] = torch.zeros(meta.packers[name].n_params, dtype=torch.float32, device=pts.device)
+            off += n
+        g_pts = torch.empty_like(pts) if need_pts else None
+        cfg = _fill_cfg(meta, pairs, ctx.packed, dgrads, need_pts)
+        check(lib().nslam_query_bwd(ctypes.byref(cfg), ptr(pts), pts.shape[0], ptr(g_raw), ptr(g_pts),
+                                    stream_ptr(pts.device)), "nslam_query_bwd")
+        out = [None, g_pts] + grid_grads
+        for name in meta.decs:
+            n = meta.n_params[name]
+            if name in dgrads:
+                out += meta.packers[name].split_grad(dgrads[name])
+            else:
+                out += [None] * n
+        return tuple(out)
+
+
+def query_points(nice, p, c_grid, stage, oob_bound=None):
+    """raw [P,4] for points p [P,3] (float64) — NICE.forward (+ eval_points' OOB rule)."""
+    if stage not in _DEC_FOR_STAGE:
+        raise ValueError(f"unknown stage {stage!r}")
+    decs = _DEC_FOR_STAGE[stage]
+    packers, bounds, nparams, params = {}, {}, {}, []
+    for name in decs:
+        dec = nice.decoder(name)
+        packers[name] = dec.packer()
+        bounds[name] = _bound_list(dec.bound)
+        plist = list(dec.parameters())
+        nparams[name] = len(plist)
+        params += plist
+    meta = QueryMeta(stage, decs, packers, bounds, None if oob_bound is None else _bound_list(oob_bound), nparams)
+    grids = []
+    for d, key in enumerate(_GRID_KEYS):
+        used = (d == _lib.DEC_COARSE and stage == "coarse") or (d == _lib.DEC_MIDDLE and stage != "coarse") or \
+               (d == _lib.DEC_FINE and stage in ("fine", "color")) or (d == _lib.DEC_COLOR and stage == "color")
+        grids.append(c_grid[key] if used else None)
+    p = p.reshape(-1, 3)
+    if p.dtype != torch.float64:
+        p = p.double()
+    return _Query.apply(meta, p, *grids, *params)
+
+
+# ----------------------------------------------------------------------------------------------
+# compositing
+# ----------------------------------------------------------------------------------------------
+class _Composite(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, raw, z):
+        raw = raw.detach().float().contiguous()
+        z = z.detach().double().contiguous()
+        n, s = z.shape
+        depth = torch.empty(n, dtype=torch.float64, device=raw.device)
+        var = torch.empty(n, dtype=torch.float64, device=raw.device)
+        color = torch.empty(n, 3, dtype=torch.float32, device=raw.device)
+        if n:
+            check(lib().nslam_composite_fwd(ptr(raw), ptr(z), n, s, ptr(depth), ptr(var), ptr(color),
+                                            stream_ptr(raw.device)), "nslam_composite_fwd")
+        ctx.save_for_backward(raw, z)
+        return depth, var, color
+
+    @staticmethod
+    def backward(ctx, gd, gv, gc):
+        raw, z = ctx.saved_tensors
+        n, s = z.shape
+        g_raw = torch.empty_like(raw)
+        if n:
+            gd = gd.contiguous().double() if gd is not None else None
+            gv = gv.contiguous().double() if gv is not None else None
+            gc = gc.contiguous().float() if gc is not None else None
+            check(lib().nslam_composite_bwd(ptr(raw), ptr(z), n, s, ptr(gd), ptr(gv), ptr(gc), ptr(g_raw),
+                                            stream_ptr(raw.device)), "nslam_composite_bwd")
+        return g_raw, None
+
+
+def composite(raw, z):
+    """(depth f64 [N], var f64 [N], color f32 [N,3]) from raw [N,S,4] f32, z [N,S] f64."""
+    return _Composite.apply(raw, z)
+
+
+# ----------------------------------------------------------------------------------------------
+# standalone trilinear lookup
+# ----------------------------------------------------------------------------------------------
+class _GridSample(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, grid, coords):
+        g = channels_last(grid.detach())
+        c = coords.detach().float().reshape(-1, 3).contiguous()
+        out = torch.empty(c.shape[0], 32, dtype=torch.float32, device=c.device)
+        dims = (ctypes.c_int32 * 3)(g.shape[2], g.shape[3], g.shape[4])
+        if c.shape[0]:
+            check(lib().nslam_grid_sample_fwd(ptr(g), dims, ptr(c), c.shape[0], ptr(out), stream_ptr(c.device)),
+                  "nslam_grid_sample_fwd")
+        ctx.save_for_backward(g, c)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        g, c = ctx.saved_tensors
+        gg = torch.zeros_like(g, memory_format=torch.channels_last_3d) if ctx.needs_input_grad[0] else None
+        gc = torch.empty_like(c) if ctx.needs_input_grad[1] else None
+        dims = (ctypes.c_int32 * 3)(g.shape[2], g.shape[3], g.shape[4])
+        if c.shape[0]:
+            check(lib().nslam_grid_sample_bwd(ptr(g), dims, ptr(c), c.shape[0], ptr(gout.contiguous().float()),
+                                              ptr(gg), ptr(gc), stream_ptr(c.device)), "nslam_grid_sample_bwd")
+        return gg, gc
+
+
+def grid_sample(grid, coords):
+    """[M,32] trilinear features of normalised coords [M,3] (x,y,z) — F.grid_sample semantics."""
+    return _GridSample.apply(grid, coords)

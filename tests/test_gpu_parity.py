@@ -1,0 +1,221 @@
+"""GPU parity of the HIP path against the reference's golden vectors and the oracle.
+
+Tolerances (measured fp32 noise floor of the reference itself):
+  forward  depth/var/color/raw : max-abs <= 2e-4 and rel-L2 <= 1e-4
+  backward (VJP, fixed cotangents) rel-L2 : <= 5e-3 grid_middle & ray/point grads,
+                                            <= 1e-3 grid_fine, <= 2e-4 grid_color/coarse & decoder params
+Every comparison is also written to gpurun_out/parity_report.json for diagnosis.
+"""
+import json
+import os
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import REPO, grids_from, rel_l2, sd_from
+from oracle import nslam_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+REPORT = {}
+FWD_ABS, FWD_REL = 2e-4, 1e-4
+
+
+def tol_for(name):
+    if name.startswith("grid_middle") or name in ("rays_o", "rays_d", "pts"):
+        return 5e-3
+    if name.startswith("grid_fine"):
+        return 1e-3
+    return 2e-4
+
+
+def record(case, name, got, ref):
+    got = got.detach().cpu().double().numpy() if torch.is_tensor(got) else np.asarray(got, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    e = {"rel_l2": rel_l2(got, ref), "max_abs": float(np.max(np.abs(got - ref))) if got.size else 0.0,
+         "ref_norm": float(np.linalg.norm(ref))}
+    REPORT.setdefault(case, {})[name] = e
+    return e
+
+
+@pytest.fixture(scope="module", autouse=True)
+def dump_report():
+    yield
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(REPO, "gpurun_out", "parity_report.json"), "w") as f:
+        json.dump(REPORT, f, indent=1, sort_keys=True)
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return torch.device("cuda:0")
+
+
+def make_nice(pkg, sd, bound, dev, lens=(2.0, 0.64, 0.32, 0.32)):
+    nice = pkg.NICE(dim=3, c_dim=32, coarse_grid_len=lens[0], middle_grid_len=lens[1], fine_grid_len=lens[2],
+                    color_grid_len=lens[3], hidden_size=32, coarse=True)
+    nice.load_state_dict({k: v.clone() for k, v in sd.items()})
+    nice.set_bound(bound)
+    return nice.to(dev)
+
+
+def make_renderer(pkg, bound, n_strat=32, n_surf=16):
+    cfg = {"rendering": {"N_samples": n_strat, "N_surface": n_surf, "N_importance": 0, "lindisp": False,
+                         "perturb": 0.0}, "scale": 1, "occupancy": True}
+    slam = SimpleNamespace(nice=True, bound=bound, H=680, W=1200, fx=600.0, fy=600.0, cx=599.5, cy=339.5)
+    return pkg.Renderer(cfg, None, slam)
+
+
+def dev_grids(tiny, dev):
+    return {k: v.to(dev).contiguous(memory_format=torch.channels_last_3d).requires_grad_(True)
+            for k, v in grids_from(tiny).items()}
+
+
+# ------------------------------------------------------------------------------------------------
+def test_grid_sample_matches_torch(pkg, dev):
+    torch.manual_seed(0)
+    grid = torch.randn(1, 32, 7, 9, 11, device=dev)
+    coords = torch.rand(5000, 3, device=dev) * 2.4 - 1.2
+    coords[:8] = torch.tensor([[-1, -1, -1], [1, 1, 1], [1, -1, 0.3], [0, 0, 0], [-1, 0.5, 1],
+                               [0.25, 0.5, 0.75], [1.0, 1.0, -1.0], [-0.5, -0.5, -0.5]], device=dev)
+    g1 = grid.clone().requires_grad_(True)
+    c1 = coords.clone().requires_grad_(True)
+    out = pkg.ops.grid_sample(g1.contiguous(memory_format=torch.channels_last_3d), c1)
+    g2 = grid.clone().requires_grad_(True)
+    c2 = coords.clone().requires_grad_(True)
+    ref = F.grid_sample(g2, c2.reshape(1, -1, 1, 1, 3), mode="bilinear", padding_mode="border",
+                        align_corners=True).reshape(32, -1).t()
+    e = record("grid_sample", "out", out, ref.detach().cpu())
+    assert e["max_abs"] < 1e-5
+    cot = torch.randn_like(ref)
+    ga, ca = torch.autograd.grad(out, (g1, c1), cot)
+    gb, cb = torch.autograd.grad(ref, (g2, c2), cot)
+    assert record("grid_sample", "grad_grid", ga, gb.cpu())["rel_l2"] < 1e-5
+    assert record("grid_sample", "grad_coords", ca, cb.cpu())["rel_l2"] < 1e-5
+
+
+def test_composite_matches_golden(pkg, dev, tiny):
+    raw = torch.from_numpy(tiny["composite.raw"]).to(dev).requires_grad_(True)
+    z = torch.from_numpy(tiny["composite.z"]).to(dev)
+    d, v, c = pkg.ops.composite(raw, z)
+    ok = record("composite", "depth", d, tiny["composite.depth"])["max_abs"] < 1e-9
+    ok &= record("composite", "var", v, tiny["composite.var"])["max_abs"] < 1e-9
+    ok &= record("composite", "rgb", c, tiny["composite.rgb"])["max_abs"] < 1e-6
+    cots = [torch.from_numpy(tiny["composite." + k]).to(dev) for k in ("cot_depth", "cot_var", "cot_color")]
+    (g,) = torch.autograd.grad((d, v, c), (raw,), cots)
+    ok &= record("composite", "grad_raw", g, tiny["composite.grad.raw"])["rel_l2"] < 1e-5
+    assert ok, REPORT["composite"]
+
+
+@pytest.mark.parametrize("with_gt", [True, False])
+def test_sampler_bitexact_vs_oracle(pkg, dev, tiny, with_gt):
+    bound = torch.from_numpy(tiny["bound"])
+    ro = torch.from_numpy(tiny["rays_o"])
+    rd = torch.from_numpy(tiny["rays_d"])
+    gt = torch.from_numpy(tiny["gt_depth"]) if with_gt else None
+    ref = orc.sample_z(ro, rd, gt, bound, 32, 16)
+    z = pkg.ops.sample_z(ro.to(dev), rd.to(dev), gt.to(dev) if gt is not None else None, bound, 32, 16)
+    record("sampler", f"z_gt{with_gt}", z, ref)
+    np.testing.assert_array_equal(z.cpu().numpy(), ref.numpy())
+
+
+@pytest.mark.parametrize("stage", ["coarse", "middle", "fine", "color"])
+def test_eval_points_matches_golden(pkg, dev, tiny, stage):
+    bound = torch.from_numpy(tiny["bound"])
+    nice = make_nice(pkg, sd_from(tiny), bound, dev)
+    r = make_renderer(pkg, bound)
+    grids = dev_grids(tiny, dev)
+    pre = f"eval.{stage}."
+    p = torch.from_numpy(tiny[pre + "pts"]).to(dev).requires_grad_(True)
+    raw = r.eval_points(p, nice, grids, stage, dev)
+    case = "eval." + stage
+    e = record(case, "raw", raw, tiny[pre + "raw"])
+    ok = e["max_abs"] <= FWD_ABS and e["rel_l2"] <= FWD_REL
+    params = dict(nice.named_parameters())
+    names = ["pts"] + list(grids) + list(params)
+    tens = [p] + list(grids.values()) + list(params.values())
+    grads = torch.autograd.grad(raw, tens, torch.from_numpy(tiny[pre + "cot_raw"]).to(dev), allow_unused=True)
+    for name, g in zip(names, grads):
+        key = pre + "grad." + name
+        if key not in tiny:
+            ok &= g is None or float(g.abs().max()) == 0.0
+            continue
+        if g is None:
+            REPORT[case][name] = "missing"
+            ok = False
+            continue
+        ok &= record(case, name, g, tiny[key])["rel_l2"] <= tol_for(name)
+    assert ok, json.dumps(REPORT[case], indent=1)
+
+
+@pytest.mark.parametrize("stage", ["coarse", "middle", "fine", "color", "color_nogt"])
+def test_render_batch_ray_matches_golden(pkg, dev, tiny, stage):
+    bound = torch.from_numpy(tiny["bound"])
+    nice = make_nice(pkg, sd_from(tiny), bound, dev)
+    r = make_renderer(pkg, bound)
+    grids = dev_grids(tiny, dev)
+    ro = torch.from_numpy(tiny["rays_o"]).to(dev).requires_grad_(True)
+    rd = torch.from_numpy(tiny["rays_d"]).to(dev).requires_grad_(True)
+    gt = None if stage == "color_nogt" else torch.from_numpy(tiny["gt_depth"]).to(dev)
+    st = "color" if stage == "color_nogt" else stage
+    depth, var, color = r.render_batch_ray(grids, nice, rd, ro, dev, st, gt_depth=gt)
+    pre = f"render.{stage}."
+    case = "render." + stage
+    ok = True
+    for nm, t in (("depth", depth), ("var", var), ("color", color)):
+        e = record(case, nm, t, tiny[pre + nm])
+        ok &= e["max_abs"] <= FWD_ABS and e["rel_l2"] <= FWD_REL
+    cots = tuple(torch.from_numpy(tiny[pre + k]).to(dev) for k in ("cot_depth", "cot_var", "cot_color"))
+    params = dict(nice.named_parameters())
+    names = list(grids) + ["rays_o", "rays_d"] + list(params)
+    tens = list(grids.values()) + [ro, rd] + list(params.values())
+    grads = torch.autograd.grad((depth, var, color), tens, cots, allow_unused=True)
+    for name, g in zip(names, grads):
+        key = pre + "grad." + name
+        if key not in tiny:
+            ok &= g is None or float(g.abs().max()) == 0.0
+            continue
+        if g is None:
+            REPORT[case][name] = "missing"
+            ok = False
+            continue
+        ok &= record(case, name, g, tiny[key])["rel_l2"] <= tol_for(name)
+    assert ok, json.dumps(REPORT[case], indent=1)
+
+
+def test_room0_color_stage_matches_golden(pkg, dev, room0):
+    gen = torch.Generator().manual_seed(7)
+    bound = orc.enlarge_bound([[-2.9, 8.9], [-3.2, 5.5], [-3.5, 3.3]], 0.32)
+    lens = {"coarse": 2.0, "middle": 0.32, "fine": 0.16, "color": 0.16}
+    grids = orc.make_grids(bound, lens, gen=gen)
+    sd = orc.init_decoders(gen)
+    nice = make_nice(pkg, sd, bound, dev, lens=(2.0, 0.32, 0.16, 0.16))
+    r = make_renderer(pkg, bound)
+    g = {k: v.to(dev).contiguous(memory_format=torch.channels_last_3d).requires_grad_(True) for k, v in grids.items()}
+    ro = torch.from_numpy(room0["rays_o"]).to(dev).requires_grad_(True)
+    rd = torch.from_numpy(room0["rays_d"]).to(dev).requires_grad_(True)
+    gt = torch.from_numpy(room0["gt_depth"]).to(dev)
+    depth, var, color = r.render_batch_ray(g, nice, rd, ro, dev, "color", gt_depth=gt)
+    ok = True
+    for nm, t in (("depth", depth), ("var", var), ("color", color)):
+        e = record("room0", nm, t, room0[nm])
+        ok &= e["max_abs"] <= FWD_ABS and e["rel_l2"] <= FWD_REL
+    cots = tuple(torch.from_numpy(room0[k]).to(dev) for k in ("cot_depth", "cot_var", "cot_color"))
+    params = dict(nice.named_parameters())
+    names = list(g) + ["rays_o", "rays_d"] + list(params)
+    grads = torch.autograd.grad((depth, var, color), list(g.values()) + [ro, rd] + list(params.values()), cots,
+                                allow_unused=True)
+    for name, gg in zip(names, grads):
+        if name in ("rays_o", "rays_d"):
+            ok &= record("room0", name, gg, room0["grad." + name])["rel_l2"] <= tol_for(name)
+        elif "norm.grad." + name in room0:
+            nrm = float(gg.double().norm()) if gg is not None else 0.0
+            ref = float(room0["norm.grad." + name])
+            rel = abs(nrm - ref) / max(ref, 1e-30)
+            REPORT["room0"][name + ".norm"] = {"got": nrm, "ref": ref, "rel": rel}
+            ok &= rel <= max(tol_for(name), 1e-4)
+    assert ok, json.dumps(REPORT["room0"], indent=1)
