@@ -1,0 +1,296 @@
+"""bench.py — ray-samples/s (fwd+bwd) of one NICE-SLAM mapping iteration, Replica room0 shape.
+
+python bench.py [--gpus N --steps K --warmup W]   (N>1: launched by torch.distributed.run)
+
+One step = one colour-stage mapping iteration of Mapper.optimize_map (src/Mapper.py:391-519) on
+synthetic room0 data resident in HBM (configs/Replica/room0.yaml bound, replica.yaml camera,
+mapping.pixels=1000 over a 5-frame window, 32 stratified + 16 surface samples):
+  pixel sampling + rays (5 frames × 200) → inside-mask prefilter → sampler kernel → fused
+  query kernel (middle+fine+colour decoders, 3 grid lookups) → compositing kernel → mapping loss →
+  backward (compositing bwd + 3 fused decoder bwd launches: grid-gradient atomics + colour-decoder
+  weight gradients) → [N>1: RCCL all-reduce of the gradients] → Adam step on grids + colour decoder.
+Weak scaling: every rank maps its own 1000 rays; value = all ranks' ray-samples / max rank time.
+"""
+import argparse
+import importlib
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+# configs/Replica/room0.yaml:3, configs/Replica/replica.yaml cam + mapping, configs/nice_slam.yaml
+ROOM0 = {
+    "bound": [[-2.9, 8.9], [-3.2, 5.5], [-3.5, 3.3]], "bound_divisible": 0.32,
+    "grid_len": {"coarse": 2.0, "middle": 0.32, "fine": 0.16, "color": 0.16},
+    "H": 680, "W": 1200, "fx": 600.0, "fy": 600.0, "cx": 599.5, "cy": 339.5,
+    "pixels": 1000, "window": 5, "n_strat": 32, "n_surf": 16, "w_color": 0.2,
+    "lr": {"decoders": 0.005, "middle": 0.005, "fine": 0.005, "color": 0.005},
+}
+FLOP_FWD_PER_SAMPLE = 2 * (15479 + 20599 + 15575)   # SURVEY §8(a10) MACs, colour stage
+BYTES_FWD_PER_SAMPLE = 3 * 1024                      # 3 trilinear lookups × 8 corners × 128 B
+F32_PEAK_TFLOPS = 157.3                              # MI355X dense fp32 (MFMA = VALU rate)
+HBM_PEAK_GBS = 8000.0
+
+
+def pkg():
+    return importlib.import_module("nice-slam_amd")
+
+
+def enlarge_bound(cfg):
+    """src/NICE_SLAM.py:145-150 (float32-rounded upper end)."""
+    b = torch.tensor(cfg["bound"], dtype=torch.float64)
+    cells = ((b[:, 1] - b[:, 0]) / cfg["bound_divisible"]).int() + 1
+    b[:, 1] = (cells.float() * torch.tensor(cfg["bound_divisible"], dtype=torch.float32)).double() + b[:, 0]
+    return b
+
+
+def grid_shape(bound, glen):
+    ext = bound[:, 1] - bound[:, 0]
+    xyz = [int(v) for v in (ext / glen).tolist()]
+    return [1, 32, xyz[2], xyz[1], xyz[0]]
+
+
+def rot(yaw, pitch):
+    cy, sy, cp, sp = math.cos(yaw), math.sin(yaw), math.cos(pitch), math.sin(pitch)
+    Rz = torch.tensor([[cy, -sy, 0], [sy, cy, 0], [0, 0, 1]], dtype=torch.float64)
+    Rx = torch.tensor([[1, 0, 0], [0, cp, -sp], [0, sp, cp]], dtype=torch.float64)
+    return Rz @ Rx
+
+
+class Room0Scene:
+    """Synthetic room0-shaped mapping workload (grids, decoders, 5 keyframes in HBM)."""
+
+    def __init__(self, dev, rank=0, cfg=ROOM0):
+        P = pkg()
+        self.cfg, self.dev = cfg, dev
+        g = torch.Generator().manual_seed(2)
+        self.bound = enlarge_bound(cfg)
+        std = {"middle": 0.01, "fine": 1e-4, "color": 0.01}
+        self.grids = {}
+        for k in ("middle", "fine", "color"):
+            t = torch.randn(grid_shape(self.bound, cfg["grid_len"][k]), generator=g) * std[k]
+            self.grids["grid_" + k] = t.to(dev).contiguous(memory_format=torch.channels_last_3d).requires_grad_(True)
+        torch.manual_seed(3)
+        self.nice = P.NICE(c_dim=32, coarse_grid_len=2.0, middle_grid_len=0.32, fine_grid_len=0.16,
+                           color_grid_len=0.16, hidden_size=32, coarse=False)
+        self.nice.set_bound(self.bound)
+        self.nice = self.nice.to(dev)
+        for d in (self.nice.middle_decoder, self.nice.fine_decoder):  # fix_fine; middle never optimised
+            d.requires_grad_(False)
+        self.renderer = P.Renderer({"rendering": {"N_samples": cfg["n_strat"], "N_surface": cfg["n_surf"],
+                                                  "N_importance": 0, "lindisp": False, "perturb": 0.0},
+                                    "occupancy": True}, None, _Slam(self.bound, cfg))
+        # keyframes: poses at the room centre, seeded yaw/pitch; analytic depth to an inner box
+        gk = torch.Generator().manual_seed(0)
+        F = cfg["window"]
+        ctr = self.bound.mean(1)
+        self.c2w = torch.zeros(F, 3, 4, dtype=torch.float32)
+        for f in range(F):
+            yaw = float(torch.rand(1, generator=gk)) * 2 * math.pi
+            pitch = (float(torch.rand(1, generator=gk)) - 0.5) * 0.6 + math.pi / 2
+            self.c2w[f, :, :3] = rot(yaw, pitch).float()
+            self.c2w[f, :, 3] = (ctr + (torch.rand(3, generator=gk, dtype=torch.float64) - 0.5) * 0.5).float()
+        self.c2w = self.c2w.to(dev)
+        H, W = cfg["H"], cfg["W"]
+        jj, ii = torch.meshgrid(torch.arange(H, device=dev, dtype=torch.float32),
+                                torch.arange(W, device=dev, dtype=torch.float32), indexing="ij")
+        dirs = torch.stack([(ii - cfg["cx"]) / cfg["fx"], -(jj - cfg["cy"]) / cfg["fy"], -torch.ones_like(ii)], -1)
+        inner = self.bound.clone()
+        inner[:, 0] += 0.1 * (self.bound[:, 1] - self.bound[:, 0])
+        inner[:, 1] -= 0.1 * (self.bound[:, 1] - self.bound[:, 0])
+        inner = inner.to(dev)
+        self.depth = torch.empty(F, H, W, device=dev)
+        gd = torch.Generator(device=dev).manual_seed(1)
+        for f in range(F):
+            rd = (dirs.reshape(-1, 1, 3) * self.c2w[f, :, :3]).sum(-1).double()
+            ro = self.c2w[f, :, 3].double().expand_as(rd)
+            t = (inner[None] - ro[:, :, None]) / rd[:, :, None]
+            d = t.max(2).values.min(1).values.float()
+            d = d * (0.9 + 0.1 * torch.rand(d.shape, device=dev, generator=gd))
+            d[torch.rand(d.shape, device=dev, generator=gd) < 0.05] = 0.0
+            self.depth[f] = d.reshape(H, W)
+        self.color = torch.rand(F, H, W, 3, device=dev, generator=gd)
+        self.dirs = dirs.reshape(-1, 3)
+        self.pix_gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+        params = [{"params": list(self.nice.color_decoder.parameters()), "lr": cfg["lr"]["decoders"]},
+                  {"params": [self.grids["grid_middle"]], "lr": cfg["lr"]["middle"]},
+                  {"params": [self.grids["grid_fine"]], "lr": cfg["lr"]["fine"]},
+                  {"params": [self.grids["grid_color"]], "lr": cfg["lr"]["color"]}]
+        self.opt = torch.optim.Adam(params, fused=True)
+        self.bound_dev = self.bound.to(dev)
+
+    def sample_batch(self):
+        """get_samples over the window (Mapper.py:437-467): 200 random pixels per frame."""
+        cfg = self.cfg
+        F, H, W = cfg["window"], cfg["H"], cfg["W"]
+        n = cfg["pixels"] // F
+        idx = torch.randint(H * W, (F, n), device=self.dev, generator=self.pix_gen)
+        depth = torch.gather(self.depth.reshape(F, -1), 1, idx).reshape(-1)
+        color = torch.gather(self.color.reshape(F, -1, 3), 1, idx[..., None].expand(F, n, 3)).reshape(-1, 3)
+        d = self.dirs[idx]                                              # [F, n, 3]
+        rays_d = torch.einsum("fnk,fjk->fnj", d, self.c2w[:, :, :3]).reshape(-1, 3)
+        rays_o = self.c2w[:, None, :, 3].expand(F, n, 3).reshape(-1, 3)
+        return rays_o, rays_d, depth, color
+
+    def step(self, stage="color", allreduce=None):
+        cfg = self.cfg
+        self.opt.zero_grad(set_to_none=False)
+        rays_o, rays_d, gt_depth, gt_color = self.sample_batch()
+        with torch.no_grad():  # inside-mask prefilter (Mapper.py:469-481)
+            t = (self.bound_dev[None] - rays_o[..., None].double()) / rays_d[..., None].double()
+            keep = t.max(2).values.min(1).values >= gt_depth
+        rays_o, rays_d, gt_depth, gt_color = rays_o[keep], rays_d[keep], gt_depth[keep], gt_color[keep]
+        depth, unc, color = self.renderer.render_batch_ray(self.grids, self.nice, rays_d, rays_o, self.dev, stage,
+                                                           gt_depth=gt_depth)
+        m = gt_depth > 0
+        loss = torch.abs(gt_depth[m] - depth[m]).sum()
+        if stage == "color":
+            loss = loss + cfg["w_color"] * torch.abs(gt_color - color).sum()
+        loss.backward()
+        if allreduce is not None:
+            allreduce(self)
+        self.opt.step()
+        return rays_o.shape[0] * (cfg["n_strat"] + cfg["n_surf"])
+
+
+class _Slam:
+    def __init__(self, bound, cfg):
+        self.nice, self.bound = True, bound
+        self.H, self.W, self.fx, self.fy, self.cx, self.cy = cfg["H"], cfg["W"], cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"]
+
+
+def allreduce_grads(scene):
+    """Sum the gradients of every optimised tensor over the ranks (RCCL over xGMI)."""
+    ts = [p.grad for grp in scene.opt.param_groups for p in grp["params"] if p.grad is not None]
+    big = [t for t in ts if t.numel() > 1 << 16]
+    small = [t for t in ts if t.numel() <= 1 << 16]
+    for t in big:
+        dist.all_reduce(t)
+    if small:
+        flat = torch.cat([t.reshape(-1) for t in small])
+        dist.all_reduce(flat)
+        off = 0
+        for t in small:
+            t.copy_(flat[off:off + t.numel()].view_as(t))
+            off += t.numel()
+
+
+def cpu_baseline(scene, budget_s=20.0):
+    """The oracle (torch CPU restatement, oracle/nslam_oracle.py) on the same workload, host cores."""
+    from oracle import nslam_oracle as orc
+    threads = torch.get_num_threads()
+    bound = scene.bound
+    grids = {k: v.detach().cpu().contiguous().requires_grad_(True) for k, v in scene.grids.items()}
+    sd = {k: v.detach().cpu() for k, v in scene.nice.state_dict().items()}
+    for k in list(sd):
+        if k.startswith("color_decoder."):
+            sd[k] = sd[k].clone().requires_grad_(True)
+    opt = torch.optim.Adam([v for k, v in sd.items() if v.requires_grad] + list(grids.values()), lr=0.005)
+    samples, iters, t0 = 0, 0, time.perf_counter()
+    while iters < 2 or (time.perf_counter() - t0 < budget_s and iters < 50):
+        ro, rd, gt, gc = (x.cpu() for x in scene.sample_batch())
+        keep = orc.inside_mask(ro, rd, gt, bound)
+        ro, rd, gt, gc = ro[keep], rd[keep], gt[keep], gc[keep]
+        if iters == 0:
+            t0 = time.perf_counter()  # first iteration = warm-up
+        opt.zero_grad()
+        d, v, c = orc.render_batch_ray(sd, grids, rd, ro, "color", bound, gt)
+        orc.mapper_loss(d, c, gt, gc, "color").backward()
+        opt.step()
+        if iters > 0:
+            samples += ro.shape[0] * 48
+        iters += 1
+    dt = time.perf_counter() - t0
+    return {"value": samples / dt, "unit": "ray-samples/s", "cores": threads, "kind": "port",
+            "sample": f"{iters - 1} colour-stage mapping iterations (1000 rays x 48 samples, fwd+bwd+Adam) after "
+                      f"1 warm-up, oracle/nslam_oracle.py on {threads} host threads, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    P = pkg()
+    scene = Room0Scene(dev, rank)
+    ar = allreduce_grads if world > 1 else None
+    for _ in range(args.warmup):
+        scene.step(allreduce=ar)
+    torch.cuda.synchronize()
+    P.ops.TIMER = P.ops.KernelTimer()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    samples = 0
+    for _ in range(args.steps):
+        samples += scene.step(allreduce=ar)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    timers = P.ops.TIMER.summary()
+    P.ops.TIMER = None
+    tot = torch.tensor([samples, dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        s = tot[:1].clone()
+        dist.all_reduce(s)
+        m = tot[1:].clone()
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        samples_all, dt_max = float(s), float(m)
+    else:
+        samples_all, dt_max = float(samples), dt
+    if rank == 0:
+        pts_per_step = samples / args.steps
+        qf = timers.get("query_fwd", {"avg_ms": float("nan")})
+        qb = timers.get("query_bwd", {"avg_ms": float("nan")})
+        dom_name, dom = max(((k, v) for k, v in timers.items()), key=lambda kv: kv[1]["total_ms"])
+        if dom_name == "query_bwd":
+            flops = pts_per_step * 2 * FLOP_FWD_PER_SAMPLE  # algorithmic minimum ≈ 2× fwd MACs
+        else:
+            flops = pts_per_step * FLOP_FWD_PER_SAMPLE
+        achieved = flops / (dom["avg_ms"] * 1e-3) / 1e12
+        out = {
+            "metric": "ray-samples/sec (fwd+bwd) per mapping iter; frames/sec on Replica room0",
+            "value": samples_all / dt_max, "unit": "ray-samples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt_max / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32 (z, depth, var in f64)",
+            "data": "synthetic room0-shaped frames (analytic depth, random colour), seeded random-init decoders",
+            "config": {"workload": "Replica room0 mapping iteration, colour stage: 1000 pixels x 48 samples "
+                                   "(5-frame window x 200), grids middle/fine/colour, Adam",
+                       "global_batch": int(round(pts_per_step)) * world, "seq_len": 48,
+                       "parallelism": f"rays sharded dp{world}, RCCL all-reduce of gradients"},
+            "roofline": {"kernel": dom_name, "bound": "mfma", "achieved": achieved, "peak": F32_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": achieved / F32_PEAK_TFLOPS, "traffic": None,
+                         "avg_launch_ms": dom["avg_ms"],
+                         "note": "fp32 MFMA (v_mfma_f32_32x32x2_f32); algorithmic FLOPs per ray-sample "
+                                 f"{FLOP_FWD_PER_SAMPLE} fwd / {2 * FLOP_FWD_PER_SAMPLE} bwd"},
+            "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in timers.items()},
+            "query_fwd_hbm_frac": (pts_per_step * BYTES_FWD_PER_SAMPLE / (qf["avg_ms"] * 1e-3) / 1e9) / HBM_PEAK_GBS,
+            "query_bwd_ms": qb["avg_ms"],
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(scene)
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

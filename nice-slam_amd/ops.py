@@ -15,6 +15,60 @@ import torch
 from . import _lib
 from ._lib import check, lib, ptr, stream_ptr
 
+class KernelTimer:
+    """Optional live timing of the C-ABI launches with HIP events on the launching stream.
+
+    ops.TIMER = KernelTimer() turns it on (bench.py does, for the timed region only); each entry
+    point records an event pair around its launches; summary() synchronises and averages.
+    """
+
+    def __init__(self):
+        self.events = {}
+
+    def span(self, name):
+        return _Span(self, name)
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, pairs in self.events.items():
+            ms = [a.elapsed_time(b) for a, b in pairs]
+            out[name] = {"calls": len(ms), "avg_ms": sum(ms) / max(len(ms), 1), "total_ms": sum(ms)}
+        return out
+
+
+class _Span:
+    def __init__(self, timer, name):
+        self.timer, self.name = timer, name
+
+    def __enter__(self):
+        self.a = torch.cuda.Event(enable_timing=True)
+        self.a.record()
+        return self
+
+    def __exit__(self, *exc):
+        b = torch.cuda.Event(enable_timing=True)
+        b.record()
+        self.timer.events.setdefault(self.name, []).append((self.a, b))
+        return False
+
+
+class _NoSpan:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+TIMER = None
+_NOSPAN = _NoSpan()
+
+
+def _span(name):
+    return TIMER.span(name) if TIMER is not None else _NOSPAN
+
+
 _DEC_FOR_STAGE = {
     "coarse": ("coarse",),
     "middle": ("middle",),
@@ -71,9 +125,10 @@ def sample_z(rays_o, rays_d, gt_depth, bound, n_strat, n_surf, lindisp=False):
     L = lib()
     wsb = L.nslam_workspace_size(0, n)
     ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=ro.device)
-    rc = L.nslam_sample_rays(ptr(ro), ptr(rd), ptr(gt), n, (ctypes.c_double * 3)(*lo), (ctypes.c_double * 3)(*hi),
-                             ptr(ts), n_strat, ptr(tu), s1, int(bool(lindisp)), ptr(z), ptr(ws), wsb,
-                             stream_ptr(ro.device))
+    with _span("sample_rays"):
+        rc = L.nslam_sample_rays(ptr(ro), ptr(rd), ptr(gt), n, (ctypes.c_double * 3)(*lo),
+                                 (ctypes.c_double * 3)(*hi), ptr(ts), n_strat, ptr(tu), s1, int(bool(lindisp)),
+                                 ptr(z), ptr(ws), wsb, stream_ptr(ro.device))
     check(rc, "nslam_sample_rays")
     return z
 
@@ -133,8 +188,9 @@ class _Query(torch.autograd.Function):
             off += n
         raw = torch.empty(pts.shape[0], 4, dtype=torch.float32, device=pts.device)
         cfg = _fill_cfg(meta, [(g, None) if g is not None else (None, None) for g in grids], packed, {}, False)
-        check(lib().nslam_query_fwd(ctypes.byref(cfg), ptr(pts), pts.shape[0], ptr(raw), stream_ptr(pts.device)),
-              "nslam_query_fwd")
+        with _span("query_fwd"):
+            rc = lib().nslam_query_fwd(ctypes.byref(cfg), ptr(pts), pts.shape[0], ptr(raw), stream_ptr(pts.device))
+        check(rc, "nslam_query_fwd")
         ctx.meta = meta
         ctx.packed = packed
         ctx.grids = grids
@@ -163,8 +219,10 @@ class _Query(torch.autograd.Function):
             off += n
         g_pts = torch.empty_like(pts) if need_pts else None
         cfg = _fill_cfg(meta, pairs, ctx.packed, dgrads, need_pts)
-        check(lib().nslam_query_bwd(ctypes.byref(cfg), ptr(pts), pts.shape[0], ptr(g_raw), ptr(g_pts),
-                                    stream_ptr(pts.device)), "nslam_query_bwd")
+        with _span("query_bwd"):
+            rc = lib().nslam_query_bwd(ctypes.byref(cfg), ptr(pts), pts.shape[0], ptr(g_raw), ptr(g_pts),
+                                       stream_ptr(pts.device))
+        check(rc, "nslam_query_bwd")
         out = [None, g_pts] + grid_grads
         for name in meta.decs:
             n = meta.n_params[name]
@@ -213,8 +271,10 @@ class _Composite(torch.autograd.Function):
         var = torch.empty(n, dtype=torch.float64, device=raw.device)
         color = torch.empty(n, 3, dtype=torch.float32, device=raw.device)
         if n:
-            check(lib().nslam_composite_fwd(ptr(raw), ptr(z), n, s, ptr(depth), ptr(var), ptr(color),
-                                            stream_ptr(raw.device)), "nslam_composite_fwd")
+            with _span("composite_fwd"):
+                rc = lib().nslam_composite_fwd(ptr(raw), ptr(z), n, s, ptr(depth), ptr(var), ptr(color),
+                                               stream_ptr(raw.device))
+            check(rc, "nslam_composite_fwd")
         ctx.save_for_backward(raw, z)
         return depth, var, color
 
@@ -227,8 +287,10 @@ class _Composite(torch.autograd.Function):
             gd = gd.contiguous().double() if gd is not None else None
             gv = gv.contiguous().double() if gv is not None else None
             gc = gc.contiguous().float() if gc is not None else None
-            check(lib().nslam_composite_bwd(ptr(raw), ptr(z), n, s, ptr(gd), ptr(gv), ptr(gc), ptr(g_raw),
-                                            stream_ptr(raw.device)), "nslam_composite_bwd")
+            with _span("composite_bwd"):
+                rc = lib().nslam_composite_bwd(ptr(raw), ptr(z), n, s, ptr(gd), ptr(gv), ptr(gc), ptr(g_raw),
+                                               stream_ptr(raw.device))
+            check(rc, "nslam_composite_bwd")
         return g_raw, None
 
 
