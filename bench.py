@@ -141,7 +141,7 @@ class Room0Scene:
 
     def step(self, stage="color", allreduce=None):
         cfg = self.cfg
-        self.opt.zero_grad(set_to_none=False)
+        self.opt.zero_grad(set_to_none=True)
         rays_o, rays_d, gt_depth, gt_color = self.sample_batch()
         with torch.no_grad():  # inside-mask prefilter (Mapper.py:469-481)
             t = (self.bound_dev[None] - rays_o[..., None].double()) / rays_d[..., None].double()

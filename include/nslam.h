@@ -63,6 +63,7 @@ typedef struct nslam_dec_grad {
   int64_t wc[5], bc[5]; /* fc_c.i.weight / .bias (unused for the coarse MLP)  */
   int64_t wo, bo;       /* output_linear.weight / .bias                       */
   int64_t B;            /* embedder._B [3][93] (unused for the coarse MLP)    */
+  int64_t count;        /* floats in the flat buffer (all parameters)         */
 } nslam_dec_grad;
 
 /* Point query: NICE.forward + Renderer.eval_points
@@ -100,10 +101,13 @@ int nslam_sample_rays(const float* rays_o, const float* rays_d, const float* gt_
 int nslam_query_fwd(const nslam_query_cfg* cfg, const double* pts, int64_t n_pts, float* raw, void* stream);
 
 /* Backward of nslam_query_fwd for cotangent g_raw[M][4]: accumulates grid gradients into
- * cfg->grid[i].grad (atomics, caller zero-initialises), parameter gradients into cfg->dgrad[i]
- * (atomics, caller zero-initialises) and writes g_pts[M][3] float64 when cfg->need_pts_grad. */
+ * cfg->grid[i].grad (atomics, caller zero-initialises), adds parameter gradients into
+ * cfg->dgrad[i] (per-workgroup LDS accumulation → partial slabs in `ws` → deterministic
+ * reduction) and writes g_pts[M][3] float64 when cfg->need_pts_grad.
+ * ws must hold nslam_query_bwd_workspace_size(cfg, n_pts) bytes (0 when no parameter grads). */
 int nslam_query_bwd(const nslam_query_cfg* cfg, const double* pts, int64_t n_pts, const float* g_raw,
-                    double* g_pts, void* stream);
+                    double* g_pts, void* ws, size_t ws_bytes, void* stream);
+size_t nslam_query_bwd_workspace_size(const nslam_query_cfg* cfg, int64_t n_pts);
 
 /* ---- compositing: raw2outputs_nerf_color, src/common.py:204-245 (occupancy mode) ------------ */
 int nslam_composite_fwd(const float* raw, const double* z_vals, int64_t n_rays, int32_t n_samples,
@@ -119,7 +123,8 @@ int nslam_composite_bwd(const float* raw, const double* z_vals, int64_t n_rays, 
  * coords[M][3] float32 normalised (x,y,z in [-1,1]); out[M][32]. */
 int nslam_grid_sample_fwd(const float* grid, const int32_t* dims, const float* coords, int64_t n,
                           float* out, void* stream);
-/* grad_grid (atomics, may be NULL) and grad_coords[M][3] (may be NULL) from grad_out[M][32]. */
+/* grad_grid (atomics, may be NULL) and grad_coords[M][3] (may be NULL) from grad_out[M][32].
+ * `dims` (Z, Y, X) is a HOST pointer in both grid_sample entry points. */
 int nslam_grid_sample_bwd(const float* grid, const int32_t* dims, const float* coords, int64_t n,
                           const float* grad_out, float* grad_grid, float* grad_coords, void* stream);
 

@@ -14,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libnslam.so")
 
 NSLAM_OK = 0
+ABI_VERSION = 2
 STAGES = {"coarse": 0, "middle": 1, "fine": 2, "color": 3}
 DEC_COARSE, DEC_MIDDLE, DEC_FINE, DEC_COLOR = 0, 1, 2, 3
 
@@ -41,6 +42,7 @@ class NslamDecGrad(ctypes.Structure):
         ("wo", ctypes.c_int64),
         ("bo", ctypes.c_int64),
         ("B", ctypes.c_int64),
+        ("count", ctypes.c_int64),
     ]
 
 
@@ -58,7 +60,7 @@ class NslamQueryCfg(ctypes.Structure):
 
 # every symbol include/nslam.h declares (tests check that the library exports all of them)
 EXPORTS = (
-    "nslam_pack_layout", "nslam_sample_rays", "nslam_query_fwd", "nslam_query_bwd",
+    "nslam_pack_layout", "nslam_sample_rays", "nslam_query_fwd", "nslam_query_bwd", "nslam_query_bwd_workspace_size",
     "nslam_composite_fwd", "nslam_composite_bwd", "nslam_grid_sample_fwd", "nslam_grid_sample_bwd",
     "nslam_workspace_size", "nslam_strerror", "nslam_abi_version",
 )
@@ -79,7 +81,9 @@ def lib():
         L.nslam_pack_layout.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int32), ctypes.c_int]
         L.nslam_sample_rays.argtypes = [vp, vp, vp, i64, dp, dp, vp, i32, vp, i32, i32, vp, vp, sz, vp]
         L.nslam_query_fwd.argtypes = [ctypes.POINTER(NslamQueryCfg), vp, i64, vp, vp]
-        L.nslam_query_bwd.argtypes = [ctypes.POINTER(NslamQueryCfg), vp, i64, vp, vp, vp]
+        L.nslam_query_bwd.argtypes = [ctypes.POINTER(NslamQueryCfg), vp, i64, vp, vp, vp, sz, vp]
+        L.nslam_query_bwd_workspace_size.argtypes = [ctypes.POINTER(NslamQueryCfg), i64]
+        L.nslam_query_bwd_workspace_size.restype = sz
         L.nslam_composite_fwd.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp]
         L.nslam_composite_bwd.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, vp]
         L.nslam_grid_sample_fwd.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), vp, i64, vp, vp]
@@ -89,6 +93,8 @@ def lib():
         L.nslam_strerror.argtypes = [ctypes.c_int]
         L.nslam_strerror.restype = ctypes.c_char_p
         L.nslam_abi_version.restype = ctypes.c_int
+        if L.nslam_abi_version() != ABI_VERSION:
+            raise RuntimeError(f"libnslam.so ABI {L.nslam_abi_version()} != {ABI_VERSION}: rebuild it")
         _lib = L
     return _lib
 

@@ -96,7 +96,9 @@ struct Scratch {
   float* cw;    // [32][8]
 };
 
-__device__ __forceinline__ void lds_sync() { __syncthreads(); }
+// Scratch is wave-private: ordering LDS writes before other lanes' reads of the same wave needs
+// only the wave's own LDS counter drained (and a compiler memory barrier), not a workgroup barrier.
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // dW[o][kofs + k] += sum_p sA[p][o] * sX[p][k]   for k < kvalid
 __device__ __forceinline__ void dw_block(float* __restrict__ dst, int ldk, int kofs, int kvalid, const Scratch& S,
@@ -107,7 +109,7 @@ __device__ __forceinline__ void dw_block(float* __restrict__ dst, int ldk, int k
   for (int s = 0; s < 16; ++s) acc = mfma32(S.sA[(2 * s + h) * TPITCH + j], S.sX[(2 * s + h) * TPITCH + j], acc);
   if (j < kvalid) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) unsafeAtomicAdd(dst + fidx(r, h) * ldk + kofs + j, acc[r]);
+    for (int r = 0; r < 16; ++r) atomicAdd(dst + fidx(r, h) * ldk + kofs + j, acc[r]);
   }
 }
 
@@ -118,7 +120,7 @@ __device__ __forceinline__ void db_vec(float* __restrict__ dst, const Scratch& S
 #pragma unroll
   for (int t = 0; t < 16; ++t) s += S.sA[(2 * t + h) * TPITCH + o];
   s += xor32(s);
-  if (h == 0) unsafeAtomicAdd(dst + o, s);
+  if (h == 0) atomicAdd(dst + o, s);
 }
 
 // sA <- d ; then per input tile: sX <- x ; dW += ...
@@ -206,20 +208,20 @@ __device__ __forceinline__ float out_row(const float* __restrict__ Wo, const flo
 template <int NC, bool WG>
 __device__ __forceinline__ void fc_bwd(const float* __restrict__ pk, const XyzPack& L, int i,
                                        const f32x16 (&cin)[NC], const f32x16& dh, const nslam_dec_grad& dg,
-                                       const Scratch& S, int lane, f32x16& dc) {
+                                       float* A, const Scratch& S, int lane, f32x16& dc) {
   gemm_acc(dc, pk + L.FCT(i) * NSLAM_FRAG, dh, lane);  // dz_i = dh_i
   if (WG) {
     wg_begin(dh, S, lane);
 #pragma unroll
-    for (int c = 0; c < NC; ++c) wg_block(dg.base + dg.wc[i], 32 * NC, 32 * c, 32, cin[c], S, lane);
-    wg_end(dg.base + dg.bc[i], S, lane);
+    for (int c = 0; c < NC; ++c) wg_block(A + dg.wc[i], 32 * NC, 32 * c, 32, cin[c], S, lane);
+    wg_end(A + dg.bc[i], S, lane);
   }
 }
 
 template <int NC, int NOUT, int GOFS, bool WG, bool EMBG>
 __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const f32x16 (&cin)[NC],
                                              const float x[3], const float (&gall)[4], const nslam_dec_grad& dg,
-                                             const Scratch& S, int lane, f32x16& dc, float gx[3]) {
+                                             float* A, const Scratch& S, int lane, f32x16& dc, float gx[3]) {
   const XyzPack L{NC};
   const int h = lane >> 5;
   uint32_t m[5];
@@ -247,11 +249,11 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
         s += S.gtab[p * 4 + GOFS + j] * S.sX[p * TPITCH + f];
       }
       s += xor32(s);
-      if (h == 0) unsafeAtomicAdd(dg.base + dg.wo + 32 * j + f, s);
+      if (h == 0) atomicAdd(A + dg.wo + 32 * j + f, s);
       if (lane == 0) {
         float sb = 0.f;
         for (int p = 0; p < 32; ++p) sb += S.gtab[p * 4 + GOFS + j];
-        unsafeAtomicAdd(dg.base + dg.bo + j, sb);
+        atomicAdd(A + dg.bo + j, sb);
       }
     }
     lds_sync();
@@ -260,57 +262,57 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
   const float* FB = pk + L.FB();
 
   // layer 4
-  fc_bwd<NC, WG>(pk, L, 4, cin, dh, dg, S, lane, dc);
+  fc_bwd<NC, WG>(pk, L, 4, cin, dh, dg, A, S, lane, dc);
   f32x16 da = apply_mask(dh, m[4]);
   if (WG) {
     wg_begin(da, S, lane);
-    wg_block(dg.base + dg.w[4], 32, 0, 32, hs[3], S, lane);
-    wg_end(dg.base + dg.b[4], S, lane);
+    wg_block(A + dg.w[4], 32, 0, 32, hs[3], S, lane);
+    wg_end(A + dg.b[4], S, lane);
   }
   dh = zero16();
   gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
   // layer 3 (input = [emb | h2])
-  fc_bwd<NC, WG>(pk, L, 3, cin, dh, dg, S, lane, dc);
+  fc_bwd<NC, WG>(pk, L, 3, cin, dh, dg, A, S, lane, dc);
   const f32x16 da3 = apply_mask(dh, m[3]);
   if (WG) {
     wg_begin(da3, S, lane);
 #pragma unroll
     for (int b = 0; b < 3; ++b)
-      wg_block(dg.base + dg.w[3], 125, 32 * b, b < 2 ? 32 : 29, emb_tile<false>(FB, x, b, lane), S, lane);
-    wg_block(dg.base + dg.w[3], 125, 93, 32, hs[2], S, lane);
-    wg_end(dg.base + dg.b[3], S, lane);
+      wg_block(A + dg.w[3], 125, 32 * b, b < 2 ? 32 : 29, emb_tile<false>(FB, x, b, lane), S, lane);
+    wg_block(A + dg.w[3], 125, 93, 32, hs[2], S, lane);
+    wg_end(A + dg.b[3], S, lane);
   }
   dh = zero16();
   gemm_acc(dh, pk + (L.L3T() + 3) * NSLAM_FRAG, da3, lane);
   // layer 2
-  fc_bwd<NC, WG>(pk, L, 2, cin, dh, dg, S, lane, dc);
+  fc_bwd<NC, WG>(pk, L, 2, cin, dh, dg, A, S, lane, dc);
   da = apply_mask(dh, m[2]);
   if (WG) {
     wg_begin(da, S, lane);
-    wg_block(dg.base + dg.w[2], 32, 0, 32, hs[1], S, lane);
-    wg_end(dg.base + dg.b[2], S, lane);
+    wg_block(A + dg.w[2], 32, 0, 32, hs[1], S, lane);
+    wg_end(A + dg.b[2], S, lane);
   }
   dh = zero16();
   gemm_acc(dh, pk + L.L2T() * NSLAM_FRAG, da, lane);
   // layer 1
-  fc_bwd<NC, WG>(pk, L, 1, cin, dh, dg, S, lane, dc);
+  fc_bwd<NC, WG>(pk, L, 1, cin, dh, dg, A, S, lane, dc);
   da = apply_mask(dh, m[1]);
   if (WG) {
     wg_begin(da, S, lane);
-    wg_block(dg.base + dg.w[1], 32, 0, 32, hs[0], S, lane);
-    wg_end(dg.base + dg.b[1], S, lane);
+    wg_block(A + dg.w[1], 32, 0, 32, hs[0], S, lane);
+    wg_end(A + dg.b[1], S, lane);
   }
   dh = zero16();
   gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
   // layer 0 (input = emb)
-  fc_bwd<NC, WG>(pk, L, 0, cin, dh, dg, S, lane, dc);
+  fc_bwd<NC, WG>(pk, L, 0, cin, dh, dg, A, S, lane, dc);
   da = apply_mask(dh, m[0]);
   if (WG) {
     wg_begin(da, S, lane);
 #pragma unroll
     for (int b = 0; b < 3; ++b)
-      wg_block(dg.base + dg.w[0], 93, 32 * b, b < 2 ? 32 : 29, emb_tile<false>(FB, x, b, lane), S, lane);
-    wg_end(dg.base + dg.b[0], S, lane);
+      wg_block(A + dg.w[0], 93, 32 * b, b < 2 ? 32 : 29, emb_tile<false>(FB, x, b, lane), S, lane);
+    wg_end(A + dg.b[0], S, lane);
   }
 
   // Fourier features: de_b = L3T_b da3 + L0T_b da0 ; G = de * cos(theta)
@@ -354,7 +356,7 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int k = 32 * b + fidx(r, h);
-            if (k < NSLAM_EMB) unsafeAtomicAdd(dg.base + dg.B + jj * NSLAM_EMB + k, acc[r]);
+            if (k < NSLAM_EMB) atomicAdd(A + dg.B + jj * NSLAM_EMB + k, acc[r]);
           }
         }
         lds_sync();
@@ -401,7 +403,8 @@ __device__ __forceinline__ f32x16 noxyz_forward(const float* __restrict__ pk, co
 
 template <bool WG>
 __device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, const f32x16& c, float g,
-                                               const nslam_dec_grad& dg, const Scratch& S, int lane, f32x16& dc) {
+                                               const nslam_dec_grad& dg, float* A, const Scratch& S, int lane,
+                                               f32x16& dc) {
   const NoXyzPack L;
   const int h = lane >> 5;
   uint32_t m[5];
@@ -424,11 +427,11 @@ __device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, con
       s += S.gtab[p * 4 + 3] * S.sX[p * TPITCH + f];
     }
     s += xor32(s);
-    if (h == 0) unsafeAtomicAdd(dg.base + dg.wo + f, s);
+    if (h == 0) atomicAdd(A + dg.wo + f, s);
     if (lane == 0) {
       float sb = 0.f;
       for (int p = 0; p < 32; ++p) sb += S.gtab[p * 4 + 3];
-      unsafeAtomicAdd(dg.base + dg.bo, sb);
+      atomicAdd(A + dg.bo, sb);
     }
     lds_sync();
   }
@@ -437,8 +440,8 @@ __device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, con
   f32x16 da = apply_mask(dh, m[4]);
   if (WG) {
     wg_begin(da, S, lane);
-    wg_block(dg.base + dg.w[4], 32, 0, 32, hs[3], S, lane);
-    wg_end(dg.base + dg.b[4], S, lane);
+    wg_block(A + dg.w[4], 32, 0, 32, hs[3], S, lane);
+    wg_end(A + dg.b[4], S, lane);
   }
   dh = zero16();
   gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
@@ -446,9 +449,9 @@ __device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, con
   da = apply_mask(dh, m[3]);
   if (WG) {
     wg_begin(da, S, lane);
-    wg_block(dg.base + dg.w[3], 64, 0, 32, c, S, lane);
-    wg_block(dg.base + dg.w[3], 64, 32, 32, hs[2], S, lane);
-    wg_end(dg.base + dg.b[3], S, lane);
+    wg_block(A + dg.w[3], 64, 0, 32, c, S, lane);
+    wg_block(A + dg.w[3], 64, 32, 32, hs[2], S, lane);
+    wg_end(A + dg.b[3], S, lane);
   }
   gemm_acc(dc, pk + L.L3T() * NSLAM_FRAG, da, lane);
   dh = zero16();
@@ -457,8 +460,8 @@ __device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, con
   da = apply_mask(dh, m[2]);
   if (WG) {
     wg_begin(da, S, lane);
-    wg_block(dg.base + dg.w[2], 32, 0, 32, hs[1], S, lane);
-    wg_end(dg.base + dg.b[2], S, lane);
+    wg_block(A + dg.w[2], 32, 0, 32, hs[1], S, lane);
+    wg_end(A + dg.b[2], S, lane);
   }
   dh = zero16();
   gemm_acc(dh, pk + L.L2T() * NSLAM_FRAG, da, lane);
@@ -466,8 +469,8 @@ __device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, con
   da = apply_mask(dh, m[1]);
   if (WG) {
     wg_begin(da, S, lane);
-    wg_block(dg.base + dg.w[1], 32, 0, 32, hs[0], S, lane);
-    wg_end(dg.base + dg.b[1], S, lane);
+    wg_block(A + dg.w[1], 32, 0, 32, hs[0], S, lane);
+    wg_end(A + dg.b[1], S, lane);
   }
   dh = zero16();
   gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
@@ -475,8 +478,8 @@ __device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, con
   da = apply_mask(dh, m[0]);
   if (WG) {
     wg_begin(da, S, lane);
-    wg_block(dg.base + dg.w[0], 32, 0, 32, c, S, lane);
-    wg_end(dg.base + dg.b[0], S, lane);
+    wg_block(A + dg.w[0], 32, 0, 32, c, S, lane);
+    wg_end(A + dg.b[0], S, lane);
   }
   gemm_acc(dc, pk + L.L0T() * NSLAM_FRAG, da, lane);
 }
@@ -485,11 +488,17 @@ __device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, con
 // grid gradient scatter (atomics shaped as two 128-B row segments per wave-instruction) and
 // coordinate gradient through the trilinear weights
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void scatter_grid_grad(float* __restrict__ grad, const Corners& cr, const f32x16& dc, bool valid,
-                                  const Scratch& S, int lane) {
-  const int h = lane >> 5, p = lane & 31;
+__device__ __forceinline__ void scatter_grid_grad(float* __restrict__ grad, const Corners& cr, const f32x16& dc,
+                                                  bool valid, const Scratch& S, int lane) {
+  // Points of a tile are consecutive samples of (mostly) one ray: runs of samples that fall in the
+  // same cell are summed in registers first, so each run costs 8 row-atomics instead of 8 per
+  // sample (surface samples cluster in 1-3 cells; this is what removes the atomic contention on
+  // the small middle grid).  Half h walks points 16h..16h+15; lane = channel, so every atomic
+  // wave-instruction is one or two 128-B row segments.
+  const int h = lane >> 5, ch = lane & 31;
   tstore(S.sA, dc, lane);
   if (h == 0) {
+    const int p = lane & 31;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       S.crow[p * 8 + k] = cr.row[k];
@@ -497,15 +506,43 @@ __device__ __forceinline__ void scatter_grid_grad(float* __restrict__ grad, cons
     }
   }
   lds_sync();
-  for (int j = 0; j < 16; ++j) {
-    const int pp = 2 * j + h;
-    const float v = S.sA[pp * TPITCH + p];
+  float acc[8], wsum[8];
+  int rows[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    acc[k] = 0.f;
+    wsum[k] = 0.f;
+    rows[k] = 0;
+  }
+  int cur = -1;
+  for (int t = 0; t < 16; ++t) {
+    const int pp = 16 * h + t;
+    const int cell = S.crow[pp * 8];
+    if (cell != cur) {
+      if (cur >= 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (wsum[k] != 0.f) unsafeAtomicAdd(grad + (size_t)rows[k] * NSLAM_C_DIM + ch, acc[k]);
+      }
+      cur = cell;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        acc[k] = 0.f;
+        wsum[k] = 0.f;
+        rows[k] = S.crow[pp * 8 + k];
+      }
+    }
+    const float v = S.sA[pp * TPITCH + ch];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const float w = S.cw[pp * 8 + k];
-      if (w != 0.f) unsafeAtomicAdd(grad + (size_t)S.crow[pp * 8 + k] * NSLAM_C_DIM + p, w * v);
+      acc[k] += w * v;
+      wsum[k] += w;
     }
   }
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    if (wsum[k] != 0.f) unsafeAtomicAdd(grad + (size_t)rows[k] * NSLAM_C_DIM + ch, acc[k]);
   lds_sync();
 }
 
@@ -579,23 +616,21 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd(QueryKArgs a) {
   }
 }
 
-// One backward launch per decoder: the decoder's forward is recomputed, its parameter / grid
-// gradients are accumulated, and its share of d/dpts is added into g_pts (launches on one stream
-// are ordered, each point is owned by one lane pair: plain read-modify-write, no atomics).
-//   DEC: NSLAM_DEC_*;  FIRST: this launch initialises g_pts instead of adding.
-template <int DEC, bool WG, bool PG, bool FIRST>
-__global__ __launch_bounds__(64, 2) void k_dec_bwd(QueryKArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  Scratch S;
-  S.sA = lds;
-  S.sX = lds + TILE_FLOATS;
-  S.gtab = lds + 2 * TILE_FLOATS;
-  S.xtab = S.gtab + 32 * 4;
-  S.crow = reinterpret_cast<int*>(S.xtab + 32 * 3);
-  S.cw = reinterpret_cast<float*>(S.crow + 32 * 8);
+// One backward launch per decoder: the decoder's forward is recomputed, its grid gradient is
+// scattered, its parameter gradients are accumulated and its share of d/dpts is added into g_pts
+// (launches on one stream are ordered and each point is owned by one lane pair: plain
+// read-modify-write, no atomics).  A workgroup holds WAVES waves; each wave walks tiles.  With
+// parameter gradients (WG) the workgroup accumulates them in LDS (ds_add_f32) over all its tiles
+// and writes one partial slab; k_slab_reduce sums the slabs in a fixed order (deterministic).
+constexpr int kScratchFloats = 2 * TILE_FLOATS + 32 * 4 + 32 * 3 + 32 * 8 * 2;
 
-  const int lane = threadIdx.x;
-  const int64_t tile = blockIdx.x;
+template <int DEC, bool WG, bool PG, bool FIRST>
+__device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, float* A, const Scratch& S,
+                                             int lane) {
+  // Every LDS-accumulator / scratch address is a function of the lane only, i.e. invariant across
+  // the tile loop; letting LICM hoist the ~300 of them pins (and spills) the register file.
+  // Re-derive them per tile.
+  asm volatile("" : "+v"(lane));
   const int h = lane >> 5, p = lane & 31;
   const int64_t idx = tile * 32 + p;
   const Pt q = load_point(a, idx);
@@ -619,25 +654,28 @@ __global__ __launch_bounds__(64, 2) void k_dec_bwd(QueryKArgs a) {
   const nslam_grid& gr = a.c.grid[DEC];
   const nslam_dec_grad& dg = a.c.dgrad[DEC];
   const float* pk = a.c.packed[DEC];
+  // The weight fragments are loop-invariant across the tile loop; hoisting their ~100 loads out of
+  // the loop would pin hundreds of registers.  Launder the base pointer per tile so they stay put.
+  asm volatile("" : "+s"(pk));
   Corners cr;
   grid_corners(cr, gr, q);
   f32x16 dc;
   float gx[3] = {0.f, 0.f, 0.f};
   if (DEC == NSLAM_DEC_COARSE) {
     const f32x16 c = gather_tile(gr.data, cr, lane);
-    noxyz_backward<WG>(pk, c, g[3], dg, S, lane, dc);
+    noxyz_backward<WG>(pk, c, g[3], dg, A, S, lane, dc);
   } else if (DEC == NSLAM_DEC_FINE) {
     Corners cm;
     grid_corners(cm, a.c.grid[NSLAM_DEC_MIDDLE], q);
     // the middle feature enters the fine decoder under torch.no_grad (decoder.py:184-187)
     const f32x16 cf[2] = {gather_tile(gr.data, cr, lane), gather_tile(a.c.grid[NSLAM_DEC_MIDDLE].data, cm, lane)};
-    xyz_backward<2, 1, 3, WG, PG || WG>(pk, cf, q.x, g, dg, S, lane, dc, gx);
+    xyz_backward<2, 1, 3, WG, PG || WG>(pk, cf, q.x, g, dg, A, S, lane, dc, gx);
   } else {
     const f32x16 c[1] = {gather_tile(gr.data, cr, lane)};
     if (DEC == NSLAM_DEC_COLOR)  // the colour decoder's 4th output is overwritten by the combiner
-      xyz_backward<1, 3, 0, WG, PG || WG>(pk, c, q.x, g, dg, S, lane, dc, gx);
+      xyz_backward<1, 3, 0, WG, PG || WG>(pk, c, q.x, g, dg, A, S, lane, dc, gx);
     else
-      xyz_backward<1, 1, 3, WG, PG || WG>(pk, c, q.x, g, dg, S, lane, dc, gx);
+      xyz_backward<1, 1, 3, WG, PG || WG>(pk, c, q.x, g, dg, A, S, lane, dc, gx);
   }
   if (gr.grad) scatter_grid_grad(gr.grad, cr, dc, q.valid, S, lane);
   if (PG) {
@@ -650,7 +688,49 @@ __global__ __launch_bounds__(64, 2) void k_dec_bwd(QueryKArgs a) {
   }
 }
 
-constexpr size_t kBwdLds = (2 * TILE_FLOATS + 32 * 4 + 32 * 3 + 32 * 8 * 2) * sizeof(float);
+template <int DEC, bool WG, bool PG, bool FIRST, int WAVES>
+__global__ __launch_bounds__(64 * WAVES, 2) void k_dec_bwd(QueryKArgs a, float* __restrict__ slab, int acc_floats) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* A = lds;  // parameter-gradient accumulator (WG only)
+  float* sc = lds + (WG ? acc_floats : 0) + wave * kScratchFloats;
+  Scratch S;
+  S.sA = sc;
+  S.sX = sc + TILE_FLOATS;
+  S.gtab = sc + 2 * TILE_FLOATS;
+  S.xtab = S.gtab + 32 * 4;
+  S.crow = reinterpret_cast<int*>(S.xtab + 32 * 3);
+  S.cw = reinterpret_cast<float*>(S.crow + 32 * 8);
+  if (WG) {
+    for (int i = threadIdx.x; i < acc_floats; i += blockDim.x) A[i] = 0.f;
+    __syncthreads();
+  }
+  const int64_t ntiles = (a.n + 31) / 32;
+  if (!WG) {  // one tile per wave (grid covers all tiles)
+    const int64_t tile = (int64_t)blockIdx.x * WAVES + wave;
+    if (tile < ntiles) dec_bwd_tile<DEC, WG, PG, FIRST>(a, tile, A, S, lane);
+    return;
+  }
+#pragma nounroll
+  for (int64_t tile = (int64_t)blockIdx.x * WAVES + wave; tile < ntiles; tile += (int64_t)gridDim.x * WAVES)
+    dec_bwd_tile<DEC, WG, PG, FIRST>(a, tile, A, S, lane);
+  if (WG) {
+    __syncthreads();
+    float* dst = slab + (size_t)blockIdx.x * acc_floats;
+    for (int i = threadIdx.x; i < acc_floats; i += blockDim.x) dst[i] = A[i];
+  }
+}
+
+// base[j] += sum_b slab[b][j]   (fixed order over b: deterministic parameter gradients)
+__global__ __launch_bounds__(256) void k_slab_reduce(const float* __restrict__ slab, int nslab, int acc_floats,
+                                                     int count, float* __restrict__ base) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= count) return;
+  float s = 0.f;
+  for (int b = 0; b < nslab; ++b) s += slab[(size_t)b * acc_floats + j];
+  base[j] += s;
+}
+
 
 bool grid_ok(const nslam_grid& g) {
   return g.data && g.dims[0] > 0 && g.dims[1] > 0 && g.dims[2] > 0 && (((uintptr_t)g.data) & 15) == 0;
@@ -696,52 +776,132 @@ extern "C" int nslam_query_fwd(const nslam_query_cfg* cfg, const double* pts, in
   return hip_status();
 }
 
+namespace {
+
+constexpr int kWavesNoWG = 4;
+constexpr int kMaxLdsBytes = 160 * 1024;
+
+int acc_floats_of(const nslam_dec_grad& dg) { return (int)((dg.count + 3) & ~int64_t(3)); }
+
+// waves per workgroup for the parameter-gradient kernels: as many as the LDS leaves room for
+int waves_wg(int acc_floats) {
+  const int per_wave = kScratchFloats * (int)sizeof(float);
+  int w = (kMaxLdsBytes - acc_floats * (int)sizeof(float)) / per_wave;
+  return w >= 8 ? 8 : (w >= 6 ? 6 : (w >= 4 ? 4 : w));
+}
+
+int64_t wg_blocks(int64_t tiles, int waves) {
+  const int64_t b = (tiles + waves - 1) / waves;
+  return b < 256 ? b : 256;  // one workgroup per CU (LDS-bound); tiles beyond are walked in-kernel
+}
+
+template <int DEC, bool WG, bool PG, bool FIRST, int WAVES>
+int launch_one(const QueryKArgs& a, float* slab, int acc, int64_t blocks, hipStream_t s) {
+  const size_t lds = ((WG ? acc : 0) + (size_t)WAVES * kScratchFloats) * sizeof(float);
+  auto kern = k_dec_bwd<DEC, WG, PG, FIRST, WAVES>;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lds) != hipSuccess)
+    return hip_status();
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(64 * WAVES), lds, s, a, slab, acc);
+  return hip_status();
+}
+
 template <int DEC, bool WG, bool PG>
-void launch_dec_bwd(const QueryKArgs& a, bool first, dim3 grid, hipStream_t s) {
-  if (first)
-    hipLaunchKernelGGL((k_dec_bwd<DEC, WG, PG, true>), grid, dim3(64), kBwdLds, s, a);
-  else
-    hipLaunchKernelGGL((k_dec_bwd<DEC, WG, PG, false>), grid, dim3(64), kBwdLds, s, a);
+int launch_dec_bwd(const QueryKArgs& a, bool first, float* slab, hipStream_t s) {
+  const int64_t tiles = (a.n + 31) / 32;
+  if (!WG) {
+    const int64_t blocks = (tiles + kWavesNoWG - 1) / kWavesNoWG;
+    return first ? launch_one<DEC, false, PG, true, kWavesNoWG>(a, nullptr, 0, blocks, s)
+                 : launch_one<DEC, false, PG, false, kWavesNoWG>(a, nullptr, 0, blocks, s);
+  }
+  const nslam_dec_grad& dg = a.c.dgrad[DEC];
+  const int acc = acc_floats_of(dg);
+  const int w = waves_wg(acc);
+  int rc;
+  if (w == 8) {
+    const int64_t blocks = wg_blocks(tiles, 8);
+    rc = first ? launch_one<DEC, true, PG, true, 8>(a, slab, acc, blocks, s)
+               : launch_one<DEC, true, PG, false, 8>(a, slab, acc, blocks, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((dg.count + 255) / 256)), dim3(256), 0, s, slab, (int)blocks,
+                       acc, (int)dg.count, dg.base);
+  } else if (w >= 4) {
+    const int64_t blocks = wg_blocks(tiles, 4);
+    rc = first ? launch_one<DEC, true, PG, true, 4>(a, slab, acc, blocks, s)
+               : launch_one<DEC, true, PG, false, 4>(a, slab, acc, blocks, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((dg.count + 255) / 256)), dim3(256), 0, s, slab, (int)blocks,
+                       acc, (int)dg.count, dg.base);
+  } else {
+    return NSLAM_EUNSUPPORTED;
+  }
+  return hip_status();
 }
 
 template <int DEC>
-void dispatch_dec_bwd(const QueryKArgs& a, bool first, dim3 grid, hipStream_t s) {
+int dispatch_dec_bwd(const QueryKArgs& a, bool first, float* slab, hipStream_t s) {
   const bool wg = a.c.dgrad[DEC].base != nullptr;
   const bool pg = a.c.need_pts_grad != 0;
-  if (wg && pg) launch_dec_bwd<DEC, true, true>(a, first, grid, s);
-  else if (wg) launch_dec_bwd<DEC, true, false>(a, first, grid, s);
-  else if (pg) launch_dec_bwd<DEC, false, true>(a, first, grid, s);
-  else launch_dec_bwd<DEC, false, false>(a, first, grid, s);
+  if (wg && pg) return launch_dec_bwd<DEC, true, true>(a, first, slab, s);
+  if (wg) return launch_dec_bwd<DEC, true, false>(a, first, slab, s);
+  if (pg) return launch_dec_bwd<DEC, false, true>(a, first, slab, s);
+  return launch_dec_bwd<DEC, false, false>(a, first, slab, s);
+}
+
+size_t bwd_ws_bytes(const nslam_query_cfg* cfg, int64_t n_pts) {
+  size_t need = 0;
+  const int64_t tiles = (n_pts + 31) / 32;
+  for (int d = 0; d < 4; ++d) {
+    const nslam_dec_grad& dg = cfg->dgrad[d];
+    if (!dg.base || dg.count <= 0) continue;
+    const int acc = acc_floats_of(dg);
+    const int w = waves_wg(acc) >= 8 ? 8 : 4;
+    const size_t b = (size_t)wg_blocks(tiles, w) * acc * sizeof(float);
+    need = b > need ? b : need;  // decoders run one after the other on the stream: one region
+  }
+  return need;
+}
+
+}  // namespace
+
+extern "C" size_t nslam_query_bwd_workspace_size(const nslam_query_cfg* cfg, int64_t n_pts) {
+  if (!cfg || n_pts <= 0) return 0;
+  return bwd_ws_bytes(cfg, n_pts);
 }
 
 extern "C" int nslam_query_bwd(const nslam_query_cfg* cfg, const double* pts, int64_t n_pts, const float* g_raw,
-                               double* g_pts, void* stream) {
+                               double* g_pts, void* ws, size_t ws_bytes, void* stream) {
   const int rc = check_cfg(cfg, true);
   if (rc) return rc;
   if (n_pts < 0 || (n_pts > 0 && (!pts || !g_raw))) return NSLAM_EINVAL;
   if (cfg->need_pts_grad && n_pts > 0 && !g_pts) return NSLAM_EINVAL;
   if (n_pts == 0) return NSLAM_OK;
+  for (int d = 0; d < 4; ++d)
+    if (cfg->dgrad[d].base && (cfg->dgrad[d].count <= 0 || waves_wg(acc_floats_of(cfg->dgrad[d])) < 4))
+      return NSLAM_EUNSUPPORTED;
+  if (ws_bytes < bwd_ws_bytes(cfg, n_pts) || (bwd_ws_bytes(cfg, n_pts) > 0 && !ws)) return NSLAM_EWORKSPACE;
   QueryKArgs a{*cfg, pts, n_pts, nullptr, g_raw, g_pts};
-  const dim3 grid((unsigned)((n_pts + 31) / 32));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  float* slab = reinterpret_cast<float*>(ws);
+  int r = NSLAM_OK;
   switch (cfg->stage) {
     case NSLAM_STAGE_COARSE:
-      dispatch_dec_bwd<NSLAM_DEC_COARSE>(a, true, grid, s);
+      r = dispatch_dec_bwd<NSLAM_DEC_COARSE>(a, true, slab, s);
       break;
     case NSLAM_STAGE_MIDDLE:
-      dispatch_dec_bwd<NSLAM_DEC_MIDDLE>(a, true, grid, s);
+      r = dispatch_dec_bwd<NSLAM_DEC_MIDDLE>(a, true, slab, s);
       break;
     case NSLAM_STAGE_FINE:
-      dispatch_dec_bwd<NSLAM_DEC_MIDDLE>(a, true, grid, s);
-      dispatch_dec_bwd<NSLAM_DEC_FINE>(a, false, grid, s);
+      r = dispatch_dec_bwd<NSLAM_DEC_MIDDLE>(a, true, slab, s);
+      if (!r) r = dispatch_dec_bwd<NSLAM_DEC_FINE>(a, false, slab, s);
       break;
     default:
-      dispatch_dec_bwd<NSLAM_DEC_MIDDLE>(a, true, grid, s);
-      dispatch_dec_bwd<NSLAM_DEC_FINE>(a, false, grid, s);
-      dispatch_dec_bwd<NSLAM_DEC_COLOR>(a, false, grid, s);
+      r = dispatch_dec_bwd<NSLAM_DEC_MIDDLE>(a, true, slab, s);
+      if (!r) r = dispatch_dec_bwd<NSLAM_DEC_FINE>(a, false, slab, s);
+      if (!r) r = dispatch_dec_bwd<NSLAM_DEC_COLOR>(a, false, slab, s);
       break;
   }
-  return hip_status();
+  return r;
 }
 
 extern "C" int nslam_pack_layout(int kind, int nc, int32_t* out, int n) {

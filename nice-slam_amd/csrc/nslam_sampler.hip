@@ -124,6 +124,58 @@ __global__ __launch_bounds__(128) void k_sample(SamplerArgs a) {
   for (int k = 0; k < s0 + s1; ++k) out[k] = m[k];
 }
 
+// One wave per ray (S = s0 + s1 <= 64): lane k holds sample k of the stratified list (k < s0)
+// or of the surface list; the final position is the rank of the value among all S values (ties
+// broken by lane), i.e. exactly the ascending order torch.sort produces — no serial merge.
+__global__ __launch_bounds__(256) void k_sample_wave(SamplerArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= a.n) return;
+  double tmin = 0.0;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const double o = (double)a.o[r * 3 + k];
+    const double dd = (double)a.d[r * 3 + k];
+    const double t0 = (a.lo[k] - o) / dd;
+    const double t1 = (a.hi[k] - o) / dd;
+    const double tm = t0 > t1 ? t0 : t1;
+    tmin = (k == 0 || tm < tmin) ? tm : tmin;
+  }
+  const double far_bb = tmin + 0.01;
+  const bool has_gt = a.gt != nullptr;
+  const int s0 = a.s0, s1 = has_gt ? a.s1 : 0, S = s0 + s1;
+  float g = 0.f, near_f = 0.01f, gmax = 0.f;
+  double far = far_bb;
+  if (has_gt) {
+    g = a.gt[r];
+    gmax = fkey_inv(*a.ws);
+    near_f = g * 0.01f;
+    const double hi = (double)(gmax * 1.2f);
+    far = far_bb < 0.0 ? 0.0 : far_bb;
+    far = far > hi ? hi : far;
+  }
+  double v = __builtin_inf();
+  if (lane < s0) {
+    const float t = a.ts[lane];
+    v = a.lindisp ? 1.0 / ((double)((1.f / near_f) * (1.f - t)) + (1.0 / far) * (double)t)
+                  : (double)(near_f * (1.f - t)) + far * (double)t;
+  } else if (lane < S) {
+    const double u = a.tu[lane - s0];
+    v = g > 0.f ? (double)(0.95f * g) * (1.0 - u) + (double)(1.05f * g) * u : 0.001 * (1.0 - u) + (double)gmax * u;
+  }
+  double* out = a.z + r * (int64_t)S;
+  if (s1 == 0) {  // no sort in the reference when N_surface == 0 (Renderer.py:168)
+    if (lane < S) out[lane] = v;
+    return;
+  }
+  int rank = 0;
+  for (int j = 0; j < S; ++j) {
+    const double vj = __shfl(v, j, 64);
+    rank += (vj < v || (vj == v && j < lane)) ? 1 : 0;
+  }
+  if (lane < S) out[rank] = v;
+}
+
 int hip_status() {
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? NSLAM_OK : NSLAM_EHIP - (int)e;
@@ -169,7 +221,10 @@ extern "C" int nslam_sample_rays(const float* rays_o, const float* rays_d, const
     const int blocks = (int)std::min<int64_t>((n_rays + 255) / 256, 1024);
     hipLaunchKernelGGL(k_max_gt, dim3(blocks), dim3(256), 0, s, gt_depth, n_rays, reinterpret_cast<uint32_t*>(ws));
   }
-  hipLaunchKernelGGL(k_sample, dim3((unsigned)((n_rays + 127) / 128)), dim3(128), 0, s, a);
+  if (s0 + (gt_depth ? s1 : 0) <= 64)
+    hipLaunchKernelGGL(k_sample_wave, dim3((unsigned)((n_rays + 3) / 4)), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_sample, dim3((unsigned)((n_rays + 127) / 128)), dim3(128), 0, s, a);
   return hip_status();
 }
 
@@ -183,4 +238,4 @@ extern "C" const char* nslam_strerror(int code) {
   }
 }
 
-extern "C" int nslam_abi_version(void) { return 1; }
+extern "C" int nslam_abi_version(void) { return 2; }

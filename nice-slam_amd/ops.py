@@ -219,9 +219,11 @@ class _Query(torch.autograd.Function):
             off += n
         g_pts = torch.empty_like(pts) if need_pts else None
         cfg = _fill_cfg(meta, pairs, ctx.packed, dgrads, need_pts)
+        wsb = lib().nslam_query_bwd_workspace_size(ctypes.byref(cfg), pts.shape[0])
+        ws = torch.empty(wsb, dtype=torch.uint8, device=pts.device) if wsb else None
         with _span("query_bwd"):
-            rc = lib().nslam_query_bwd(ctypes.byref(cfg), ptr(pts), pts.shape[0], ptr(g_raw), ptr(g_pts),
-                                       stream_ptr(pts.device))
+            rc = lib().nslam_query_bwd(ctypes.byref(cfg), ptr(pts), pts.shape[0], ptr(g_raw), ptr(g_pts), ptr(ws),
+                                       wsb, stream_ptr(pts.device))
         check(rc, "nslam_query_bwd")
         out = [None, g_pts] + grid_grads
         for name in meta.decs:

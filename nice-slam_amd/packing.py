@@ -158,6 +158,7 @@ class DecoderPacker:
         if base is None:
             return g
         g.base = base.data_ptr()
+        g.count = self.n_params
         o = self.offsets
         for i in range(5):
             g.w[i] = o[f"pts_linears.{i}.weight"]

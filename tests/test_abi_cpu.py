@@ -25,7 +25,7 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_strerror(pkg):
     L = pkg._lib.lib()
-    assert L.nslam_abi_version() == 1
+    assert L.nslam_abi_version() == 2
     assert L.nslam_strerror(0) == b"ok"
     assert b"invalid" in L.nslam_strerror(-1)
 
@@ -48,6 +48,7 @@ def test_argument_validation_without_gpu(pkg):
     cfg = pkg._lib.NslamQueryCfg()
     cfg.stage = 7
     assert L.nslam_query_fwd(ctypes.byref(cfg), None, 10, None, None) == -1
+    assert L.nslam_query_bwd(ctypes.byref(cfg), None, 10, None, None, None, 0, None) == -1
     assert L.nslam_composite_fwd(None, None, 4, 0, None, None, None, None) == -1
     assert L.nslam_composite_fwd(None, None, 4, 1000, None, None, None, None) == -2
     dims = (ctypes.c_int32 * 3)(0, 1, 1)
