@@ -721,14 +721,25 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_dec_bwd(QueryKArgs a, float* 
   }
 }
 
-// base[j] += sum_b slab[b][j]   (fixed order over b: deterministic parameter gradients)
-__global__ __launch_bounds__(256) void k_slab_reduce(const float* __restrict__ slab, int nslab, int acc_floats,
-                                                     int count, float* __restrict__ base) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= count) return;
+// base[j] += sum_b slab[b][j].  A workgroup owns 64 parameters; each of its 16 waves sums every
+// 16th slab and the 16 partials are combined in LDS in a fixed order: deterministic, with 16x the
+// memory-level parallelism of a one-thread-per-parameter loop.
+__global__ __launch_bounds__(1024) void k_slab_reduce(const float* __restrict__ slab, int nslab, int acc_floats,
+                                                      int count, float* __restrict__ base) {
+  __shared__ float part[16][64];
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + c;
   float s = 0.f;
-  for (int b = 0; b < nslab; ++b) s += slab[(size_t)b * acc_floats + j];
-  base[j] += s;
+  if (j < count)
+    for (int b = g; b < nslab; b += 16) s += slab[(size_t)b * acc_floats + j];
+  part[g][c] = s;
+  __syncthreads();
+  if (g == 0 && j < count) {
+    float t = part[0][c];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) t += part[k][c];
+    base[j] += t;
+  }
 }
 
 
@@ -823,14 +834,14 @@ int launch_dec_bwd(const QueryKArgs& a, bool first, float* slab, hipStream_t s) 
     rc = first ? launch_one<DEC, true, PG, true, 8>(a, slab, acc, blocks, s)
                : launch_one<DEC, true, PG, false, 8>(a, slab, acc, blocks, s);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((dg.count + 255) / 256)), dim3(256), 0, s, slab, (int)blocks,
+    hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((dg.count + 63) / 64)), dim3(1024), 0, s, slab, (int)blocks,
                        acc, (int)dg.count, dg.base);
   } else if (w >= 4) {
     const int64_t blocks = wg_blocks(tiles, 4);
     rc = first ? launch_one<DEC, true, PG, true, 4>(a, slab, acc, blocks, s)
                : launch_one<DEC, true, PG, false, 4>(a, slab, acc, blocks, s);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((dg.count + 255) / 256)), dim3(256), 0, s, slab, (int)blocks,
+    hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((dg.count + 63) / 64)), dim3(1024), 0, s, slab, (int)blocks,
                        acc, (int)dg.count, dg.base);
   } else {
     return NSLAM_EUNSUPPORTED;
