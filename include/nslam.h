@@ -90,9 +90,12 @@ int nslam_pack_layout(int kind, int nc, int32_t* out, int n);
  * z_vals[N][S0+S1] (float64) for rays_o/rays_d [N][3] float32 and gt_depth [N] float32
  * (NULL = no depth: S1 is forced to 0 and near = 0.01).  t_strat = torch.linspace(0,1,S0)
  * (float32), t_surf = torch.linspace(0,1,S1).double() — passed in so the sampler uses the very
- * values the reference uses.  ws must hold nslam_workspace_size(NSLAM_WS_SAMPLER, N) bytes. */
-int nslam_sample_rays(const float* rays_o, const float* rays_d, const float* gt_depth, int64_t n_rays,
-                      const double* bound_lo, const double* bound_hi, /* HOST pointers, 3 each */
+ * values the reference uses.  The batch-global max(gt_depth) (Renderer.py:109,144) is computed
+ * over the N rays unless gt_max (a DEVICE float) is given — a ray-sharded job passes the
+ * all-reduced maximum so every shard samples exactly as the full batch would.
+ * ws must hold nslam_workspace_size(NSLAM_WS_SAMPLER, N) bytes. */
+int nslam_sample_rays(const float* rays_o, const float* rays_d, const float* gt_depth, const float* gt_max,
+                      int64_t n_rays, const double* bound_lo, const double* bound_hi, /* HOST pointers, 3 each */
                       const float* t_strat, int32_t s0, const double* t_surf, int32_t s1,
                       int32_t lindisp, double* z_vals, void* ws, size_t ws_bytes, void* stream);
 

@@ -7,10 +7,13 @@ The directory name is not a Python identifier: import with importlib.import_modu
 """
 import sys as _sys
 
-from . import _lib, common, decoder, ops, packing, renderer  # noqa: F401
+from . import _lib, common, config, decoder, distributed, mapper, ops, packing, renderer, slam, tracker  # noqa: F401
 from .decoder import NICE, MLP, MLP_no_xyz  # noqa: F401
+from .mapper import Mapper  # noqa: F401
 from .renderer import Renderer  # noqa: F401
+from .tracker import Tracker  # noqa: F401
 
 _sys.modules.setdefault("nice_slam_amd", _sys.modules[__name__])
 
-__all__ = ["NICE", "MLP", "MLP_no_xyz", "Renderer", "common", "decoder", "ops", "packing", "renderer"]
+__all__ = ["NICE", "MLP", "MLP_no_xyz", "Renderer", "Tracker", "Mapper", "common", "config", "decoder",
+           "distributed", "mapper", "ops", "packing", "renderer", "slam", "tracker"]

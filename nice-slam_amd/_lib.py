@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libnslam.so")
 
 NSLAM_OK = 0
-ABI_VERSION = 2
+ABI_VERSION = 3
 STAGES = {"coarse": 0, "middle": 1, "fine": 2, "color": 3}
 DEC_COARSE, DEC_MIDDLE, DEC_FINE, DEC_COLOR = 0, 1, 2, 3
 
@@ -79,7 +79,7 @@ def lib():
         vp, i32, i64, sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
         dp = ctypes.POINTER(ctypes.c_double)
         L.nslam_pack_layout.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int32), ctypes.c_int]
-        L.nslam_sample_rays.argtypes = [vp, vp, vp, i64, dp, dp, vp, i32, vp, i32, i32, vp, vp, sz, vp]
+        L.nslam_sample_rays.argtypes = [vp, vp, vp, vp, i64, dp, dp, vp, i32, vp, i32, i32, vp, vp, sz, vp]
         L.nslam_query_fwd.argtypes = [ctypes.POINTER(NslamQueryCfg), vp, i64, vp, vp]
         L.nslam_query_bwd.argtypes = [ctypes.POINTER(NslamQueryCfg), vp, i64, vp, vp, vp, sz, vp]
         L.nslam_query_bwd_workspace_size.argtypes = [ctypes.POINTER(NslamQueryCfg), i64]

@@ -19,6 +19,11 @@ def as_intrinsics_matrix(intrinsics):
     return K
 
 
+def random_select(l, k):
+    """src/common.py:66-71: k random indices of range(l) (numpy RNG, as the reference)."""
+    return list(np.random.permutation(np.array(range(l)))[:min(l, k)])
+
+
 def get_rays_from_uv(i, j, c2w, H, W, fx, fy, cx, cy, device):
     """src/common.py:74-89: dirs=((i-cx)/fx, -(j-cy)/fy, -1); rays_d = R dirs; rays_o = t."""
     if isinstance(c2w, np.ndarray):

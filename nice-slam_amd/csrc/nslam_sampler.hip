@@ -25,6 +25,8 @@ __device__ __forceinline__ float fkey_inv(uint32_t k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
 
+__global__ void k_key_of(const float* __restrict__ gmax, uint32_t* __restrict__ ws) { *ws = fkey(*gmax); }
+
 __global__ __launch_bounds__(256) void k_max_gt(const float* __restrict__ gt, int64_t n, uint32_t* __restrict__ ws) {
   uint32_t m = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -189,7 +191,8 @@ extern "C" size_t nslam_workspace_size(int which, int64_t n) {
   return 0;
 }
 
-extern "C" int nslam_sample_rays(const float* rays_o, const float* rays_d, const float* gt_depth, int64_t n_rays,
+extern "C" int nslam_sample_rays(const float* rays_o, const float* rays_d, const float* gt_depth, const float* gt_max,
+                                 int64_t n_rays,
                                  const double* bound_lo, const double* bound_hi, const float* t_strat, int32_t s0,
                                  const double* t_surf, int32_t s1, int32_t lindisp, double* z_vals, void* ws,
                                  size_t ws_bytes, void* stream) {
@@ -216,7 +219,9 @@ extern "C" int nslam_sample_rays(const float* rays_o, const float* rays_d, const
   a.lindisp = lindisp;
   a.z = z_vals;
   a.ws = reinterpret_cast<const uint32_t*>(ws);
-  if (gt_depth) {
+  if (gt_depth && gt_max) {
+    hipLaunchKernelGGL(k_key_of, dim3(1), dim3(1), 0, s, gt_max, reinterpret_cast<uint32_t*>(ws));
+  } else if (gt_depth) {
     if (hipMemsetAsync(ws, 0, 4, s) != hipSuccess) return hip_status();
     const int blocks = (int)std::min<int64_t>((n_rays + 255) / 256, 1024);
     hipLaunchKernelGGL(k_max_gt, dim3(blocks), dim3(256), 0, s, gt_depth, n_rays, reinterpret_cast<uint32_t*>(ws));
@@ -238,4 +243,4 @@ extern "C" const char* nslam_strerror(int code) {
   }
 }
 
-extern "C" int nslam_abi_version(void) { return 2; }
+extern "C" int nslam_abi_version(void) { return 3; }

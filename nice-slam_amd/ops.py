@@ -110,8 +110,11 @@ def _t_tables(device, s0, s1):
     return _T_CACHE[key]
 
 
-def sample_z(rays_o, rays_d, gt_depth, bound, n_strat, n_surf, lindisp=False):
-    """z_vals [N, n_strat(+n_surf)] float64 (surface samples only when gt_depth is given)."""
+def sample_z(rays_o, rays_d, gt_depth, bound, n_strat, n_surf, lindisp=False, gt_max=None):
+    """z_vals [N, n_strat(+n_surf)] float64 (surface samples only when gt_depth is given).
+
+    gt_max: optional device float scalar = max(gt_depth) over the FULL batch (ray sharding).
+    """
     ro = rays_o.detach().float().contiguous()
     rd = rays_d.detach().float().contiguous()
     n = ro.shape[0]
@@ -126,7 +129,8 @@ def sample_z(rays_o, rays_d, gt_depth, bound, n_strat, n_surf, lindisp=False):
     wsb = L.nslam_workspace_size(0, n)
     ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=ro.device)
     with _span("sample_rays"):
-        rc = L.nslam_sample_rays(ptr(ro), ptr(rd), ptr(gt), n, (ctypes.c_double * 3)(*lo),
+        gm = gt_max.detach().float().reshape(1).contiguous() if (gt_max is not None and gt is not None) else None
+        rc = L.nslam_sample_rays(ptr(ro), ptr(rd), ptr(gt), ptr(gm), n, (ctypes.c_double * 3)(*lo),
                                  (ctypes.c_double * 3)(*hi), ptr(ts), n_strat, ptr(tu), s1, int(bool(lindisp)),
                                  ptr(z), ptr(ws), wsb, stream_ptr(ro.device))
     check(rc, "nslam_sample_rays")

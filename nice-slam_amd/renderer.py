@@ -36,12 +36,16 @@ class Renderer(object):
         """Renderer.eval_points (Renderer.py:23-61): raw [M,4]; OOB points get occupancy logit 100."""
         return decoders(p, c_grid=c, stage=stage, oob_bound=self.bound)
 
-    def render_batch_ray(self, c, decoders, rays_d, rays_o, device, stage, gt_depth=None):
-        """Renderer.render_batch_ray (Renderer.py:63-198) → (depth f64 [N], uncertainty f64 [N], color f32 [N,3])."""
+    def render_batch_ray(self, c, decoders, rays_d, rays_o, device, stage, gt_depth=None, gt_max=None):
+        """Renderer.render_batch_ray (Renderer.py:63-198) → (depth f64 [N], uncertainty f64 [N], color f32 [N,3]).
+
+        gt_max (extension): device scalar max(gt_depth) of the full batch when rays are sharded.
+        """
         if stage == "coarse":
             gt_depth = None
         n_rays = rays_o.shape[0]
-        z = ops.sample_z(rays_o, rays_d, gt_depth, self.bound, self.N_samples, self.N_surface, self.lindisp)
+        z = ops.sample_z(rays_o, rays_d, gt_depth, self.bound, self.N_samples, self.N_surface, self.lindisp,
+                         gt_max=gt_max)
         pts = rays_o[..., None, :] + rays_d[..., None, :] * z[..., :, None]
         raw = self.eval_points(pts.reshape(-1, 3), decoders, c, stage, device)
         raw = raw.reshape(n_rays, z.shape[1], 4)

@@ -1,0 +1,130 @@
+"""Tracker drop-in: camera optimisation on the HIP render path (src/Tracker.py).
+
+`optimize_cam_in_batch` keeps the reference's signature and semantics (Tracker.py:71-128).
+The frame loop's per-frame logic (Tracker.py:184-256) is `track_frame`; dataset loading,
+process synchronisation and visualisation (Tracker.py:144-183) are out of scope.
+"""
+from __future__ import annotations
+
+import copy
+
+import numpy as np
+import torch
+
+from .common import get_camera_from_tensor, get_samples, get_tensor_from_camera
+
+
+class Tracker(object):
+    def __init__(self, cfg, args, slam, generator=None):
+        self.cfg = cfg
+        self.args = args
+        self.scale = cfg.get("scale", 1)
+        self.coarse = cfg["coarse"]
+        self.occupancy = cfg["occupancy"]
+        self.nice = slam.nice
+        self.bound = slam.bound
+        self.renderer = slam.renderer
+        self.shared_c = slam.shared_c
+        self.shared_decoders = slam.shared_decoders
+        self.estimate_c2w_list = slam.estimate_c2w_list
+        self.gt_c2w_list = slam.gt_c2w_list
+        self.mapping_idx = slam.mapping_idx
+        t = cfg["tracking"]
+        self.cam_lr = t["lr"]
+        self.device = t["device"]
+        self.num_cam_iters = t["iters"]
+        self.gt_camera = t["gt_camera"]
+        self.tracking_pixels = t["pixels"]
+        self.seperate_LR = t["seperate_LR"]
+        self.w_color_loss = t["w_color_loss"]
+        self.ignore_edge_W = t["ignore_edge_W"]
+        self.ignore_edge_H = t["ignore_edge_H"]
+        self.handle_dynamic = t["handle_dynamic"]
+        self.use_color_in_tracking = t["use_color_in_tracking"]
+        self.const_speed_assumption = t["const_speed_assumption"]
+        self.H, self.W, self.fx, self.fy, self.cx, self.cy = slam.H, slam.W, slam.fx, slam.fy, slam.cx, slam.cy
+        self.prev_mapping_idx = -1
+        self.generator = generator  # pixel-selection RNG (None = torch's global device generator)
+        self.c = {}
+        self.decoders = None
+        self._bound_dev = None
+
+    def _inside_mask(self, rays_o, rays_d, gt_depth):
+        """Tracker.py:95-100: keep rays whose AABB exit distance >= gt depth."""
+        if self._bound_dev is None or self._bound_dev.device != rays_o.device:
+            self._bound_dev = self.bound.to(rays_o.device)
+        with torch.no_grad():
+            t = (self._bound_dev.unsqueeze(0) - rays_o.detach().unsqueeze(-1)) / rays_d.detach().unsqueeze(-1)
+            t, _ = torch.min(torch.max(t, dim=2)[0], dim=1)
+            return t >= gt_depth
+
+    def optimize_cam_in_batch(self, camera_tensor, gt_color, gt_depth, batch_size, optimizer):
+        """One camera iteration: sample pixels, render, uncertainty-weighted L1, backward, step."""
+        device = self.device
+        H, W, fx, fy, cx, cy = self.H, self.W, self.fx, self.fy, self.cx, self.cy
+        optimizer.zero_grad()
+        c2w = get_camera_from_tensor(camera_tensor)
+        Wedge, Hedge = self.ignore_edge_W, self.ignore_edge_H
+        rays_o, rays_d, b_depth, b_color = get_samples(Hedge, H - Hedge, Wedge, W - Wedge, batch_size, H, W, fx, fy,
+                                                       cx, cy, c2w, gt_depth, gt_color, device,
+                                                       generator=self.generator)
+        if self.nice:
+            keep = self._inside_mask(rays_o, rays_d, b_depth)
+            rays_d, rays_o, b_depth, b_color = rays_d[keep], rays_o[keep], b_depth[keep], b_color[keep]
+        depth, uncertainty, color = self.renderer.render_batch_ray(self.c, self.decoders, rays_d, rays_o, device,
+                                                                   stage="color", gt_depth=b_depth)
+        uncertainty = uncertainty.detach()
+        resid = torch.abs(b_depth - depth) / torch.sqrt(uncertainty + 1e-10)
+        if self.handle_dynamic:
+            mask = (resid < 10 * resid.median()) & (b_depth > 0)
+        else:
+            mask = b_depth > 0
+        loss = resid[mask].sum()
+        if self.use_color_in_tracking:
+            loss = loss + self.w_color_loss * torch.abs(b_color - color)[mask].sum()
+        loss.backward()
+        optimizer.step()
+        optimizer.zero_grad()
+        return loss.item()
+
+    def update_para_from_mapping(self):
+        """Tracker.py:130-142: snapshot the mapper's decoders and grids (no gradients needed)."""
+        if self.mapping_idx[0] != self.prev_mapping_idx:
+            self.decoders = copy.deepcopy(self.shared_decoders).to(self.device)
+            # tracking optimises the camera only: decoder/grid gradients are never used
+            self.decoders.requires_grad_(False)
+            for key, val in self.shared_c.items():
+                self.c[key] = val.detach().clone().to(self.device)
+            self.prev_mapping_idx = self.mapping_idx[0].clone()
+
+    def track_frame(self, idx, gt_color, gt_depth, gt_c2w, pre_c2w=None, prev2_c2w=None):
+        """Per-frame camera estimate (Tracker.py:184-256, without sync/visualisation) → c2w [4,4]."""
+        device = self.device
+        self.update_para_from_mapping()
+        gt_depth, gt_color = gt_depth.to(device), gt_color.to(device)
+        if idx == 0 or self.gt_camera:
+            return gt_c2w.clone()
+        if self.const_speed_assumption and prev2_c2w is not None:
+            pre = pre_c2w.float().to(device)
+            delta = pre @ prev2_c2w.to(device).float().inverse()
+            est = delta @ pre
+        else:
+            est = pre_c2w.to(device)
+        camera_tensor = get_tensor_from_camera(est.detach()).to(device)
+        if self.seperate_LR:
+            T = camera_tensor[-3:].clone().requires_grad_(True)
+            quad = camera_tensor[:4].clone().requires_grad_(True)
+            optimizer = torch.optim.Adam([{"params": [T], "lr": self.cam_lr},
+                                          {"params": [quad], "lr": self.cam_lr * 0.2}])
+        else:
+            camera_tensor = camera_tensor.clone().requires_grad_(True)
+            optimizer = torch.optim.Adam([camera_tensor], lr=self.cam_lr)
+        best, best_loss = None, np.inf
+        for _ in range(self.num_cam_iters):
+            if self.seperate_LR:
+                camera_tensor = torch.cat([quad, T], 0)
+            loss = self.optimize_cam_in_batch(camera_tensor, gt_color, gt_depth, self.tracking_pixels, optimizer)
+            if loss < best_loss:
+                best_loss, best = loss, camera_tensor.clone().detach()
+        bottom = torch.tensor([[0, 0, 0, 1.0]], dtype=torch.float32, device=device)
+        return torch.cat([get_camera_from_tensor(best), bottom], 0)

@@ -136,8 +136,10 @@ def far_bound(rays_o, rays_d, bound):
     return t.max(2).values.min(1).values
 
 
-def sample_z(rays_o, rays_d, gt_depth, bound, n_strat, n_surf, lindisp=False):
-    """Stratified + surface sampler, src/utils/Renderer.py:82-170 (perturb=0) → z [N,S] f64."""
+def sample_z(rays_o, rays_d, gt_depth, bound, n_strat, n_surf, lindisp=False, gt_max=None):
+    """Stratified + surface sampler, src/utils/Renderer.py:82-170 (perturb=0) → z [N,S] f64.
+
+    gt_max: max(gt_depth) of the FULL batch when this call sees only a shard of it."""
     with torch.no_grad():
         far_bb = far_bound(rays_o, rays_d, bound)[:, None] + 0.01
         t_s = torch.linspace(0.0, 1.0, n_strat)
@@ -148,7 +150,8 @@ def sample_z(rays_o, rays_d, gt_depth, bound, n_strat, n_surf, lindisp=False):
         else:
             gt = gt_depth.reshape(-1, 1)
             near = gt.repeat(1, n_strat) * 0.01
-            far = torch.clamp(far_bb, 0, torch.max(gt * 1.2))
+            gmax = torch.max(gt) if gt_max is None else gt_max.reshape(()).float()
+            far = torch.clamp(far_bb, 0, gmax * 1.2)
         if lindisp:
             z = 1.0 / (1.0 / near * (1.0 - t_s) + 1.0 / far * t_s)
         else:
@@ -159,7 +162,7 @@ def sample_z(rays_o, rays_d, gt_depth, bound, n_strat, n_surf, lindisp=False):
             zs = torch.zeros(gt.shape[0], n_surf, dtype=torch.float64)
             g = gt[pos]
             zs[pos] = (0.95 * g) * (1.0 - t_u) + (1.05 * g) * t_u
-            zs[~pos] = 0.001 * (1.0 - t_u) + torch.max(gt) * t_u
+            zs[~pos] = 0.001 * (1.0 - t_u) + gmax * t_u
             z = torch.sort(torch.cat([z, zs], -1), -1).values
     return z
 
@@ -179,11 +182,11 @@ def composite(raw, z, occupancy=True):
 
 
 def render_batch_ray(sd, grids, rays_d, rays_o, stage, bound, gt_depth=None,
-                     n_strat=32, n_surf=16, coarse_bound=None, return_z=False):
+                     n_strat=32, n_surf=16, coarse_bound=None, return_z=False, gt_max=None):
     """Renderer.render_batch_ray, src/utils/Renderer.py:63-198 (N_importance=0, perturb=0)."""
     if stage == "coarse":
         gt_depth = None
-    z = sample_z(rays_o, rays_d, gt_depth, bound, n_strat, n_surf)
+    z = sample_z(rays_o, rays_d, gt_depth, bound, n_strat, n_surf, gt_max=gt_max)
     pts = rays_o[:, None, :] + rays_d[:, None, :] * z[:, :, None]
     raw = eval_points(sd, pts.reshape(-1, 3), grids, stage, bound, coarse_bound)
     depth, var, rgb, _ = composite(raw.reshape(z.shape[0], z.shape[1], 4), z)

@@ -25,7 +25,7 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_strerror(pkg):
     L = pkg._lib.lib()
-    assert L.nslam_abi_version() == 2
+    assert L.nslam_abi_version() == 3
     assert L.nslam_strerror(0) == b"ok"
     assert b"invalid" in L.nslam_strerror(-1)
 
@@ -54,7 +54,7 @@ def test_argument_validation_without_gpu(pkg):
     dims = (ctypes.c_int32 * 3)(0, 1, 1)
     assert L.nslam_grid_sample_fwd(None, dims, None, 5, None, None) == -1
     lo = (ctypes.c_double * 3)(0, 0, 0)
-    assert L.nslam_sample_rays(None, None, None, 3, lo, lo, None, 500, None, 0, 0, None, None, 0, None) == -2
+    assert L.nslam_sample_rays(None, None, None, None, 3, lo, lo, None, 500, None, 0, 0, None, None, 0, None) == -2
 
 
 def test_no_cpu_fallback(pkg):
