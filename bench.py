@@ -139,23 +139,26 @@ class Room0Scene:
         rays_o = self.c2w[:, None, :, 3].expand(F, n, 3).reshape(-1, 3)
         return rays_o, rays_d, depth, color
 
-    def step(self, stage="color", allreduce=None):
+    def step(self, stage="color", sharded=False):
         cfg = self.cfg
+        D = pkg().distributed
         self.opt.zero_grad(set_to_none=True)
         rays_o, rays_d, gt_depth, gt_color = self.sample_batch()
         with torch.no_grad():  # inside-mask prefilter (Mapper.py:469-481)
             t = (self.bound_dev[None] - rays_o[..., None].double()) / rays_d[..., None].double()
             keep = t.max(2).values.min(1).values >= gt_depth
         rays_o, rays_d, gt_depth, gt_color = rays_o[keep], rays_d[keep], gt_depth[keep], gt_color[keep]
+        # ray-sharded job: the sampler's batch-global max(gt_depth) is taken over all ranks' rays
+        gmax = D.global_max(gt_depth) if sharded else None
         depth, unc, color = self.renderer.render_batch_ray(self.grids, self.nice, rays_d, rays_o, self.dev, stage,
-                                                           gt_depth=gt_depth)
+                                                           gt_depth=gt_depth, gt_max=gmax)
         m = gt_depth > 0
         loss = torch.abs(gt_depth[m] - depth[m]).sum()
         if stage == "color":
             loss = loss + cfg["w_color"] * torch.abs(gt_color - color).sum()
         loss.backward()
-        if allreduce is not None:
-            allreduce(self)
+        if sharded:
+            D.allreduce_grads(D.optimizer_params(self.opt))
         self.opt.step()
         return rays_o.shape[0] * (cfg["n_strat"] + cfg["n_surf"])
 
@@ -164,22 +167,6 @@ class _Slam:
     def __init__(self, bound, cfg):
         self.nice, self.bound = True, bound
         self.H, self.W, self.fx, self.fy, self.cx, self.cy = cfg["H"], cfg["W"], cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"]
-
-
-def allreduce_grads(scene):
-    """Sum the gradients of every optimised tensor over the ranks (RCCL over xGMI)."""
-    ts = [p.grad for grp in scene.opt.param_groups for p in grp["params"] if p.grad is not None]
-    big = [t for t in ts if t.numel() > 1 << 16]
-    small = [t for t in ts if t.numel() <= 1 << 16]
-    for t in big:
-        dist.all_reduce(t)
-    if small:
-        flat = torch.cat([t.reshape(-1) for t in small])
-        dist.all_reduce(flat)
-        off = 0
-        for t in small:
-            t.copy_(flat[off:off + t.numel()].view_as(t))
-            off += t.numel()
 
 
 def cpu_baseline(scene, budget_s=20.0):
@@ -229,9 +216,9 @@ def main():
     dev = torch.device("cuda", local)
     P = pkg()
     scene = Room0Scene(dev, rank)
-    ar = allreduce_grads if world > 1 else None
+    sharded = world > 1
     for _ in range(args.warmup):
-        scene.step(allreduce=ar)
+        scene.step(sharded=sharded)
     torch.cuda.synchronize()
     P.ops.TIMER = P.ops.KernelTimer()
     if world > 1:
@@ -240,7 +227,7 @@ def main():
     t0 = time.perf_counter()
     samples = 0
     for _ in range(args.steps):
-        samples += scene.step(allreduce=ar)
+        samples += scene.step(sharded=sharded)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -159,7 +159,8 @@ def test_mapper_optimize_map_schedule(tiny, monkeypatch):
         for gi, name in enumerate(("decoders", "coarse", "middle", "fine", "color")):
             opt.param_groups[gi]["lr"] = st[stage][name + "_lr"]
         opt.zero_grad()
-        parts = [oracle_samples(sc, fp.log[2 * it + f], 0, sc.H, 0, sc.W, sc.c2w, sc.depth, sc.color)
+        # draw 0 is the overlap keyframe selection's (Mapper.py:185-186); then 2 frames per iteration
+        parts = [oracle_samples(sc, fp.log[1 + 2 * it + f], 0, sc.H, 0, sc.W, sc.c2w, sc.depth, sc.color)
                  for f in range(2)]
         ro, rd, gd, gc = (torch.cat([p[q] for p in parts]) for q in range(4))
         keep = orc.inside_mask(ro, rd, gd, sc.bound)
