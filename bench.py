@@ -118,12 +118,12 @@ class Room0Scene:
             self.depth[f] = d.reshape(H, W)
         self.color = torch.rand(F, H, W, 3, device=dev, generator=gd)
         self.dirs = dirs.reshape(-1, 3)
-        self.pix_gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+        torch.cuda.manual_seed(1000 + rank)  # pixel draws use the (graph-safe) default generator
         params = [{"params": list(self.nice.color_decoder.parameters()), "lr": cfg["lr"]["decoders"]},
                   {"params": [self.grids["grid_middle"]], "lr": cfg["lr"]["middle"]},
                   {"params": [self.grids["grid_fine"]], "lr": cfg["lr"]["fine"]},
                   {"params": [self.grids["grid_color"]], "lr": cfg["lr"]["color"]}]
-        self.opt = torch.optim.Adam(params, fused=True)
+        self.opt = torch.optim.Adam(params, fused=True, capturable=True)
         self.bound_dev = self.bound.to(dev)
 
     def sample_batch(self):
@@ -131,7 +131,7 @@ class Room0Scene:
         cfg = self.cfg
         F, H, W = cfg["window"], cfg["H"], cfg["W"]
         n = cfg["pixels"] // F
-        idx = torch.randint(H * W, (F, n), device=self.dev, generator=self.pix_gen)
+        idx = torch.randint(H * W, (F, n), device=self.dev)
         depth = torch.gather(self.depth.reshape(F, -1), 1, idx).reshape(-1)
         color = torch.gather(self.color.reshape(F, -1, 3), 1, idx[..., None].expand(F, n, 3)).reshape(-1, 3)
         d = self.dirs[idx]                                              # [F, n, 3]
@@ -140,27 +140,35 @@ class Room0Scene:
         return rays_o, rays_d, depth, color
 
     def step(self, stage="color", sharded=False):
+        """One mapping iteration with no host synchronisation (hipGraph-capturable).
+
+        The inside-mask prefilter (Mapper.py:469-481) removes rays; here they stay in the batch
+        with zero loss weight (their gradients are exactly zero) and the sampler's batch-global
+        max(gt_depth) is taken over the kept rays only — the same maths without a host-side
+        compaction.  Returns the number of kept ray-samples (device tensor).
+        """
         cfg = self.cfg
         D = pkg().distributed
         self.opt.zero_grad(set_to_none=True)
         rays_o, rays_d, gt_depth, gt_color = self.sample_batch()
-        with torch.no_grad():  # inside-mask prefilter (Mapper.py:469-481)
+        with torch.no_grad():
             t = (self.bound_dev[None] - rays_o[..., None].double()) / rays_d[..., None].double()
             keep = t.max(2).values.min(1).values >= gt_depth
-        rays_o, rays_d, gt_depth, gt_color = rays_o[keep], rays_d[keep], gt_depth[keep], gt_color[keep]
-        # ray-sharded job: the sampler's batch-global max(gt_depth) is taken over all ranks' rays
-        gmax = D.global_max(gt_depth) if sharded else None
+            gmax = torch.where(keep, gt_depth, torch.full_like(gt_depth, float("-inf"))).max().reshape(1)
+            if sharded:
+                gmax = D.global_max(gmax)
         depth, unc, color = self.renderer.render_batch_ray(self.grids, self.nice, rays_d, rays_o, self.dev, stage,
                                                            gt_depth=gt_depth, gt_max=gmax)
-        m = gt_depth > 0
-        loss = torch.abs(gt_depth[m] - depth[m]).sum()
+        m = keep & (gt_depth > 0)
+        loss = torch.where(m, torch.abs(gt_depth - depth), torch.zeros_like(depth)).sum()
         if stage == "color":
-            loss = loss + cfg["w_color"] * torch.abs(gt_color - color).sum()
+            cl = torch.where(keep[:, None], torch.abs(gt_color - color), torch.zeros_like(color)).sum()
+            loss = loss + cfg["w_color"] * cl
         loss.backward()
         if sharded:
             D.allreduce_grads(D.optimizer_params(self.opt))
         self.opt.step()
-        return rays_o.shape[0] * (cfg["n_strat"] + cfg["n_surf"])
+        return keep.sum() * (cfg["n_strat"] + cfg["n_surf"])
 
 
 class _Slam:
@@ -206,6 +214,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="no hipGraph capture")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -220,18 +229,45 @@ def main():
     for _ in range(args.warmup):
         scene.step(sharded=sharded)
     torch.cuda.synchronize()
-    P.ops.TIMER = P.ops.KernelTimer()
+    graph, mode = None, "eager"
+    if not args.eager:
+        try:  # capture one whole mapping iteration as a hipGraph (removes per-op host launch cost)
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    scene.step(sharded=sharded)
+            torch.cuda.current_stream().wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                g_samples = scene.step(sharded=sharded)
+            graph.replay()
+            torch.cuda.synchronize()
+            mode = "hipgraph"
+        except Exception as e:  # pragma: no cover - fall back to eager launches
+            print(f"graph capture failed, eager mode: {e!r}", file=sys.stderr)
+            graph = None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    samples = 0
+    acc = torch.zeros((), dtype=torch.int64, device=dev)
     for _ in range(args.steps):
-        samples += scene.step(sharded=sharded)
+        if graph is not None:
+            graph.replay()
+            acc += g_samples
+        else:
+            acc += scene.step(sharded=sharded)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    samples = int(acc)
+    # per-kernel durations: HIP events around each C-ABI launch, on the launching stream, over
+    # extra eager steps of the same kernels (events cannot bracket single kernels inside a replay)
+    P.ops.TIMER = P.ops.KernelTimer()
+    for _ in range(max(5, args.steps // 4)):
+        scene.step(sharded=sharded)
     timers = P.ops.TIMER.summary()
     P.ops.TIMER = None
     tot = torch.tensor([samples, dt], dtype=torch.float64, device=dev)
@@ -257,6 +293,7 @@ def main():
             "metric": "ray-samples/sec (fwd+bwd) per mapping iter; frames/sec on Replica room0",
             "value": samples_all / dt_max, "unit": "ray-samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt_max / args.steps * 1e3, "higher_is_better": True,
+            "launch_mode": mode,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32 (z, depth, var in f64)",
             "data": "synthetic room0-shaped frames (analytic depth, random colour), seeded random-init decoders",
             "config": {"workload": "Replica room0 mapping iteration, colour stage: 1000 pixels x 48 samples "

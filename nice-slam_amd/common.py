@@ -27,7 +27,8 @@ def random_select(l, k):
 def get_rays_from_uv(i, j, c2w, H, W, fx, fy, cx, cy, device):
     """src/common.py:74-89: dirs=((i-cx)/fx, -(j-cy)/fy, -1); rays_d = R dirs; rays_o = t."""
     if isinstance(c2w, np.ndarray):
-        c2w = torch.from_numpy(c2w).to(device)
+        c2w = torch.from_numpy(c2w)
+    c2w = c2w.to(device)
     dirs = torch.stack([(i - cx) / fx, -(j - cy) / fy, -torch.ones_like(i)], -1).to(device)
     rays_d = torch.sum(dirs[:, None, :] * c2w[:3, :3], -1)
     rays_o = c2w[:3, -1].expand(rays_d.shape)

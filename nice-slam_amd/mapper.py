@@ -146,6 +146,7 @@ class Mapper(object):
         bottom = torch.tensor([[0, 0, 0, 1.0]], dtype=torch.float32, device=device)
         cur_gt_depth = cur_gt_depth.to(device)
         cur_gt_color = cur_gt_color.to(device).float()
+        cur_c2w = cur_c2w.to(device)
 
         if len(keyframe_dict) == 0:
             optimize_frame = []
