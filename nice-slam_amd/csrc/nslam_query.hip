@@ -100,41 +100,67 @@ struct Scratch {
 // only the wave's own LDS counter drained (and a compiler memory barrier), not a workgroup barrier.
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// dW[o][kofs + k] += sum_p sA[p][o] * sX[p][k]   for k < kvalid
-__device__ __forceinline__ void dw_block(float* __restrict__ dst, int ldk, int kofs, int kvalid, const Scratch& S,
+// Parameter-gradient slab of one wave, addressed as a raw buffer: every update is a buffer store
+// (or load + store) with the lane-dependent part of the offset in a VGPR and the uniform part
+// (parameter block, row) in soffset, so the ~350 updates per tile cost one address VGPR per block.
+// A slab address is owned by one lane of one wave, so no atomics: WG == 1 (a wave's only tile)
+// stores, WG == 2 (waves walking several tiles over a zeroed slab) read-modify-writes; both are
+// per-lane program-ordered.
+struct Slab {
+  __amdgpu_buffer_rsrc_t r;
+};
+
+__device__ __forceinline__ Slab make_slab(float* base, int floats) {
+  return Slab{__builtin_amdgcn_make_buffer_rsrc(base, 0, floats * 4, 0x00020000)};
+}
+
+template <int WG>
+__device__ __forceinline__ void put(const Slab& A, int lane_off, int uni_off, float v) {
+  // the b32 intrinsics move raw bits (unsigned): bit-cast, never convert
+  if (WG == 2) v += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(A.r, lane_off * 4, uni_off * 4, 0));
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), A.r, lane_off * 4, uni_off * 4, 0);
+}
+
+// dW[o][kofs + k] += sum_p sA[p][o] * sX[p][k]   for k < kvalid   (dW at slab offset base)
+template <int WG>
+__device__ __forceinline__ void dw_block(const Slab& A, int base, int ldk, int kofs, int kvalid, const Scratch& S,
                                          int lane) {
   const int h = lane >> 5, j = lane & 31;
   f32x16 acc = zero16();
 #pragma unroll
   for (int s = 0; s < 16; ++s) acc = mfma32(S.sA[(2 * s + h) * TPITCH + j], S.sX[(2 * s + h) * TPITCH + j], acc);
   if (j < kvalid) {
+    const int lo = 4 * h * ldk + j;  // fidx(r, h) = (r & 3) + 8 (r >> 2) + 4 h
 #pragma unroll
-    for (int r = 0; r < 16; ++r) atomicAdd(dst + fidx(r, h) * ldk + kofs + j, acc[r]);
+    for (int r = 0; r < 16; ++r) put<WG>(A, lo, base + ((r & 3) + 8 * (r >> 2)) * ldk + kofs, acc[r]);
   }
 }
 
 // db[o] += sum_p sA[p][o]
-__device__ __forceinline__ void db_vec(float* __restrict__ dst, const Scratch& S, int lane) {
+template <int WG>
+__device__ __forceinline__ void db_vec(const Slab& A, int base, const Scratch& S, int lane) {
   const int h = lane >> 5, o = lane & 31;
   float s = 0.f;
 #pragma unroll
   for (int t = 0; t < 16; ++t) s += S.sA[(2 * t + h) * TPITCH + o];
   s += xor32(s);
-  if (h == 0) atomicAdd(dst + o, s);
+  if (h == 0) put<WG>(A, o, base, s);
 }
 
 // sA <- d ; then per input tile: sX <- x ; dW += ...
 __device__ __forceinline__ void wg_begin(const f32x16& d, const Scratch& S, int lane) { tstore(S.sA, d, lane); }
-__device__ __forceinline__ void wg_block(float* __restrict__ dW, int ldk, int kofs, int kvalid, const f32x16& x,
+template <int WG>
+__device__ __forceinline__ void wg_block(const Slab& A, int base, int ldk, int kofs, int kvalid, const f32x16& x,
                                          const Scratch& S, int lane) {
   tstore(S.sX, x, lane);
   lds_sync();
-  dw_block(dW, ldk, kofs, kvalid, S, lane);
+  dw_block<WG>(A, base, ldk, kofs, kvalid, S, lane);
   lds_sync();
 }
-__device__ __forceinline__ void wg_end(float* __restrict__ db, const Scratch& S, int lane) {
+template <int WG>
+__device__ __forceinline__ void wg_end(const Slab& A, int base, const Scratch& S, int lane) {
   lds_sync();
-  db_vec(db, S, lane);
+  db_vec<WG>(A, base, S, lane);
   lds_sync();
 }
 
@@ -205,28 +231,28 @@ __device__ __forceinline__ float out_row(const float* __restrict__ Wo, const flo
 // Parameter gradients (WG) go through LDS transposes + MFMA over the 32 points and are added
 // with atomics shaped as two 128-B row segments.
 // ------------------------------------------------------------------------------------------
-template <int NC, bool WG>
+template <int NC, int WG>
 __device__ __forceinline__ void fc_bwd(const float* __restrict__ pk, const XyzPack& L, int i,
                                        const f32x16 (&cin)[NC], const f32x16& dh, const nslam_dec_grad& dg,
-                                       float* A, const Scratch& S, int lane, f32x16& dc) {
+                                       const Slab& A, const Scratch& S, int lane, f32x16& dc) {
   gemm_acc(dc, pk + L.FCT(i) * NSLAM_FRAG, dh, lane);  // dz_i = dh_i
   if (WG) {
     wg_begin(dh, S, lane);
 #pragma unroll
-    for (int c = 0; c < NC; ++c) wg_block(A + dg.wc[i], 32 * NC, 32 * c, 32, cin[c], S, lane);
-    wg_end(A + dg.bc[i], S, lane);
+    for (int c = 0; c < NC; ++c) wg_block<WG>(A, dg.wc[i], 32 * NC, 32 * c, 32, cin[c], S, lane);
+    wg_end<WG>(A, dg.bc[i], S, lane);
   }
 }
 
-template <int NC, int NOUT, int GOFS, bool WG, bool EMBG>
+template <int NC, int NOUT, int GOFS, int WG, bool EMBG>
 __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const f32x16 (&cin)[NC],
                                              const float x[3], const float (&gall)[4], const nslam_dec_grad& dg,
-                                             float* A, const Scratch& S, int lane, f32x16& dc, float gx[3]) {
+                                             const Slab& A, const Scratch& S, int lane, f32x16& dc, float gx[3]) {
   const XyzPack L{NC};
   const int h = lane >> 5;
   uint32_t m[5];
   f32x16 hs[4];
-  const f32x16 h4 = xyz_forward<NC, WG>(pk, cin, x, lane, m, hs);
+  const f32x16 h4 = xyz_forward<NC, WG != 0>(pk, cin, x, lane, m, hs);
 
   // output layer: dh4 = Wo^T g
   f32x16 dh = zero16();
@@ -249,11 +275,18 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
         s += S.gtab[p * 4 + GOFS + j] * S.sX[p * TPITCH + f];
       }
       s += xor32(s);
-      if (h == 0) atomicAdd(A + dg.wo + 32 * j + f, s);
+      if (h == 0) put<WG>(A, f, dg.wo + 32 * j, s);
       if (lane == 0) {
         float sb = 0.f;
         for (int p = 0; p < 32; ++p) sb += S.gtab[p * 4 + GOFS + j];
-        atomicAdd(A + dg.bo + j, sb);
+        put<WG>(A, 0, dg.bo + j, sb);
+      }
+    }
+    if (WG == 1 && GOFS + NOUT < 4 && GOFS == 0) {  // colour: output row 3 is never used, store zeros
+#pragma unroll
+      for (int j = NOUT; j < 4; ++j) {
+        if (h == 0) put<1>(A, f, dg.wo + 32 * j, 0.f);
+        if (lane == 0) put<1>(A, 0, dg.bo + j, 0.f);
       }
     }
     lds_sync();
@@ -266,8 +299,8 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
   f32x16 da = apply_mask(dh, m[4]);
   if (WG) {
     wg_begin(da, S, lane);
-    wg_block(A + dg.w[4], 32, 0, 32, hs[3], S, lane);
-    wg_end(A + dg.b[4], S, lane);
+    wg_block<WG>(A, dg.w[4], 32, 0, 32, hs[3], S, lane);
+    wg_end<WG>(A, dg.b[4], S, lane);
   }
   dh = zero16();
   gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
@@ -278,9 +311,9 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
     wg_begin(da3, S, lane);
 #pragma unroll
     for (int b = 0; b < 3; ++b)
-      wg_block(A + dg.w[3], 125, 32 * b, b < 2 ? 32 : 29, emb_tile<false>(FB, x, b, lane), S, lane);
-    wg_block(A + dg.w[3], 125, 93, 32, hs[2], S, lane);
-    wg_end(A + dg.b[3], S, lane);
+      wg_block<WG>(A, dg.w[3], 125, 32 * b, b < 2 ? 32 : 29, emb_tile<false>(FB, x, b, lane), S, lane);
+    wg_block<WG>(A, dg.w[3], 125, 93, 32, hs[2], S, lane);
+    wg_end<WG>(A, dg.b[3], S, lane);
   }
   dh = zero16();
   gemm_acc(dh, pk + (L.L3T() + 3) * NSLAM_FRAG, da3, lane);
@@ -289,8 +322,8 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
   da = apply_mask(dh, m[2]);
   if (WG) {
     wg_begin(da, S, lane);
-    wg_block(A + dg.w[2], 32, 0, 32, hs[1], S, lane);
-    wg_end(A + dg.b[2], S, lane);
+    wg_block<WG>(A, dg.w[2], 32, 0, 32, hs[1], S, lane);
+    wg_end<WG>(A, dg.b[2], S, lane);
   }
   dh = zero16();
   gemm_acc(dh, pk + L.L2T() * NSLAM_FRAG, da, lane);
@@ -299,8 +332,8 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
   da = apply_mask(dh, m[1]);
   if (WG) {
     wg_begin(da, S, lane);
-    wg_block(A + dg.w[1], 32, 0, 32, hs[0], S, lane);
-    wg_end(A + dg.b[1], S, lane);
+    wg_block<WG>(A, dg.w[1], 32, 0, 32, hs[0], S, lane);
+    wg_end<WG>(A, dg.b[1], S, lane);
   }
   dh = zero16();
   gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
@@ -311,8 +344,8 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
     wg_begin(da, S, lane);
 #pragma unroll
     for (int b = 0; b < 3; ++b)
-      wg_block(A + dg.w[0], 93, 32 * b, b < 2 ? 32 : 29, emb_tile<false>(FB, x, b, lane), S, lane);
-    wg_end(A + dg.b[0], S, lane);
+      wg_block<WG>(A, dg.w[0], 93, 32 * b, b < 2 ? 32 : 29, emb_tile<false>(FB, x, b, lane), S, lane);
+    wg_end<WG>(A, dg.b[0], S, lane);
   }
 
   // Fourier features: de_b = L3T_b da3 + L0T_b da0 ; G = de * cos(theta)
@@ -356,7 +389,7 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int k = 32 * b + fidx(r, h);
-            if (k < NSLAM_EMB) atomicAdd(A + dg.B + jj * NSLAM_EMB + k, acc[r]);
+            if (k < NSLAM_EMB) put<WG>(A, jj * NSLAM_EMB + 4 * h, dg.B + 32 * b + (r & 3) + 8 * (r >> 2), acc[r]);
           }
         }
         lds_sync();
@@ -401,15 +434,15 @@ __device__ __forceinline__ f32x16 noxyz_forward(const float* __restrict__ pk, co
   return relu16(a);
 }
 
-template <bool WG>
+template <int WG>
 __device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, const f32x16& c, float g,
-                                               const nslam_dec_grad& dg, float* A, const Scratch& S, int lane,
+                                               const nslam_dec_grad& dg, const Slab& A, const Scratch& S, int lane,
                                                f32x16& dc) {
   const NoXyzPack L;
   const int h = lane >> 5;
   uint32_t m[5];
   f32x16 hs[4];
-  const f32x16 h4 = noxyz_forward<WG>(pk, c, lane, m, hs);
+  const f32x16 h4 = noxyz_forward<WG != 0>(pk, c, lane, m, hs);
   f32x16 dh;
   {
     const f32x16 w = vec_tile(pk + L.Wo(), lane);
@@ -427,11 +460,11 @@ __device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, con
       s += S.gtab[p * 4 + 3] * S.sX[p * TPITCH + f];
     }
     s += xor32(s);
-    if (h == 0) atomicAdd(A + dg.wo + f, s);
+    if (h == 0) put<WG>(A, f, dg.wo, s);
     if (lane == 0) {
       float sb = 0.f;
       for (int p = 0; p < 32; ++p) sb += S.gtab[p * 4 + 3];
-      atomicAdd(A + dg.bo, sb);
+      put<WG>(A, 0, dg.bo, sb);
     }
     lds_sync();
   }
@@ -440,8 +473,8 @@ __device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, con
   f32x16 da = apply_mask(dh, m[4]);
   if (WG) {
     wg_begin(da, S, lane);
-    wg_block(A + dg.w[4], 32, 0, 32, hs[3], S, lane);
-    wg_end(A + dg.b[4], S, lane);
+    wg_block<WG>(A, dg.w[4], 32, 0, 32, hs[3], S, lane);
+    wg_end<WG>(A, dg.b[4], S, lane);
   }
   dh = zero16();
   gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
@@ -449,9 +482,9 @@ __device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, con
   da = apply_mask(dh, m[3]);
   if (WG) {
     wg_begin(da, S, lane);
-    wg_block(A + dg.w[3], 64, 0, 32, c, S, lane);
-    wg_block(A + dg.w[3], 64, 32, 32, hs[2], S, lane);
-    wg_end(A + dg.b[3], S, lane);
+    wg_block<WG>(A, dg.w[3], 64, 0, 32, c, S, lane);
+    wg_block<WG>(A, dg.w[3], 64, 32, 32, hs[2], S, lane);
+    wg_end<WG>(A, dg.b[3], S, lane);
   }
   gemm_acc(dc, pk + L.L3T() * NSLAM_FRAG, da, lane);
   dh = zero16();
@@ -460,8 +493,8 @@ __device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, con
   da = apply_mask(dh, m[2]);
   if (WG) {
     wg_begin(da, S, lane);
-    wg_block(A + dg.w[2], 32, 0, 32, hs[1], S, lane);
-    wg_end(A + dg.b[2], S, lane);
+    wg_block<WG>(A, dg.w[2], 32, 0, 32, hs[1], S, lane);
+    wg_end<WG>(A, dg.b[2], S, lane);
   }
   dh = zero16();
   gemm_acc(dh, pk + L.L2T() * NSLAM_FRAG, da, lane);
@@ -469,8 +502,8 @@ __device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, con
   da = apply_mask(dh, m[1]);
   if (WG) {
     wg_begin(da, S, lane);
-    wg_block(A + dg.w[1], 32, 0, 32, hs[0], S, lane);
-    wg_end(A + dg.b[1], S, lane);
+    wg_block<WG>(A, dg.w[1], 32, 0, 32, hs[0], S, lane);
+    wg_end<WG>(A, dg.b[1], S, lane);
   }
   dh = zero16();
   gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
@@ -478,8 +511,8 @@ __device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, con
   da = apply_mask(dh, m[0]);
   if (WG) {
     wg_begin(da, S, lane);
-    wg_block(A + dg.w[0], 32, 0, 32, c, S, lane);
-    wg_end(A + dg.b[0], S, lane);
+    wg_block<WG>(A, dg.w[0], 32, 0, 32, c, S, lane);
+    wg_end<WG>(A, dg.b[0], S, lane);
   }
   gemm_acc(dc, pk + L.L0T() * NSLAM_FRAG, da, lane);
 }
@@ -619,15 +652,18 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd(QueryKArgs a) {
 // One backward launch per decoder: the decoder's forward is recomputed, its grid gradient is
 // scattered, its parameter gradients are accumulated and its share of d/dpts is added into g_pts
 // (launches on one stream are ordered and each point is owned by one lane pair: plain
-// read-modify-write, no atomics).  A workgroup holds WAVES waves; each wave walks tiles.  With
-// parameter gradients (WG) the workgroup accumulates them in LDS (ds_add_f32) over all its tiles
-// and writes one partial slab; k_slab_reduce sums the slabs in a fixed order (deterministic).
+// read-modify-write, no atomics).  With parameter gradients every wave owns a slab of the
+// workspace (WG == 1: one tile per wave, slab = tile; WG == 2: a fixed number of waves walk the
+// tiles over pre-zeroed slabs) and k_slab_reduce sums the slabs in a fixed order
+// (deterministic).  LDS holds only each wave's transpose scratch: LDS float atomics
+// (ds_add_f32, one RMW per lane) were the bottleneck of the previous shared-accumulator design.
 constexpr int kScratchFloats = 2 * TILE_FLOATS + 32 * 4 + 32 * 3 + 32 * 8 * 2;
+constexpr int kWavesBwd = 4;
+constexpr int kMaxSlabs = 4096;  // WG == 2 above this many tiles
 
-template <int DEC, bool WG, bool PG, bool FIRST>
-__device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, float* A, const Scratch& S,
-                                             int lane) {
-  // Every LDS-accumulator / scratch address is a function of the lane only, i.e. invariant across
+template <int DEC, int WG, bool PG, bool FIRST>
+__device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, const Slab& A, const Scratch& S,
+                                             int lane) {  // Every LDS-accumulator / scratch address is a function of the lane only, i.e. invariant across
   // the tile loop; letting LICM hoist the ~300 of them pins (and spills) the register file.
   // Re-derive them per tile.
   asm volatile("" : "+v"(lane));
@@ -688,12 +724,12 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
   }
 }
 
-template <int DEC, bool WG, bool PG, bool FIRST, int WAVES>
-__global__ __launch_bounds__(64 * WAVES, 2) void k_dec_bwd(QueryKArgs a, float* __restrict__ slab, int acc_floats) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
+template <int DEC, int WG, bool PG, bool FIRST>
+__global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd(QueryKArgs a, float* __restrict__ slab,
+                                                                 int acc_floats) {
+  __shared__ __attribute__((aligned(16))) float lds[kWavesBwd * kScratchFloats];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float* A = lds;  // parameter-gradient accumulator (WG only)
-  float* sc = lds + (WG ? acc_floats : 0) + wave * kScratchFloats;
+  float* sc = lds + wave * kScratchFloats;
   Scratch S;
   S.sA = sc;
   S.sX = sc + TILE_FLOATS;
@@ -701,44 +737,38 @@ __global__ __launch_bounds__(64 * WAVES, 2) void k_dec_bwd(QueryKArgs a, float* 
   S.xtab = S.gtab + 32 * 4;
   S.crow = reinterpret_cast<int*>(S.xtab + 32 * 3);
   S.cw = reinterpret_cast<float*>(S.crow + 32 * 8);
-  if (WG) {
-    for (int i = threadIdx.x; i < acc_floats; i += blockDim.x) A[i] = 0.f;
-    __syncthreads();
-  }
   const int64_t ntiles = (a.n + 31) / 32;
-  if (!WG) {  // one tile per wave (grid covers all tiles)
-    const int64_t tile = (int64_t)blockIdx.x * WAVES + wave;
-    if (tile < ntiles) dec_bwd_tile<DEC, WG, PG, FIRST>(a, tile, A, S, lane);
+  const int64_t w = (int64_t)blockIdx.x * kWavesBwd + wave;
+  const Slab A = make_slab(WG ? slab + (size_t)w * acc_floats : slab, WG ? acc_floats : 0);
+  if (WG != 2) {  // one tile per wave (grid covers all tiles)
+    if (w < ntiles) dec_bwd_tile<DEC, WG, PG, FIRST>(a, w, A, S, lane);
     return;
   }
 #pragma nounroll
-  for (int64_t tile = (int64_t)blockIdx.x * WAVES + wave; tile < ntiles; tile += (int64_t)gridDim.x * WAVES)
+  for (int64_t tile = w; tile < ntiles; tile += (int64_t)gridDim.x * kWavesBwd)
     dec_bwd_tile<DEC, WG, PG, FIRST>(a, tile, A, S, lane);
-  if (WG) {
-    __syncthreads();
-    float* dst = slab + (size_t)blockIdx.x * acc_floats;
-    for (int i = threadIdx.x; i < acc_floats; i += blockDim.x) dst[i] = A[i];
-  }
 }
 
-// base[j] += sum_b slab[b][j].  A workgroup owns 64 parameters; each of its 16 waves sums every
-// 16th slab and the 16 partials are combined in LDS in a fixed order: deterministic, with 16x the
-// memory-level parallelism of a one-thread-per-parameter loop.
-__global__ __launch_bounds__(1024) void k_slab_reduce(const float* __restrict__ slab, int nslab, int acc_floats,
+// base[j] += sum_b slab[b][j].  A workgroup owns 256 parameters (float4 per lane); each of its 16
+// waves sums every 16th slab and the 16 partials are combined in LDS in a fixed order:
+// deterministic, with 16x the memory-level parallelism of a one-thread-per-parameter loop.
+__global__ __launch_bounds__(1024) void k_slab_reduce(const float* __restrict__ slab, int64_t nslab, int acc_floats,
                                                       int count, float* __restrict__ base) {
-  __shared__ float part[16][64];
+  __shared__ f32x4 part[16][64];
   const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int j = blockIdx.x * 64 + c;
-  float s = 0.f;
+  const int j = (blockIdx.x * 64 + c) * 4;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
   if (j < count)
-    for (int b = g; b < nslab; b += 16) s += slab[(size_t)b * acc_floats + j];
+    for (int64_t b = g; b < nslab; b += 16) s += *reinterpret_cast<const f32x4*>(slab + b * acc_floats + j);
   part[g][c] = s;
   __syncthreads();
   if (g == 0 && j < count) {
-    float t = part[0][c];
+    f32x4 t = part[0][c];
 #pragma unroll
     for (int k = 1; k < 16; ++k) t += part[k][c];
-    base[j] += t;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (j + e < count) base[j + e] += t[e];
   }
 }
 
@@ -789,63 +819,54 @@ extern "C" int nslam_query_fwd(const nslam_query_cfg* cfg, const double* pts, in
 
 namespace {
 
-constexpr int kWavesNoWG = 4;
-constexpr int kMaxLdsBytes = 160 * 1024;
-
 int acc_floats_of(const nslam_dec_grad& dg) { return (int)((dg.count + 3) & ~int64_t(3)); }
 
-// waves per workgroup for the parameter-gradient kernels: as many as the LDS leaves room for
-int waves_wg(int acc_floats) {
-  const int per_wave = kScratchFloats * (int)sizeof(float);
-  int w = (kMaxLdsBytes - acc_floats * (int)sizeof(float)) / per_wave;
-  return w >= 8 ? 8 : (w >= 6 ? 6 : (w >= 4 ? 4 : w));
+// Slab cap: kMaxSlabs, or NSLAM_MAX_SLABS from the environment (tests use it to reach the
+// multi-tile read-modify-write mode at small sizes).
+int64_t max_slabs() {
+  const char* e = getenv("NSLAM_MAX_SLABS");
+  const long v = e ? strtol(e, nullptr, 10) : 0;
+  return v > 0 ? v : kMaxSlabs;
 }
 
-int64_t wg_blocks(int64_t tiles, int waves) {
-  const int64_t b = (tiles + waves - 1) / waves;
-  return b < 256 ? b : 256;  // one workgroup per CU (LDS-bound); tiles beyond are walked in-kernel
+// parameter-gradient slabs for a decoder: one per tile up to the cap, else one per launched wave
+// (the cap rounded up to whole workgroups), each wave walking tiles with grid stride
+int64_t n_slabs(int64_t tiles) {
+  const int64_t cap = max_slabs();
+  return tiles <= cap ? tiles : (cap + kWavesBwd - 1) / kWavesBwd * kWavesBwd;
 }
 
-template <int DEC, bool WG, bool PG, bool FIRST, int WAVES>
+template <int DEC, int WG, bool PG, bool FIRST>
 int launch_one(const QueryKArgs& a, float* slab, int acc, int64_t blocks, hipStream_t s) {
-  const size_t lds = ((WG ? acc : 0) + (size_t)WAVES * kScratchFloats) * sizeof(float);
-  auto kern = k_dec_bwd<DEC, WG, PG, FIRST, WAVES>;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lds) != hipSuccess)
-    return hip_status();
-  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(64 * WAVES), lds, s, a, slab, acc);
+  hipLaunchKernelGGL((k_dec_bwd<DEC, WG, PG, FIRST>), dim3((unsigned)blocks), dim3(64 * kWavesBwd), 0, s, a, slab,
+                     acc);
   return hip_status();
 }
 
-template <int DEC, bool WG, bool PG>
+template <int DEC, int WG, bool PG>
 int launch_dec_bwd(const QueryKArgs& a, bool first, float* slab, hipStream_t s) {
   const int64_t tiles = (a.n + 31) / 32;
-  if (!WG) {
-    const int64_t blocks = (tiles + kWavesNoWG - 1) / kWavesNoWG;
-    return first ? launch_one<DEC, false, PG, true, kWavesNoWG>(a, nullptr, 0, blocks, s)
-                 : launch_one<DEC, false, PG, false, kWavesNoWG>(a, nullptr, 0, blocks, s);
+  if (WG == 0) {
+    const int64_t blocks = (tiles + kWavesBwd - 1) / kWavesBwd;
+    return first ? launch_one<DEC, 0, PG, true>(a, nullptr, 0, blocks, s)
+                 : launch_one<DEC, 0, PG, false>(a, nullptr, 0, blocks, s);
   }
   const nslam_dec_grad& dg = a.c.dgrad[DEC];
   const int acc = acc_floats_of(dg);
-  const int w = waves_wg(acc);
+  const int64_t nslab = n_slabs(tiles);
+  const int64_t blocks = (nslab + kWavesBwd - 1) / kWavesBwd;
   int rc;
-  if (w == 8) {
-    const int64_t blocks = wg_blocks(tiles, 8);
-    rc = first ? launch_one<DEC, true, PG, true, 8>(a, slab, acc, blocks, s)
-               : launch_one<DEC, true, PG, false, 8>(a, slab, acc, blocks, s);
-    if (rc) return rc;
-    hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((dg.count + 63) / 64)), dim3(1024), 0, s, slab, (int)blocks,
-                       acc, (int)dg.count, dg.base);
-  } else if (w >= 4) {
-    const int64_t blocks = wg_blocks(tiles, 4);
-    rc = first ? launch_one<DEC, true, PG, true, 4>(a, slab, acc, blocks, s)
-               : launch_one<DEC, true, PG, false, 4>(a, slab, acc, blocks, s);
-    if (rc) return rc;
-    hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((dg.count + 63) / 64)), dim3(1024), 0, s, slab, (int)blocks,
-                       acc, (int)dg.count, dg.base);
+  if (tiles <= max_slabs()) {
+    rc = first ? launch_one<DEC, 1, PG, true>(a, slab, acc, blocks, s)
+               : launch_one<DEC, 1, PG, false>(a, slab, acc, blocks, s);
   } else {
-    return NSLAM_EUNSUPPORTED;
+    if (hipMemsetAsync(slab, 0, (size_t)nslab * acc * sizeof(float), s) != hipSuccess) return hip_status();
+    rc = first ? launch_one<DEC, 2, PG, true>(a, slab, acc, blocks, s)
+               : launch_one<DEC, 2, PG, false>(a, slab, acc, blocks, s);
   }
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((dg.count + 255) / 256)), dim3(1024), 0, s, slab, nslab, acc,
+                     (int)dg.count, dg.base);
   return hip_status();
 }
 
@@ -853,10 +874,10 @@ template <int DEC>
 int dispatch_dec_bwd(const QueryKArgs& a, bool first, float* slab, hipStream_t s) {
   const bool wg = a.c.dgrad[DEC].base != nullptr;
   const bool pg = a.c.need_pts_grad != 0;
-  if (wg && pg) return launch_dec_bwd<DEC, true, true>(a, first, slab, s);
-  if (wg) return launch_dec_bwd<DEC, true, false>(a, first, slab, s);
-  if (pg) return launch_dec_bwd<DEC, false, true>(a, first, slab, s);
-  return launch_dec_bwd<DEC, false, false>(a, first, slab, s);
+  if (wg && pg) return launch_dec_bwd<DEC, 1, true>(a, first, slab, s);
+  if (wg) return launch_dec_bwd<DEC, 1, false>(a, first, slab, s);
+  if (pg) return launch_dec_bwd<DEC, 0, true>(a, first, slab, s);
+  return launch_dec_bwd<DEC, 0, false>(a, first, slab, s);
 }
 
 size_t bwd_ws_bytes(const nslam_query_cfg* cfg, int64_t n_pts) {
@@ -865,9 +886,7 @@ size_t bwd_ws_bytes(const nslam_query_cfg* cfg, int64_t n_pts) {
   for (int d = 0; d < 4; ++d) {
     const nslam_dec_grad& dg = cfg->dgrad[d];
     if (!dg.base || dg.count <= 0) continue;
-    const int acc = acc_floats_of(dg);
-    const int w = waves_wg(acc) >= 8 ? 8 : 4;
-    const size_t b = (size_t)wg_blocks(tiles, w) * acc * sizeof(float);
+    const size_t b = (size_t)n_slabs(tiles) * acc_floats_of(dg) * sizeof(float);
     need = b > need ? b : need;  // decoders run one after the other on the stream: one region
   }
   return need;
@@ -888,7 +907,7 @@ extern "C" int nslam_query_bwd(const nslam_query_cfg* cfg, const double* pts, in
   if (cfg->need_pts_grad && n_pts > 0 && !g_pts) return NSLAM_EINVAL;
   if (n_pts == 0) return NSLAM_OK;
   for (int d = 0; d < 4; ++d)
-    if (cfg->dgrad[d].base && (cfg->dgrad[d].count <= 0 || waves_wg(acc_floats_of(cfg->dgrad[d])) < 4))
+    if (cfg->dgrad[d].base && cfg->dgrad[d].count <= 0)
       return NSLAM_EUNSUPPORTED;
   if (ws_bytes < bwd_ws_bytes(cfg, n_pts) || (bwd_ws_bytes(cfg, n_pts) > 0 && !ws)) return NSLAM_EWORKSPACE;
   QueryKArgs a{*cfg, pts, n_pts, nullptr, g_raw, g_pts};

@@ -188,6 +188,14 @@ def test_render_batch_ray_matches_golden(pkg, dev, tiny, stage):
     assert ok, json.dumps(REPORT[case], indent=1)
 
 
+
+@pytest.mark.parametrize("stage", ["coarse", "fine", "color"])
+def test_render_batch_ray_rmw_slabs(pkg, dev, tiny, stage, monkeypatch):
+    """Same parity with the parameter-gradient slab count capped at 3, so each wave walks several
+    tiles and accumulates by read-modify-write (the mode used above 4096 tiles)."""
+    monkeypatch.setenv("NSLAM_MAX_SLABS", "3")
+    test_render_batch_ray_matches_golden(pkg, dev, tiny, stage)
+
 def test_room0_color_stage_matches_golden(pkg, dev, room0):
     gen = torch.Generator().manual_seed(7)
     bound = orc.enlarge_bound([[-2.9, 8.9], [-3.2, 5.5], [-3.5, 3.3]], 0.32)
