@@ -67,7 +67,7 @@ def rot(yaw, pitch):
 class Room0Scene:
     """Synthetic room0-shaped mapping workload (grids, decoders, 5 keyframes in HBM)."""
 
-    def __init__(self, dev, rank=0, cfg=ROOM0):
+    def __init__(self, dev, rank=0, cfg=ROOM0, path="fused"):
         P = pkg()
         self.cfg, self.dev = cfg, dev
         g = torch.Generator().manual_seed(2)
@@ -119,12 +119,30 @@ class Room0Scene:
         self.color = torch.rand(F, H, W, 3, device=dev, generator=gd)
         self.dirs = dirs.reshape(-1, 3)
         torch.cuda.manual_seed(1000 + rank)  # pixel draws use the (graph-safe) default generator
-        params = [{"params": list(self.nice.color_decoder.parameters()), "lr": cfg["lr"]["decoders"]},
-                  {"params": [self.grids["grid_middle"]], "lr": cfg["lr"]["middle"]},
-                  {"params": [self.grids["grid_fine"]], "lr": cfg["lr"]["fine"]},
-                  {"params": [self.grids["grid_color"]], "lr": cfg["lr"]["color"]}]
-        self.opt = torch.optim.Adam(params, fused=True, capturable=True)
         self.bound_dev = self.bound.to(dev)
+        self.frames = [(self.depth[f], self.color[f], self.c2w[f]) for f in range(F)]
+        # frustum_feature_selection (Mapper.py:314-333): voxels seen by the current frame (frame 0)
+        self.rows = {}
+        for k in ("grid_middle", "grid_fine", "grid_color"):
+            m = P.mapper.frustum_mask(self.c2w[0], k, self.grids[k].shape[2:], self.depth[0], self.bound, H, W,
+                                      cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"])
+            self.rows[k] = P.engine.frustum_rows(m)
+        self.path = path
+        if path == "fused":
+            for t in self.grids.values():
+                t.requires_grad_(False)
+            self.engine = P.engine.MappingEngine(self.nice, self.grids, self.bound, cfg["n_strat"], cfg["n_surf"],
+                                                 w_color=cfg["w_color"], device=dev)
+            self.opt = P.ops.FusedAdam(
+                [{"params": [self.engine.decs["color"].param], "lr": cfg["lr"]["decoders"]}] +
+                [{"params": [self.grids[k]], "lr": cfg["lr"][k[5:]], "rows": self.rows[k]}
+                 for k in ("grid_middle", "grid_fine", "grid_color")])
+        else:
+            params = [{"params": list(self.nice.color_decoder.parameters()), "lr": cfg["lr"]["decoders"]},
+                      {"params": [self.grids["grid_middle"]], "lr": cfg["lr"]["middle"]},
+                      {"params": [self.grids["grid_fine"]], "lr": cfg["lr"]["fine"]},
+                      {"params": [self.grids["grid_color"]], "lr": cfg["lr"]["color"]}]
+            self.opt = torch.optim.Adam(params, fused=True, capturable=True)
 
     def sample_batch(self):
         """get_samples over the window (Mapper.py:437-467): 200 random pixels per frame."""
@@ -140,7 +158,23 @@ class Room0Scene:
         return rays_o, rays_d, depth, color
 
     def step(self, stage="color", sharded=False):
-        """One mapping iteration with no host synchronisation (hipGraph-capturable).
+        """One colour-stage mapping iteration, no host synchronisation (hipGraph-capturable);
+        returns the number of kept ray-samples (device tensor)."""
+        if self.path != "fused":
+            return self.step_autograd(stage, sharded)
+        cfg = self.cfg
+        D = pkg().distributed
+        F, H, W = cfg["window"], cfg["H"], cfg["W"]
+        n = cfg["pixels"] // F
+        pix = torch.randint(H * W, (F * n,), device=self.dev)
+        _, keep = self.engine.iteration(
+            stage, self.frames, pix, n, (H, W), (cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"]), self.opt,
+            trainable_decoders=("color",), gt_max=(lambda g: D.global_max(g)) if sharded else None,
+            allreduce=(lambda gs: D.allreduce_tensors(gs)) if sharded else None)
+        return keep.sum() * (cfg["n_strat"] + cfg["n_surf"])
+
+    def step_autograd(self, stage="color", sharded=False):
+        """The same iteration through the autograd drop-in path (dense Adam, torch glue ops).
 
         The inside-mask prefilter (Mapper.py:469-481) removes rays; here they stay in the batch
         with zero loss weight (their gradients are exactly zero) and the sampler's batch-global
@@ -215,6 +249,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture")
+    ap.add_argument("--path", choices=("fused", "autograd"), default="fused",
+                    help="fused engine (default) or the autograd drop-in path")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -224,7 +260,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     P = pkg()
-    scene = Room0Scene(dev, rank)
+    scene = Room0Scene(dev, rank, path=args.path)
     sharded = world > 1
     for _ in range(args.warmup):
         scene.step(sharded=sharded)

@@ -76,6 +76,13 @@ typedef struct nslam_query_cfg {
   nslam_grid grid[4];       /* indexed by NSLAM_DEC_*                                     */
   const float* packed[4];   /* packed decoder weights (nslam_pack_layout), NULL if unused */
   nslam_dec_grad dgrad[4];  /* parameter-gradient destinations                            */
+  /* Ray form of the point list (ABI v4): when rays_o != NULL the points are generated in-kernel
+   * as pts[r*S + s] = rays_o[r] + rays_d[r] * z_vals[r][s] in float64 (Renderer.py:172-174,
+   * float32 rays promoted), the `pts` argument is ignored and need_pts_grad must be 0. */
+  const float* rays_o;      /* [M/S][3] float32 */
+  const float* rays_d;      /* [M/S][3] float32 */
+  const double* z_vals;     /* [M/S][S] float64 */
+  int64_t n_samples;        /* S */
 } nslam_query_cfg;
 
 /* ---- packing ------------------------------------------------------------------------------
@@ -130,6 +137,77 @@ int nslam_grid_sample_fwd(const float* grid, const int32_t* dims, const float* c
  * `dims` (Z, Y, X) is a HOST pointer in both grid_sample entry points. */
 int nslam_grid_sample_bwd(const float* grid, const int32_t* dims, const float* coords, int64_t n,
                           const float* grad_out, float* grad_grid, float* grad_coords, void* stream);
+
+/* ---- mapping / tracking iteration (ABI v4) ------------------------------------------------ */
+#define NSLAM_MAX_FRAMES 32
+
+/* One RGB-D frame resident on the device (keyframe_dict entry / current frame). */
+typedef struct nslam_frame {
+  const float* depth; /* [H][W] float32                              */
+  const float* color; /* [H][W][3] float32                           */
+  const float* c2w;   /* [3 or 4][4] float32 row-major camera-to-world */
+} nslam_frame;
+
+/* get_samples (src/common.py:92-134: get_sample_uv + select_uv + get_rays_from_uv) for
+ * n_frames frames (HOST array, <= NSLAM_MAX_FRAMES) x n_per pixels each, plus the inside-mask
+ * prefilter of Mapper.py:469-481 / Tracker.py:93-104.  pix[f*n_per + k] is select_uv's randint
+ * index into the frame's window [h0,h1) x [w0,w1) (row-major over the window).  Outputs are
+ * [n_frames*n_per] rays in frame order.  With bound_lo/bound_hi (HOST, float64 [3]) a ray whose
+ * bound-exit distance is < gt depth gets keep = 0 and gt_depth = 0 (it then contributes nothing:
+ * the prefilter removes it in the reference); NULL bounds keep every ray. */
+int nslam_gather_rays(const nslam_frame* frames, int32_t n_frames, int64_t n_per, const int64_t* pix,
+                      int32_t H, int32_t W, int32_t h0, int32_t h1, int32_t w0, int32_t w1, float fx, float fy,
+                      float cx, float cy, const double* bound_lo, const double* bound_hi, float* rays_o,
+                      float* rays_d, float* gt_depth, float* gt_color, uint8_t* keep, void* stream);
+
+/* Rendering loss fused with compositing and its backward (the loss is a sum of per-ray terms).
+ *   mode NSLAM_LOSS_MAPPER (Mapper.py:487-501):
+ *     L = sum_{keep, gt>0} |gt - depth| + [use_color] w_color * sum_{keep} |gt_c - color|
+ *   mode NSLAM_LOSS_TRACKER (Tracker.py:110-123), u = var (detached):
+ *     r = |gt - depth| / sqrt(u + 1e-10);  m = keep & gt>0 [& r < 10 median_{keep}(r) if handle_dynamic]
+ *     L = sum_m r + [use_color] w_color * sum_m |gt_c - color|
+ * Writes depth/var (float64 [N]) and color (float32 [N][3]) like nslam_composite_fwd, the
+ * per-ray loss terms ray_loss (float64 [N], may be NULL) and, when g_raw != NULL, dL/draw
+ * [N][S][4] for dL = 1.  keep may be NULL (all rays kept).  The tracker's median needs
+ * N <= 16384 rays. ws: nslam_render_loss_workspace_size bytes. */
+enum { NSLAM_LOSS_MAPPER = 0, NSLAM_LOSS_TRACKER = 1 };
+typedef struct nslam_loss_cfg {
+  int32_t mode;
+  int32_t use_color;
+  int32_t handle_dynamic;
+  float w_color;
+} nslam_loss_cfg;
+int nslam_render_loss(const nslam_loss_cfg* cfg, const float* raw, const double* z_vals, int64_t n_rays,
+                      int32_t n_samples, const float* gt_depth, const float* gt_color, const uint8_t* keep,
+                      double* depth, double* var, float* color, double* ray_loss, float* g_raw, void* ws,
+                      size_t ws_bytes, void* stream);
+size_t nslam_render_loss_workspace_size(const nslam_loss_cfg* cfg, int64_t n_rays);
+
+/* Adam (torch.optim.Adam, weight_decay 0, amsgrad off: Tracker.py:126, Mapper.py:504) over up to
+ * NSLAM_ADAM_MAX_SEGS parameter segments in one launch.  A segment is dense (rows == NULL: n
+ * floats) or row-masked (n row indices of row_len floats each, row_len % 4 == 0 and 16-byte
+ * aligned param/grad/state): the frustum-selected voxels of a channels-last grid
+ * (Mapper.py:314-333), updated in place in the dense grid with state for the selected rows only
+ * (exp_avg/exp_avg_sq are [n][row_len], in row-list order).  Like torch, every segment has its
+ * own step count (`step`, a device float, 0 before the first update): the launch uses step+1
+ * and the last workgroup to finish advances every segment's step (graph-replay safe); `ticket`
+ * is a device uint32 the caller zero-initialises once.  Pass only segments that have a gradient
+ * this iteration (torch skips parameters whose .grad is None).  With zero_grad the grad entries
+ * read are reset to 0. */
+#define NSLAM_ADAM_MAX_SEGS 16
+typedef struct nslam_adam_seg {
+  float* param;
+  float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  float* step;
+  const int32_t* rows;
+  int64_t n;
+  int32_t row_len;
+  float lr;
+} nslam_adam_seg;
+int nslam_adam_step(const nslam_adam_seg* segs, int32_t n_segs, float beta1, float beta2, float eps,
+                    int32_t zero_grad, uint32_t* ticket, void* stream);
 
 enum { NSLAM_WS_SAMPLER = 0 };
 size_t nslam_workspace_size(int which, int64_t n);

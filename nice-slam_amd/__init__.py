@@ -7,7 +7,7 @@ The directory name is not a Python identifier: import with importlib.import_modu
 """
 import sys as _sys
 
-from . import _lib, common, config, decoder, distributed, mapper, ops, packing, renderer, slam, tracker  # noqa: F401
+from . import _lib, common, config, decoder, distributed, engine, mapper, ops, packing, renderer, slam, tracker  # noqa: F401
 from .decoder import NICE, MLP, MLP_no_xyz  # noqa: F401
 from .mapper import Mapper  # noqa: F401
 from .renderer import Renderer  # noqa: F401

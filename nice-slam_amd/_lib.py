@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libnslam.so")
 
 NSLAM_OK = 0
-ABI_VERSION = 3
+ABI_VERSION = 4
 STAGES = {"coarse": 0, "middle": 1, "fine": 2, "color": 3}
 DEC_COARSE, DEC_MIDDLE, DEC_FINE, DEC_COLOR = 0, 1, 2, 3
 
@@ -55,6 +55,38 @@ class NslamQueryCfg(ctypes.Structure):
         ("grid", NslamGrid * 4),
         ("packed", ctypes.c_void_p * 4),
         ("dgrad", NslamDecGrad * 4),
+        ("rays_o", ctypes.c_void_p),
+        ("rays_d", ctypes.c_void_p),
+        ("z_vals", ctypes.c_void_p),
+        ("n_samples", ctypes.c_int64),
+    ]
+
+
+MAX_FRAMES = 32
+ADAM_MAX_SEGS = 16
+LOSS_MAPPER, LOSS_TRACKER = 0, 1
+
+
+class NslamFrame(ctypes.Structure):
+    _fields_ = [("depth", ctypes.c_void_p), ("color", ctypes.c_void_p), ("c2w", ctypes.c_void_p)]
+
+
+class NslamLossCfg(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_int32), ("use_color", ctypes.c_int32), ("handle_dynamic", ctypes.c_int32),
+                ("w_color", ctypes.c_float)]
+
+
+class NslamAdamSeg(ctypes.Structure):
+    _fields_ = [
+        ("param", ctypes.c_void_p),
+        ("grad", ctypes.c_void_p),
+        ("exp_avg", ctypes.c_void_p),
+        ("exp_avg_sq", ctypes.c_void_p),
+        ("step", ctypes.c_void_p),
+        ("rows", ctypes.c_void_p),
+        ("n", ctypes.c_int64),
+        ("row_len", ctypes.c_int32),
+        ("lr", ctypes.c_float),
     ]
 
 
@@ -62,7 +94,8 @@ class NslamQueryCfg(ctypes.Structure):
 EXPORTS = (
     "nslam_pack_layout", "nslam_sample_rays", "nslam_query_fwd", "nslam_query_bwd", "nslam_query_bwd_workspace_size",
     "nslam_composite_fwd", "nslam_composite_bwd", "nslam_grid_sample_fwd", "nslam_grid_sample_bwd",
-    "nslam_workspace_size", "nslam_strerror", "nslam_abi_version",
+    "nslam_workspace_size", "nslam_strerror", "nslam_abi_version", "nslam_gather_rays", "nslam_render_loss",
+    "nslam_render_loss_workspace_size", "nslam_adam_step",
 )
 
 _lib = None
@@ -93,6 +126,14 @@ def lib():
         L.nslam_strerror.argtypes = [ctypes.c_int]
         L.nslam_strerror.restype = ctypes.c_char_p
         L.nslam_abi_version.restype = ctypes.c_int
+        f32 = ctypes.c_float
+        L.nslam_gather_rays.argtypes = [ctypes.POINTER(NslamFrame), i32, i64, vp, i32, i32, i32, i32, i32, i32,
+                                        f32, f32, f32, f32, dp, dp, vp, vp, vp, vp, vp, vp]
+        L.nslam_render_loss.argtypes = [ctypes.POINTER(NslamLossCfg), vp, vp, i64, i32, vp, vp, vp, vp, vp, vp, vp,
+                                        vp, vp, sz, vp]
+        L.nslam_render_loss_workspace_size.argtypes = [ctypes.POINTER(NslamLossCfg), i64]
+        L.nslam_render_loss_workspace_size.restype = sz
+        L.nslam_adam_step.argtypes = [ctypes.POINTER(NslamAdamSeg), i32, f32, f32, f32, i32, vp, vp]
         if L.nslam_abi_version() != ABI_VERSION:
             raise RuntimeError(f"libnslam.so ABI {L.nslam_abi_version()} != {ABI_VERSION}: rebuild it")
         _lib = L

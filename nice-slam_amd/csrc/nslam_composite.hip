@@ -117,31 +117,11 @@ __global__ __launch_bounds__(256) void k_composite_fwd(const float* __restrict__
   }
 }
 
-__global__ __launch_bounds__(256) void k_composite_bwd(const float* __restrict__ raw, const double* __restrict__ zv,
-                                                       int64_t n, int S, const double* __restrict__ gdep,
-                                                       const double* __restrict__ gvar,
-                                                       const float* __restrict__ gcol, float* __restrict__ graw) {
-  const int lane = threadIdx.x & 63;
-  const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (ray >= n) return;
-  const float* rr = raw + ray * (int64_t)S * 4;
-  const double* zz = zv + ray * (int64_t)S;
-  const int nch = (S + 63) / 64;
-  RaySample sm[kMaxS / 64];
-  float carry = 1.f;
-  double d = 0.0;
-#pragma unroll
-  for (int c = 0; c < kMaxS / 64; ++c) {
-    if (c >= nch) break;
-    sm[c] = load_sample(rr, zz, S, c * 64 + lane, lane, carry);
-    d += (double)sm[c].w * sm[c].z;
-  }
-  d = wave_sumd(d);
-  const double gd = gdep ? gdep[ray] : 0.0;
-  const double gv = gvar ? gvar[ray] : 0.0;
-  const float gc0 = gcol ? gcol[ray * 3 + 0] : 0.f;
-  const float gc1 = gcol ? gcol[ray * 3 + 1] : 0.f;
-  const float gc2 = gcol ? gcol[ray * 3 + 2] : 0.f;
+// Backward of one ray (the wave owns it) given its loaded samples, depth and cotangents
+// (g_depth, g_var float64; g_color float32); writes g_raw for the ray's samples.
+__device__ __forceinline__ void ray_bwd(const RaySample (&sm)[kMaxS / 64], int nch, int S, double d, double gd,
+                                        double gv, float gc0, float gc1, float gc2, float* __restrict__ gr,
+                                        int lane) {
   // d var / d depth = -sum_k [gv*(w dz) + (gv dz) w]
   double sdep = 0.0;
 #pragma unroll
@@ -186,9 +166,185 @@ __global__ __launch_bounds__(256) void k_composite_bwd(const float* __restrict__
       o[1] = gc1 * s.w;
       o[2] = gc2 * s.w;
       o[3] = g_occ;
-      *reinterpret_cast<f32x4*>(graw + (ray * (int64_t)S + k) * 4) = o;
+      *reinterpret_cast<f32x4*>(gr + (int64_t)k * 4) = o;
     }
   }
+}
+
+// Forward of one ray: loads all its samples (kept in registers for a backward) and returns
+// depth (float64), var (float64) and colour (float32 x3) exactly as k_composite_fwd.
+struct RayOut {
+  double d, v;
+  float c0, c1, c2;
+};
+
+__device__ __forceinline__ RayOut ray_fwd(const float* rr, const double* zz, int S, int nch, RaySample (&sm)[kMaxS / 64],
+                                          int lane) {
+  float carry = 1.f;
+  RayOut o{0.0, 0.0, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < kMaxS / 64; ++c) {
+    if (c >= nch) break;
+    sm[c] = load_sample(rr, zz, S, c * 64 + lane, lane, carry);
+    o.c0 += sm[c].w * sm[c].raw[0];
+    o.c1 += sm[c].w * sm[c].raw[1];
+    o.c2 += sm[c].w * sm[c].raw[2];
+    o.d += (double)sm[c].w * sm[c].z;
+  }
+  o.c0 = wave_sum(o.c0);
+  o.c1 = wave_sum(o.c1);
+  o.c2 = wave_sum(o.c2);
+  o.d = wave_sumd(o.d);
+#pragma unroll
+  for (int c = 0; c < kMaxS / 64; ++c) {
+    if (c >= nch) break;
+    const double dz = sm[c].z - o.d;
+    o.v += ((double)sm[c].w * dz) * dz;  // (weights*tmp)*tmp
+  }
+  o.v = wave_sumd(o.v);
+  return o;
+}
+
+__global__ __launch_bounds__(256) void k_composite_bwd(const float* __restrict__ raw, const double* __restrict__ zv,
+                                                       int64_t n, int S, const double* __restrict__ gdep,
+                                                       const double* __restrict__ gvar,
+                                                       const float* __restrict__ gcol, float* __restrict__ graw) {
+  const int lane = threadIdx.x & 63;
+  const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (ray >= n) return;
+  const float* rr = raw + ray * (int64_t)S * 4;
+  const double* zz = zv + ray * (int64_t)S;
+  const int nch = (S + 63) / 64;
+  RaySample sm[kMaxS / 64];
+  float carry = 1.f;
+  double d = 0.0;
+#pragma unroll
+  for (int c = 0; c < kMaxS / 64; ++c) {
+    if (c >= nch) break;
+    sm[c] = load_sample(rr, zz, S, c * 64 + lane, lane, carry);
+    d += (double)sm[c].w * sm[c].z;
+  }
+  d = wave_sumd(d);
+  const double gd = gdep ? gdep[ray] : 0.0;
+  const double gv = gvar ? gvar[ray] : 0.0;
+  const float gc0 = gcol ? gcol[ray * 3 + 0] : 0.f;
+  const float gc1 = gcol ? gcol[ray * 3 + 1] : 0.f;
+  const float gc2 = gcol ? gcol[ray * 3 + 2] : 0.f;
+  ray_bwd(sm, nch, S, d, gd, gv, gc0, gc1, gc2, graw + ray * (int64_t)S * 4, lane);
+}
+
+// ------------------------------------------------------------------------------------------
+// Rendering loss fused with compositing fwd + bwd (Mapper.py:487-503, Tracker.py:110-125)
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ double sgnd(double x) { return (double)((x > 0.0) - (x < 0.0)); }
+__device__ __forceinline__ float sgnf(float x) { return (float)((x > 0.f) - (x < 0.f)); }
+
+struct LossArgs {
+  nslam_loss_cfg cfg;
+  const float* raw;
+  const double* z;
+  int64_t n;
+  int S;
+  const float *gt, *gtc;
+  const uint8_t* keep;
+  double *depth, *var;
+  float* color;
+  double* ray_loss;
+  float* g_raw;
+  double* resid;      // tracker: r per ray (ws)
+  const double* thr;  // tracker: 10 * median (ws), read by the backward pass
+};
+
+// PASS 0: mapper, fwd + loss + bwd in one pass.
+// PASS 1: tracker fwd (outputs + residual r).  PASS 2: tracker loss + bwd (after the median).
+template <int PASS>
+__global__ __launch_bounds__(256) void k_render_loss(LossArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (ray >= a.n) return;
+  const int S = a.S;
+  const float* rr = a.raw + ray * (int64_t)S * 4;
+  const double* zz = a.z + ray * (int64_t)S;
+  const int nch = (S + 63) / 64;
+  RaySample sm[kMaxS / 64];
+  const RayOut o = ray_fwd(rr, zz, S, nch, sm, lane);
+  const bool kp = a.keep ? a.keep[ray] != 0 : true;
+  const float gt = a.gt[ray];
+  if (PASS != 2 && lane == 0) {
+    a.depth[ray] = o.d;
+    a.var[ray] = o.v;
+    a.color[ray * 3 + 0] = o.c0;
+    a.color[ray * 3 + 1] = o.c1;
+    a.color[ray * 3 + 2] = o.c2;
+  }
+  const double x = (double)gt - o.d;  // gt (float32) - depth (float64) in float64
+  double gd = 0.0, lossd = 0.0;
+  bool mcol = false;
+  if (PASS == 0) {
+    const bool m = kp && gt > 0.f;
+    gd = m ? -sgnd(x) : 0.0;
+    lossd = m ? fabs(x) : 0.0;
+    mcol = kp && a.cfg.use_color;
+  } else {
+    const double sq = sqrt(o.v + 1e-10);  // uncertainty detached (Tracker.py:110)
+    const double r = fabs(x) / sq;
+    if (PASS == 1) {
+      if (lane == 0) a.resid[ray] = r;
+      return;
+    }
+    const bool m = kp && gt > 0.f && (!a.cfg.handle_dynamic || r < *a.thr);
+    gd = m ? -(sgnd(x) * (1.0 / sq)) : 0.0;
+    lossd = m ? r : 0.0;
+    mcol = m && a.cfg.use_color;
+  }
+  float gc0 = 0.f, gc1 = 0.f, gc2 = 0.f;
+  if (mcol) {  // d/dc of w * |gt_c - c|  (float32 branch of the loss)
+    const float e0 = a.gtc[ray * 3 + 0] - o.c0, e1 = a.gtc[ray * 3 + 1] - o.c1, e2 = a.gtc[ray * 3 + 2] - o.c2;
+    const float w = a.cfg.w_color;
+    gc0 = -(w * sgnf(e0));
+    gc1 = -(w * sgnf(e1));
+    gc2 = -(w * sgnf(e2));
+    lossd += (double)(w * ((fabsf(e0) + fabsf(e1)) + fabsf(e2)));
+  }
+  if (a.ray_loss && lane == 0) a.ray_loss[ray] = lossd;
+  if (a.g_raw) ray_bwd(sm, nch, S, o.d, gd, 0.0, gc0, gc1, gc2, a.g_raw + ray * (int64_t)S * 4, lane);
+}
+
+// Tracker handle_dynamic: thr = 10 * median(r over kept rays) (torch.median: lower median).
+// One workgroup: kept residuals into LDS (padded with +inf to a power of two), bitonic sort.
+constexpr int kMedianMax = 16384;
+
+__global__ __launch_bounds__(1024) void k_median_thr(const double* __restrict__ r, const uint8_t* __restrict__ keep,
+                                                     int n, double* __restrict__ thr) {
+  extern __shared__ double sv[];
+  __shared__ int cnt;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  int np2 = 1;
+  while (np2 < n) np2 <<= 1;
+  for (int i = threadIdx.x; i < np2; i += blockDim.x) sv[i] = INFINITY;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    if (!keep || keep[i]) sv[atomicAdd(&cnt, 1)] = r[i];
+  }
+  __syncthreads();
+  for (int k = 2; k <= np2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < np2; i += blockDim.x) {
+        const int l = i ^ j;
+        if (l > i) {
+          const double x = sv[i], y = sv[l];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) {
+            sv[i] = y;
+            sv[l] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x == 0) *thr = cnt > 0 ? 10.0 * sv[(cnt - 1) / 2] : INFINITY;
 }
 
 int hip_status() {
@@ -220,5 +376,66 @@ extern "C" int nslam_composite_bwd(const float* raw, const double* z_vals, int64
   const dim3 grid((unsigned)((n_rays + 3) / 4)), block(256);
   hipLaunchKernelGGL(k_composite_bwd, grid, block, 0, reinterpret_cast<hipStream_t>(stream), raw, z_vals, n_rays,
                      (int)n_samples, g_depth, g_var, g_color, g_raw);
+  return hip_status();
+}
+
+namespace {
+size_t loss_ws(const nslam_loss_cfg* cfg, int64_t n) {
+  if (!cfg || cfg->mode != NSLAM_LOSS_TRACKER || n <= 0) return 0;
+  return (size_t)(n + 1) * sizeof(double);
+}
+}  // namespace
+
+extern "C" size_t nslam_render_loss_workspace_size(const nslam_loss_cfg* cfg, int64_t n_rays) {
+  return loss_ws(cfg, n_rays);
+}
+
+extern "C" int nslam_render_loss(const nslam_loss_cfg* cfg, const float* raw, const double* z_vals, int64_t n_rays,
+                                 int32_t n_samples, const float* gt_depth, const float* gt_color,
+                                 const uint8_t* keep, double* depth, double* var, float* color, double* ray_loss,
+                                 float* g_raw, void* ws, size_t ws_bytes, void* stream) {
+  if (!cfg || (cfg->mode != NSLAM_LOSS_MAPPER && cfg->mode != NSLAM_LOSS_TRACKER)) return NSLAM_EINVAL;
+  if (n_rays < 0 || n_samples <= 0) return NSLAM_EINVAL;
+  if (n_samples > kMaxS) return NSLAM_EUNSUPPORTED;
+  if (n_rays == 0) return NSLAM_OK;
+  if (!raw || !z_vals || !gt_depth || !depth || !var || !color) return NSLAM_EINVAL;
+  if (cfg->use_color && !gt_color) return NSLAM_EINVAL;
+  const bool trk = cfg->mode == NSLAM_LOSS_TRACKER;
+  if (trk && cfg->handle_dynamic && n_rays > kMedianMax) return NSLAM_EUNSUPPORTED;
+  if (ws_bytes < loss_ws(cfg, n_rays) || (loss_ws(cfg, n_rays) && !ws)) return NSLAM_EWORKSPACE;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  LossArgs a{};
+  a.cfg = *cfg;
+  a.raw = raw;
+  a.z = z_vals;
+  a.n = n_rays;
+  a.S = n_samples;
+  a.gt = gt_depth;
+  a.gtc = gt_color;
+  a.keep = keep;
+  a.depth = depth;
+  a.var = var;
+  a.color = color;
+  a.ray_loss = ray_loss;
+  a.g_raw = g_raw;
+  const dim3 grid((unsigned)((n_rays + 3) / 4)), block(256);
+  if (!trk) {
+    hipLaunchKernelGGL(k_render_loss<0>, grid, block, 0, s, a);
+    return hip_status();
+  }
+  double* w = reinterpret_cast<double*>(ws);
+  a.resid = w;
+  a.thr = w + n_rays;
+  hipLaunchKernelGGL(k_render_loss<1>, grid, block, 0, s, a);  // outputs + residuals
+  if (cfg->handle_dynamic) {
+    int np2 = 1;
+    while (np2 < n_rays) np2 <<= 1;
+    const size_t lds = (size_t)np2 * sizeof(double);
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_median_thr), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess)
+      return hip_status();
+    hipLaunchKernelGGL(k_median_thr, dim3(1), dim3(1024), lds, s, w, keep, (int)n_rays, w + n_rays);
+  }
+  hipLaunchKernelGGL(k_render_loss<2>, grid, block, 0, s, a);
   return hip_status();
 }

@@ -1,0 +1,259 @@
+// nslam_mapping.hip — the per-iteration glue of Mapper.optimize_map / Tracker.optimize_cam_in_batch
+// as two single-launch kernels on gfx950:
+//   k_gather_rays : get_samples (src/common.py:74-134) for all frames of the window at once, with
+//                   the inside-mask prefilter (Mapper.py:469-481, Tracker.py:93-104) folded in;
+//   k_adam        : torch.optim.Adam's update (Mapper.py:504, Tracker.py:126) over dense parameter
+//                   segments and frustum-masked grid rows (Mapper.py:314-333) in one launch.
+// Both are HBM/latency-bound elementwise work: no LDS, coalesced float4 rows where the layout allows.
+#include <math.h>
+
+#include "nslam_dev.h"
+
+namespace {
+
+int hip_status() {
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? NSLAM_OK : NSLAM_EHIP - (int)e;
+}
+
+// ------------------------------------------------------------------------------------------
+// pixel sampling + rays + inside mask
+// ------------------------------------------------------------------------------------------
+struct GatherArgs {
+  nslam_frame fr[NSLAM_MAX_FRAMES];
+  int64_t n_per, n;
+  const int64_t* pix;
+  int32_t W, h0, w0, ww;
+  float fx, fy, cx, cy;
+  int32_t use_bound;
+  double lo[3], hi[3];
+  float *ro, *rd, *gd, *gc;
+  uint8_t* keep;
+};
+
+// torch.max / torch.min propagate NaN
+__device__ __forceinline__ double nanmax(double a, double b) { return (a > b || a != a) ? a : b; }
+__device__ __forceinline__ double nanmin(double a, double b) { return (a < b || a != a) ? a : b; }
+
+__global__ __launch_bounds__(256) void k_gather_rays(GatherArgs a) {
+  const int64_t ray = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (ray >= a.n) return;
+  const int f = (int)(ray / a.n_per);
+  const nslam_frame fr = a.fr[f];
+  const int64_t k = a.pix[ray];
+  // window index -> (row, col); torch.linspace(W0, W1-1, W1-W0) holds exact integers
+  const int64_t r = k / a.ww, c = k - r * a.ww;
+  const int64_t px = (a.h0 + r) * a.W + (a.w0 + c);
+  const float i = (float)(a.w0 + c), j = (float)(a.h0 + r);
+  // dirs = ((i-cx)/fx, -(j-cy)/fy, -1); rays_d = sum(dirs * c2w[:3,:3], -1) (common.py:80-86).
+  // On the GPU torch divides by a CPU scalar as a multiply by its float reciprocal
+  // (BinaryDivTrueKernel), which is what the reference runs: do the same.
+  const float d0 = (i - a.cx) * (1.f / a.fx);
+  const float d1 = -(j - a.cy) * (1.f / a.fy);
+  const float d2 = -1.f;
+  float o[3], d[3];
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    const float* row = fr.c2w + 4 * m;
+    // torch's 3-element sum reduces as (p0 + p2) + p1 on this device (tools/probes/rays_order.py)
+    d[m] = (d0 * row[0] + d2 * row[2]) + d1 * row[1];
+    o[m] = row[3];
+  }
+  float gt = fr.depth[px];
+  bool kp = true;
+  if (a.use_bound) {  // t = (bound - o) / d (float64); t_exit = min_axis max(t_lo, t_hi) >= gt
+    double tex = 0.0;
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      const double tl = (a.lo[m] - (double)o[m]) / (double)d[m];
+      const double th = (a.hi[m] - (double)o[m]) / (double)d[m];
+      const double tm = nanmax(tl, th);
+      tex = m == 0 ? tm : nanmin(tex, tm);
+    }
+    kp = tex >= (double)gt;
+  }
+  if (!kp) gt = 0.f;
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    a.ro[ray * 3 + m] = o[m];
+    a.rd[ray * 3 + m] = d[m];
+    a.gc[ray * 3 + m] = fr.color[px * 3 + m];
+  }
+  a.gd[ray] = gt;
+  if (a.keep) a.keep[ray] = kp ? 1 : 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// Adam
+// ------------------------------------------------------------------------------------------
+struct AdamArgs {
+  nslam_adam_seg seg[NSLAM_ADAM_MAX_SEGS];
+  int64_t blk0[NSLAM_ADAM_MAX_SEGS + 1];  // first workgroup of each segment
+  int32_t nseg;
+  float b1, b2, eps;
+  int32_t zero_grad;
+  uint32_t* ticket;
+};
+
+constexpr int kAdamThreads = 256;
+constexpr int kDensePerBlock = kAdamThreads;  // one float per thread (dense segments are small)
+
+// torch.optim.Adam (single-tensor form, the reference's torch 1.11):
+//   m = b1 m + (1-b1) g;  v = b2 v + (1-b2) g g;  p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+// with torch's GPU division by a host scalar done as a multiply by its float reciprocal.
+struct AdamCoef {
+  float b1, omb1, b2, omb2, eps, rbc2s, step_size;
+};
+
+__device__ __forceinline__ float adam_one(float& p, float g, float& m, float& v, const AdamCoef& c) {
+  m = c.b1 * m + c.omb1 * g;
+  v = c.b2 * v + c.omb2 * g * g;
+  const float den = sqrtf(v) * c.rbc2s + c.eps;
+  p = p - c.step_size * (m / den);
+  return p;
+}
+
+__global__ __launch_bounds__(kAdamThreads) void k_adam(AdamArgs a) {
+  const int64_t b = blockIdx.x;
+  int s = 0;
+  while (s + 1 < a.nseg && b >= a.blk0[s + 1]) ++s;
+  const nslam_adam_seg& sg = a.seg[s];
+  const float t = *sg.step + 1.f;
+  const double bc1 = 1.0 - pow((double)a.b1, (double)t);
+  const double bc2 = 1.0 - pow((double)a.b2, (double)t);
+  AdamCoef c;
+  c.b1 = a.b1;
+  c.omb1 = 1.f - a.b1;
+  c.b2 = a.b2;
+  c.omb2 = 1.f - a.b2;
+  c.eps = a.eps;
+  c.rbc2s = 1.f / (float)sqrt(bc2);
+  c.step_size = (float)((double)sg.lr / bc1);
+  const int64_t lb = b - a.blk0[s];
+  if (!sg.rows) {
+    const int64_t e = lb * kDensePerBlock + threadIdx.x;
+    if (e < sg.n) {
+      float p = sg.param[e], m = sg.exp_avg[e], v = sg.exp_avg_sq[e];
+      const float g = sg.grad[e];
+      adam_one(p, g, m, v, c);
+      sg.param[e] = p;
+      sg.exp_avg[e] = m;
+      sg.exp_avg_sq[e] = v;
+      if (a.zero_grad) sg.grad[e] = 0.f;
+    }
+  } else {
+    const int q = sg.row_len / 4;                 // float4 per row
+    const int64_t rows_per_block = kAdamThreads / q;
+    const int64_t ri = lb * rows_per_block + threadIdx.x / q;
+    const int part = threadIdx.x % q;
+    if (threadIdx.x < rows_per_block * q && ri < sg.n) {
+      const int64_t base = (int64_t)sg.rows[ri] * sg.row_len + part * 4;
+      const int64_t sbase = ri * sg.row_len + part * 4;
+      f32x4 p = *reinterpret_cast<const f32x4*>(sg.param + base);
+      const f32x4 g = *reinterpret_cast<const f32x4*>(sg.grad + base);
+      f32x4 m = *reinterpret_cast<const f32x4*>(sg.exp_avg + sbase);
+      f32x4 v = *reinterpret_cast<const f32x4*>(sg.exp_avg_sq + sbase);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float pk = p[k], mk = m[k], vk = v[k];
+        adam_one(pk, g[k], mk, vk, c);
+        p[k] = pk;
+        m[k] = mk;
+        v[k] = vk;
+      }
+      *reinterpret_cast<f32x4*>(sg.param + base) = p;
+      *reinterpret_cast<f32x4*>(sg.exp_avg + sbase) = m;
+      *reinterpret_cast<f32x4*>(sg.exp_avg_sq + sbase) = v;
+      if (a.zero_grad) *reinterpret_cast<f32x4*>(sg.grad + base) = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  // the last workgroup to finish advances every segment's step (all have read theirs by then)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const unsigned tk = atomicAdd(a.ticket, 1u);
+    if (tk == gridDim.x - 1) {
+      for (int k = 0; k < a.nseg; ++k) *a.seg[k].step += 1.f;
+      *a.ticket = 0u;
+      __threadfence();
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int nslam_gather_rays(const nslam_frame* frames, int32_t n_frames, int64_t n_per, const int64_t* pix,
+                                 int32_t H, int32_t W, int32_t h0, int32_t h1, int32_t w0, int32_t w1, float fx,
+                                 float fy, float cx, float cy, const double* bound_lo, const double* bound_hi,
+                                 float* rays_o, float* rays_d, float* gt_depth, float* gt_color, uint8_t* keep,
+                                 void* stream) {
+  if (!frames || n_frames <= 0 || n_frames > NSLAM_MAX_FRAMES || n_per < 0) return NSLAM_EINVAL;
+  if (H <= 0 || W <= 0 || h0 < 0 || w0 < 0 || h1 > H || w1 > W || h1 <= h0 || w1 <= w0) return NSLAM_EINVAL;
+  if ((bound_lo == nullptr) != (bound_hi == nullptr)) return NSLAM_EINVAL;
+  const int64_t n = (int64_t)n_frames * n_per;
+  if (n == 0) return NSLAM_OK;
+  if (!pix || !rays_o || !rays_d || !gt_depth || !gt_color) return NSLAM_EINVAL;
+  GatherArgs a{};
+  for (int f = 0; f < n_frames; ++f) {
+    if (!frames[f].depth || !frames[f].color || !frames[f].c2w) return NSLAM_EINVAL;
+    a.fr[f] = frames[f];
+  }
+  a.n_per = n_per;
+  a.n = n;
+  a.pix = pix;
+  a.W = W;
+  a.h0 = h0;
+  a.w0 = w0;
+  a.ww = w1 - w0;
+  a.fx = fx;
+  a.fy = fy;
+  a.cx = cx;
+  a.cy = cy;
+  a.use_bound = bound_lo != nullptr;
+  for (int k = 0; k < 3 && a.use_bound; ++k) {
+    a.lo[k] = bound_lo[k];
+    a.hi[k] = bound_hi[k];
+  }
+  a.ro = rays_o;
+  a.rd = rays_d;
+  a.gd = gt_depth;
+  a.gc = gt_color;
+  a.keep = keep;
+  hipLaunchKernelGGL(k_gather_rays, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), a);
+  return hip_status();
+}
+
+extern "C" int nslam_adam_step(const nslam_adam_seg* segs, int32_t n_segs, float beta1, float beta2, float eps,
+                               int32_t zero_grad, uint32_t* ticket, void* stream) {
+  if (!segs || n_segs <= 0 || n_segs > NSLAM_ADAM_MAX_SEGS || !ticket) return NSLAM_EINVAL;
+  AdamArgs a{};
+  int64_t blocks = 0;
+  for (int s = 0; s < n_segs; ++s) {
+    const nslam_adam_seg& g = segs[s];
+    if (g.n < 0 || !g.step || (g.n > 0 && (!g.param || !g.grad || !g.exp_avg || !g.exp_avg_sq))) return NSLAM_EINVAL;
+    a.seg[s] = g;
+    a.blk0[s] = blocks;
+    if (g.rows) {
+      if (g.row_len <= 0 || g.row_len % 4 || g.row_len / 4 > kAdamThreads) return NSLAM_EINVAL;
+      const uintptr_t al = (uintptr_t)g.param | (uintptr_t)g.grad | (uintptr_t)g.exp_avg | (uintptr_t)g.exp_avg_sq;
+      if (al & 15) return NSLAM_EINVAL;
+      const int64_t rpb = kAdamThreads / (g.row_len / 4);
+      blocks += (g.n + rpb - 1) / rpb;
+    } else {
+      blocks += (g.n + kDensePerBlock - 1) / kDensePerBlock;
+    }
+  }
+  a.blk0[n_segs] = blocks;
+  a.nseg = n_segs;
+  a.b1 = beta1;
+  a.b2 = beta2;
+  a.eps = eps;
+  a.zero_grad = zero_grad;
+  a.ticket = ticket;
+  if (blocks == 0) return NSLAM_EINVAL;  // every segment empty: nothing would advance the steps
+  if (blocks >= (int64_t(1) << 31)) return NSLAM_EUNSUPPORTED;
+  hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(kAdamThreads), 0, reinterpret_cast<hipStream_t>(stream),
+                     a);
+  return hip_status();
+}

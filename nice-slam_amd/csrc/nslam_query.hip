@@ -36,9 +36,16 @@ __device__ __forceinline__ Pt load_point(const QueryKArgs& a, int64_t idx) {
   Pt q;
   q.valid = idx < a.n;
   const int64_t i = q.valid ? idx : 0;  // invalid tail lanes compute on a real point, write nothing
-  q.p[0] = a.pts[i * 3 + 0];
-  q.p[1] = a.pts[i * 3 + 1];
-  q.p[2] = a.pts[i * 3 + 2];
+  if (a.c.rays_o) {  // pts = rays_o + rays_d * z (float64, Renderer.py:172-174); host checks n < 2^31
+    const uint32_t r = (uint32_t)i / (uint32_t)a.c.n_samples;
+    const double z = a.c.z_vals[i];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) q.p[k] = (double)a.c.rays_o[r * 3 + k] + (double)a.c.rays_d[r * 3 + k] * z;
+  } else {
+    q.p[0] = a.pts[i * 3 + 0];
+    q.p[1] = a.pts[i * 3 + 1];
+    q.p[2] = a.pts[i * 3 + 2];
+  }
   bool in = true;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -787,7 +794,10 @@ int check_cfg(const nslam_query_cfg* c, bool bwd) {
     if (!grid_ok(c->grid[d]) || !c->packed[d]) return NSLAM_EINVAL;
     if ((((uintptr_t)c->packed[d]) & 15) != 0) return NSLAM_EINVAL;
   }
-  (void)bwd;
+  if (c->rays_o) {
+    if (!c->rays_d || !c->z_vals || c->n_samples <= 0) return NSLAM_EINVAL;
+    if (bwd && c->need_pts_grad) return NSLAM_EUNSUPPORTED;
+  }
   return NSLAM_OK;
 }
 
@@ -802,7 +812,8 @@ extern "C" int nslam_query_fwd(const nslam_query_cfg* cfg, const double* pts, in
                                void* stream) {
   const int rc = check_cfg(cfg, false);
   if (rc) return rc;
-  if (n_pts < 0 || (n_pts > 0 && (!pts || !raw))) return NSLAM_EINVAL;
+  if (n_pts < 0 || (n_pts > 0 && ((!pts && !cfg->rays_o) || !raw))) return NSLAM_EINVAL;
+  if (cfg->rays_o && (n_pts >= (int64_t(1) << 31) || n_pts % cfg->n_samples)) return NSLAM_EINVAL;
   if (n_pts == 0) return NSLAM_OK;
   QueryKArgs a{*cfg, pts, n_pts, raw, nullptr, nullptr};
   const int64_t tiles = (n_pts + 31) / 32;
@@ -903,7 +914,8 @@ extern "C" int nslam_query_bwd(const nslam_query_cfg* cfg, const double* pts, in
                                double* g_pts, void* ws, size_t ws_bytes, void* stream) {
   const int rc = check_cfg(cfg, true);
   if (rc) return rc;
-  if (n_pts < 0 || (n_pts > 0 && (!pts || !g_raw))) return NSLAM_EINVAL;
+  if (n_pts < 0 || (n_pts > 0 && ((!pts && !cfg->rays_o) || !g_raw))) return NSLAM_EINVAL;
+  if (cfg->rays_o && (n_pts >= (int64_t(1) << 31) || n_pts % cfg->n_samples)) return NSLAM_EINVAL;
   if (cfg->need_pts_grad && n_pts > 0 && !g_pts) return NSLAM_EINVAL;
   if (n_pts == 0) return NSLAM_OK;
   for (int d = 0; d < 4; ++d)

@@ -29,11 +29,16 @@ def global_max(x: torch.Tensor, group=None) -> torch.Tensor:
 
 
 def allreduce_grads(params, group=None, bucket_bytes: int = 64 << 20):
-    """Sum .grad of `params` over ranks.  Large tensors (feature grids) are reduced in place, small
-    ones (decoder weights, camera 7-vectors) are coalesced into buckets of ≤ bucket_bytes."""
+    """Sum .grad of `params` over ranks (see allreduce_tensors)."""
+    allreduce_tensors([p.grad for p in params if p is not None and p.grad is not None], group, bucket_bytes)
+
+
+def allreduce_tensors(grads, group=None, bucket_bytes: int = 64 << 20):
+    """Sum tensors over ranks in place.  Large ones (feature-grid gradients; the fused engine
+    passes all grids as one flat buffer) are reduced in place, small ones (decoder weights, camera
+    7-vectors) are coalesced into buckets of ≤ bucket_bytes."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
         return
-    grads = [p.grad for p in params if p is not None and p.grad is not None]
     small, size = [], 0
 
     def flush():

@@ -1,0 +1,170 @@
+"""Fused NICE-SLAM mapping iteration on the HIP kernels, without autograd.
+
+One iteration of Mapper.optimize_map's inner loop (src/Mapper.py:421-519) is
+
+    randint pixels → get_samples + inside-mask     nslam_gather_rays        (1 launch)
+    sampler                                         nslam_sample_rays        (2-3 launches)
+    pts = o + d·z, grids + decoders → raw          nslam_query_fwd, ray form
+    compositing + mapping loss + their backward    nslam_render_loss        (1 launch)
+    zero gradients                                  one memset over a flat buffer
+    decoders + grids backward                      nslam_query_bwd, ray form
+    [ray-sharded: RCCL all-reduce of the gradients]
+    Adam over frustum-masked grid rows + decoders  nslam_adam_step          (1 launch)
+    re-pack the optimised decoder                   one gather
+
+with every buffer persistent, so the whole iteration can be captured in a hipGraph.  The maths
+is the reference's: the inside-mask drops rays by zero loss weight instead of compaction (their
+gradients are exactly zero and the sampler's batch max only sees kept rays), and Adam updates
+the frustum-selected voxels in place instead of through masked copies (Mapper.py:314-333,
+394-401, 511-519) — the same elementwise update.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+
+from . import _lib, ops
+from ._lib import check, lib, ptr, stream_ptr
+
+_GRID_OF = {"coarse": "grid_coarse", "middle": "grid_middle", "fine": "grid_fine", "color": "grid_color"}
+
+
+class FlatDecoder:
+    """A decoder's parameters re-bound as views of one flat float32 buffer (named_parameters
+    order = the nslam_dec_grad layout) with a trailing zero slot, so packing is one gather into a
+    persistent buffer and Adam sees one dense segment.  Parameter identity (and state_dict keys)
+    is unchanged."""
+
+    def __init__(self, dec):
+        self.dec = dec
+        self.packer = dec.packer()
+        params = list(dec.parameters())
+        n = sum(p.numel() for p in params)
+        dev = params[0].device
+        flat = torch.zeros(n + 1, dtype=torch.float32, device=dev)
+        off = 0
+        with torch.no_grad():
+            for p in params:
+                k = p.numel()
+                flat[off:off + k].copy_(p.detach().reshape(-1))
+                p.data = flat[off:off + k].view_as(p)
+                off += k
+        self.flat = flat
+        self.param = flat[:n]                       # Adam segment
+        self.grad = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.packed = torch.empty(self.packer.index.shape[0], dtype=torch.float32, device=dev)
+        self.idx = self.packer.device_index(dev)
+        self.repack()
+
+    def repack(self):
+        torch.index_select(self.flat, 0, self.idx, out=self.packed)
+
+
+class MappingEngine:
+    """Fused mapping iterations over shared grids `c` (dict of [1,32,Z,Y,X] channels-last grids)
+    and a NICE decoder stack, for the stage schedule of Mapper.optimize_map."""
+
+    def __init__(self, nice, c, bound, n_strat, n_surf, lindisp=False, w_color=0.2, device="cuda"):
+        self.nice, self.c, self.bound = nice, c, bound
+        self.n_strat, self.n_surf, self.lindisp, self.w_color = n_strat, n_surf, lindisp, w_color
+        self.device = torch.device(device)
+        names = [n for n in ("coarse", "middle", "fine", "color") if hasattr(nice, n + "_decoder")]
+        self.decs = {n: FlatDecoder(nice.decoder(n)) for n in names}
+        self.dec_bounds = {n: ops._bound_list(nice.decoder(n).bound) for n in names}
+        self.oob = ops._bound_list(bound)
+        # one flat gradient buffer for every grid: zeroing is a single memset
+        sizes = {k: v.numel() for k, v in c.items()}
+        self.gbuf = torch.zeros(sum(sizes.values()), dtype=torch.float32, device=self.device)
+        self.ggrad, off = {}, 0
+        for k, v in c.items():
+            if not v.is_contiguous(memory_format=torch.channels_last_3d):
+                raise ValueError(f"{k} must be channels-last (ops.channels_last)")
+            Z, Y, X = v.shape[2:]
+            self.ggrad[k] = self.gbuf[off:off + sizes[k]].view(1, Z, Y, X, 32).permute(0, 4, 1, 2, 3)
+            off += sizes[k]
+
+    # -- query in ray form ---------------------------------------------------------------------
+    def _cfg(self, stage, ro, rd, z, grid_grads, dec_grads):
+        decs = ops._DEC_FOR_STAGE[stage]
+        meta = ops.QueryMeta(stage, decs, {n: self.decs[n].packer for n in decs},
+                             {n: self.dec_bounds[n] for n in decs}, self.oob, None)
+        pairs = [(None, None)] * 4
+        for n in decs:
+            key = _GRID_OF[n]
+            pairs[ops._DEC_ID[n]] = (self.c[key], self.ggrad[key] if key in grid_grads else None)
+        packed = {n: self.decs[n].packed for n in decs}
+        dg = {n: self.decs[n].grad for n in decs if n in dec_grads}
+        cfg = ops._fill_cfg(meta, pairs, packed, dg, False)
+        cfg.rays_o, cfg.rays_d, cfg.z_vals, cfg.n_samples = ptr(ro), ptr(rd), ptr(z), z.shape[1]
+        return cfg
+
+    def query_fwd(self, stage, ro, rd, z):
+        n = z.numel()
+        raw = torch.empty(n, 4, dtype=torch.float32, device=z.device)
+        cfg = self._cfg(stage, ro, rd, z, (), ())
+        with ops._span("query_fwd"):
+            rc = lib().nslam_query_fwd(ctypes.byref(cfg), None, n, ptr(raw), stream_ptr(z.device))
+        check(rc, "nslam_query_fwd")
+        return raw
+
+    def query_bwd(self, stage, ro, rd, z, g_raw, grid_grads, dec_grads):
+        n = z.numel()
+        cfg = self._cfg(stage, ro, rd, z, grid_grads, dec_grads)
+        wsb = lib().nslam_query_bwd_workspace_size(ctypes.byref(cfg), n)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=z.device) if wsb else None
+        with ops._span("query_bwd"):
+            rc = lib().nslam_query_bwd(ctypes.byref(cfg), None, n, ptr(g_raw), None, ptr(ws), wsb,
+                                       stream_ptr(z.device))
+        check(rc, "nslam_query_bwd")
+
+    # -- one iteration ---------------------------------------------------------------------------
+    def grads_for(self, stage, trainable_decoders):
+        """(grid keys, decoder names) that receive gradients in `stage` (Mapper.py:335-341)."""
+        decs = ops._DEC_FOR_STAGE[stage]
+        keys = tuple(_GRID_OF[n] for n in decs)
+        return keys, tuple(n for n in decs if n in trainable_decoders)
+
+    def adam_grads(self, stage, trainable_decoders):
+        keys, dnames = self.grads_for(stage, trainable_decoders)
+        g = {self.c[k]: self.ggrad[k] for k in keys}
+        g.update({self.decs[n].param: self.decs[n].grad for n in dnames})
+        return g
+
+    def iteration(self, stage, frames, pix, n_per, hw, intrinsics, optimizer, trainable_decoders=("color",),
+                  gt_max=None, allreduce=None, use_gt_in_sampler=True):
+        """One mapping iteration; returns (ray_loss f64 [N], keep uint8 [N]) as device tensors.
+
+        frames: [(depth, color, c2w)] of the window; pix: int64 [len(frames)*n_per] randint
+        indices over the full image; hw = (H, W); intrinsics = (fx, fy, cx, cy).
+        gt_max: callable(gt_depth) → device scalar for a ray-sharded job (all-reduced max);
+        allreduce: callable(list of grads) run before Adam (ray sharding).
+        """
+        H, W = hw
+        fx, fy, cx, cy = intrinsics
+        ro, rd, gd, gc, keep = ops.gather_rays(frames, pix, n_per, H, W, (0, H, 0, W), fx, fy, cx, cy, self.bound)
+        gsamp = gd if (use_gt_in_sampler and stage != "coarse") else None
+        gm = gt_max(gd) if (gt_max is not None and gsamp is not None) else None
+        z = ops.sample_z(ro, rd, gsamp, self.bound, self.n_strat, self.n_surf, self.lindisp, gt_max=gm)
+        raw = self.query_fwd(stage, ro, rd, z)
+        _, _, _, ray_loss, g_raw = ops.render_loss(raw, z, gd, gc, keep, mode="mapper", use_color=stage == "color",
+                                                   w_color=self.w_color)
+        keys, dnames = self.grads_for(stage, trainable_decoders)
+        self.gbuf.zero_()
+        for n in dnames:
+            self.decs[n].grad.zero_()
+        self.query_bwd(stage, ro, rd, z, g_raw, keys, dnames)
+        grads = self.adam_grads(stage, trainable_decoders)
+        if allreduce is not None:  # the grid gradients as one flat buffer, plus the decoder gradients
+            allreduce([self.gbuf] + [self.decs[n].grad for n in dnames])
+        optimizer.step(grads=grads)
+        for n in dnames:
+            self.decs[n].repack()
+        return ray_loss, keep
+
+
+def frustum_rows(mask_xyz: torch.Tensor) -> torch.Tensor:
+    """int32 voxel rows (z*Y*X + y*X + x, channels-last) of a get_mask_from_c2w mask [X, Y, Z]."""
+    m = mask_xyz.permute(2, 1, 0).reshape(-1)
+    return torch.nonzero(m).reshape(-1).to(torch.int32)

@@ -38,6 +38,40 @@ def _remap_bilinear(img, u, v):
     return tap(x0, y0) * w00 + tap(x0 + 1, y0) * w01 + tap(x0, y0 + 1) * w10 + tap(x0 + 1, y0 + 1) * w11
 
 
+def frustum_mask(c2w, key, val_shape, depth, bound, H, W, fx, fy, cx, cy):
+    """Mapper.get_mask_from_c2w (Mapper.py:93-164) on the device: bool mask [X, Y, Z] of the
+    grid voxels inside the camera frustum up to the observed depth + 0.5 m, or within 0.5 m of
+    the camera.  val_shape = (Z, Y, X)."""
+    dev = depth.device
+    nz, ny, nx = val_shape[0], val_shape[1], val_shape[2]
+    if key == "grid_coarse":
+        return torch.ones(nx, ny, nz, dtype=torch.bool, device=dev)
+    b = bound
+    X, Y, Z = torch.meshgrid(torch.linspace(float(b[0][0]), float(b[0][1]), nx, device=dev),
+                             torch.linspace(float(b[1][0]), float(b[1][1]), ny, device=dev),
+                             torch.linspace(float(b[2][0]), float(b[2][1]), nz, device=dev), indexing="ij")
+    points = torch.stack([X, Y, Z], dim=-1).reshape(-1, 3)
+    c2w = c2w.to(dev).float()
+    if c2w.shape[0] == 3:
+        c2w = torch.cat([c2w, torch.tensor([[0, 0, 0, 1.0]], device=dev)], 0)
+    w2c = torch.linalg.inv(c2w)
+    cam = points @ w2c[:3, :3].T + w2c[:3, 3]
+    cam = cam.double()
+    cam[:, 0] *= -1
+    K = torch.tensor([[fx, 0.0, cx], [0.0, fy, cy], [0.0, 0.0, 1.0]], dtype=torch.float64, device=dev)
+    uvz = cam @ K.T
+    z = uvz[:, 2] + 1e-5
+    uv = (uvz[:, :2] / z[:, None]).float()
+    depths = _remap_bilinear(depth.float(), uv[:, 0], uv[:, 1])
+    mask = (uv[:, 0] < W) & (uv[:, 0] > 0) & (uv[:, 1] < H) & (uv[:, 1] > 0)
+    depths = torch.where(depths == 0, depths.max(), depths)
+    mask = mask & (0 <= -z) & (-z <= depths.double() + 0.5)
+    ray_o = c2w[:3, 3]
+    d = points - ray_o
+    mask = mask | ((d * d).sum(1) < 0.5 * 0.5)
+    return mask.reshape(nx, ny, nz)
+
+
 class Mapper(object):
     def __init__(self, cfg, args, slam, coarse_mapper=False, generator=None):
         self.cfg = cfg
@@ -77,34 +111,8 @@ class Mapper(object):
     # ------------------------------------------------------------------------------------------
     def get_mask_from_c2w(self, c2w, key, val_shape, depth):
         """Frustum voxel selection (Mapper.py:93-164) → bool mask [X, Y, Z] on the device."""
-        dev = depth.device
-        nz, ny, nx = val_shape[0], val_shape[1], val_shape[2]
-        if key == "grid_coarse":
-            return torch.ones(nx, ny, nz, dtype=torch.bool, device=dev)
-        b = self.bound
-        X, Y, Z = torch.meshgrid(torch.linspace(float(b[0][0]), float(b[0][1]), nx, device=dev),
-                                 torch.linspace(float(b[1][0]), float(b[1][1]), ny, device=dev),
-                                 torch.linspace(float(b[2][0]), float(b[2][1]), nz, device=dev), indexing="ij")
-        points = torch.stack([X, Y, Z], dim=-1).reshape(-1, 3)
-        c2w = c2w.to(dev).float()
-        w2c = torch.linalg.inv(c2w)
-        cam = points @ w2c[:3, :3].T + w2c[:3, 3]
-        cam = cam.double()
-        cam[:, 0] *= -1
-        K = torch.tensor([[self.fx, 0.0, self.cx], [0.0, self.fy, self.cy], [0.0, 0.0, 1.0]], dtype=torch.float64,
-                         device=dev)
-        uvz = cam @ K.T
-        z = uvz[:, 2] + 1e-5
-        uv = (uvz[:, :2] / z[:, None]).float()
-        depths = _remap_bilinear(depth.float(), uv[:, 0], uv[:, 1])
-        H, W = self.H, self.W
-        mask = (uv[:, 0] < W) & (uv[:, 0] > 0) & (uv[:, 1] < H) & (uv[:, 1] > 0)
-        depths = torch.where(depths == 0, depths.max(), depths)
-        mask = mask & (0 <= -z) & (-z <= depths.double() + 0.5)
-        ray_o = c2w[:3, 3]
-        d = points - ray_o
-        mask = mask | ((d * d).sum(1) < 0.5 * 0.5)
-        return mask.reshape(nx, ny, nz)
+        return frustum_mask(c2w, key, val_shape, depth, self.bound, self.H, self.W, self.fx, self.fy, self.cx,
+                            self.cy)
 
     def keyframe_selection_overlap(self, gt_color, gt_depth, c2w, keyframe_dict, k, N_samples=16, pixels=100):
         """Mapper.py:166-228: keyframes whose frustum sees the current frame's surface samples."""

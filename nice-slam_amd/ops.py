@@ -336,3 +336,171 @@ class _GridSample(torch.autograd.Function):
 def grid_sample(grid, coords):
     """[M,32] trilinear features of normalised coords [M,3] (x,y,z) — F.grid_sample semantics."""
     return _GridSample.apply(grid, coords)
+
+
+# ----------------------------------------------------------------------------------------------
+# fused mapping / tracking iteration (ABI v4): pixel gather, render loss, ray-form query, Adam
+# ----------------------------------------------------------------------------------------------
+def gather_rays(frames, pix, n_per, H, W, window, fx, fy, cx, cy, bound=None):
+    """get_samples (src/common.py:92-134) for every frame of a window in one launch, plus the
+    inside-mask prefilter (Mapper.py:469-481) when `bound` is given.
+
+    frames: list of (depth [H,W] f32, color [H,W,3] f32, c2w [3|4,4] f32) device tensors;
+    pix: int64 [len(frames)*n_per] select_uv randint indices into each frame's window
+    (h0, h1, w0, w1).  Returns rays_o, rays_d [N,3] f32, gt_depth [N] f32 (0 for dropped rays),
+    gt_color [N,3] f32, keep [N] uint8.
+    """
+    nf = len(frames)
+    if nf == 0 or nf > _lib.MAX_FRAMES:
+        raise ValueError(f"1..{_lib.MAX_FRAMES} frames, got {nf}")
+    dev = pix.device
+    arr = (_lib.NslamFrame * nf)()
+    keepalive = []
+    for f, (d, c, m) in enumerate(frames):
+        d = d.detach().float().contiguous()
+        c = c.detach().float().contiguous()
+        m = m.detach().float().contiguous()
+        if tuple(d.shape) != (H, W) or tuple(c.shape) != (H, W, 3) or m.shape[-1] != 4 or m.shape[0] < 3:
+            raise ValueError("frame tensors must be depth [H,W], color [H,W,3], c2w [3|4,4]")
+        keepalive += [d, c, m]
+        arr[f].depth, arr[f].color, arr[f].c2w = ptr(d), ptr(c), ptr(m)
+    pix = pix.to(torch.int64).contiguous()
+    n = nf * n_per
+    ro = torch.empty(n, 3, dtype=torch.float32, device=dev)
+    rd = torch.empty(n, 3, dtype=torch.float32, device=dev)
+    gd = torch.empty(n, dtype=torch.float32, device=dev)
+    gc = torch.empty(n, 3, dtype=torch.float32, device=dev)
+    keep = torch.empty(n, dtype=torch.uint8, device=dev)
+    h0, h1, w0, w1 = window
+    if bound is not None:
+        lo, hi = _bound_list(bound)
+        blo, bhi = (ctypes.c_double * 3)(*lo), (ctypes.c_double * 3)(*hi)
+    else:
+        blo = bhi = None
+    with _span("gather_rays"):
+        rc = lib().nslam_gather_rays(arr, nf, n_per, ptr(pix), H, W, h0, h1, w0, w1, fx, fy, cx, cy, blo, bhi,
+                                     ptr(ro), ptr(rd), ptr(gd), ptr(gc), ptr(keep), stream_ptr(dev))
+    check(rc, "nslam_gather_rays")
+    return ro, rd, gd, gc, keep
+
+
+def render_loss(raw, z, gt_depth, gt_color, keep=None, mode="mapper", use_color=True, handle_dynamic=False,
+                w_color=0.2, want_grad=True):
+    """Mapper/Tracker rendering loss fused with compositing and its backward (see nslam.h).
+
+    raw [N,S,4] (or [N*S,4]) f32, z [N,S] f64.  Returns (depth f64 [N], var f64 [N],
+    color f32 [N,3], ray_loss f64 [N], g_raw f32 like raw or None) where sum(ray_loss) is the loss
+    and g_raw = dloss/draw.
+    """
+    z = z.detach().double().contiguous()
+    n, s = z.shape
+    dev = z.device
+    raw = raw.detach().float().contiguous()
+    cfg = _lib.NslamLossCfg(_lib.LOSS_MAPPER if mode == "mapper" else _lib.LOSS_TRACKER, int(bool(use_color)),
+                            int(bool(handle_dynamic)), float(w_color))
+    depth = torch.empty(n, dtype=torch.float64, device=dev)
+    var = torch.empty(n, dtype=torch.float64, device=dev)
+    color = torch.empty(n, 3, dtype=torch.float32, device=dev)
+    ray_loss = torch.empty(n, dtype=torch.float64, device=dev)
+    g_raw = torch.empty_like(raw) if want_grad else None
+    wsb = lib().nslam_render_loss_workspace_size(ctypes.byref(cfg), n)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev) if wsb else None
+    gt_depth = gt_depth.detach().float().contiguous()
+    gt_color = gt_color.detach().float().contiguous() if gt_color is not None else None
+    keep = keep.contiguous() if keep is not None else None
+    if n:
+        with _span("render_loss"):
+            rc = lib().nslam_render_loss(ctypes.byref(cfg), ptr(raw), ptr(z), n, s, ptr(gt_depth), ptr(gt_color),
+                                         ptr(keep), ptr(depth), ptr(var), ptr(color), ptr(ray_loss), ptr(g_raw),
+                                         ptr(ws), wsb, stream_ptr(dev))
+        check(rc, "nslam_render_loss")
+    return depth, var, color, ray_loss, g_raw
+
+
+class FusedAdam:
+    """torch.optim.Adam (betas, eps; no weight decay / amsgrad) stepping every parameter segment
+    in one HIP launch (nslam_adam_step).  Construction mirrors torch:
+
+        FusedAdam([{"params": [...], "lr": 0.005}, {"params": [grid], "lr": 0.1, "rows": idx}, ...])
+
+    A group's "rows" (int32 device tensor of voxel indices) restricts a channels-last grid to the
+    frustum-selected voxels (Mapper.py:314-333): only those rows are updated, in place, with Adam
+    state for them alone.  Parameters whose .grad is None are skipped like torch does (their step
+    count does not advance); `grads` may map a parameter to an explicit gradient tensor instead.
+    Step counts live on the device, so step() can be captured in a hipGraph.
+    """
+
+    def __init__(self, groups, betas=(0.9, 0.999), eps=1e-8):
+        self.param_groups = []
+        self.betas, self.eps = betas, eps
+        self.state = {}
+        dev = None
+        for g in groups:
+            g = dict(g)
+            g["params"] = list(g["params"])
+            self.param_groups.append(g)
+            for p in g["params"]:
+                dev = p.device
+        self.device = dev
+        self.ticket = torch.zeros(1, dtype=torch.int32, device=dev) if dev is not None else None
+
+    def _st(self, p, rows):
+        st = self.state.get(p)
+        if st is None:
+            if rows is not None:
+                n = rows.numel() * 32
+                ex, ex2 = (torch.zeros(n, dtype=torch.float32, device=p.device) for _ in range(2))
+            else:
+                ex, ex2 = torch.zeros_like(p), torch.zeros_like(p)
+            st = {"exp_avg": ex, "exp_avg_sq": ex2, "step": torch.zeros(1, dtype=torch.float32, device=p.device)}
+            self.state[p] = st
+        return st
+
+    def segments(self, grads=None):
+        segs = []
+        for g in self.param_groups:
+            rows = g.get("rows")
+            for p in g["params"]:
+                gr = grads.get(p) if grads is not None else p.grad
+                if gr is None:
+                    continue
+                st = self._st(p, rows)
+                s = _lib.NslamAdamSeg()
+                s.param, s.grad = ptr(p.data), ptr(gr)
+                s.exp_avg, s.exp_avg_sq, s.step = ptr(st["exp_avg"]), ptr(st["exp_avg_sq"]), ptr(st["step"])
+                if rows is not None:
+                    if not (p.is_contiguous(memory_format=torch.channels_last_3d) and
+                            gr.is_contiguous(memory_format=torch.channels_last_3d)):
+                        raise ValueError("row-masked Adam needs channels-last grid and grad")
+                    s.rows, s.n, s.row_len = ptr(rows), rows.numel(), p.shape[1]
+                else:  # elementwise over storage: any dense layout shared by param, grad and state
+                    dense = p.is_contiguous() or p.is_contiguous(memory_format=torch.channels_last_3d)
+                    if not (dense and gr.stride() == p.stride() and st["exp_avg"].stride() == p.stride()):
+                        raise ValueError("dense Adam segments need param, grad and state of one dense layout")
+                    s.rows, s.n, s.row_len = None, p.numel(), 0
+                s.lr = float(g["lr"])
+                segs.append((s, p, gr))
+        return segs
+
+    @torch.no_grad()
+    def step(self, grads=None, zero_grad=False):
+        segs = self.segments(grads)
+        if not segs:
+            return
+        if len(segs) > _lib.ADAM_MAX_SEGS:
+            raise ValueError(f"at most {_lib.ADAM_MAX_SEGS} parameter tensors per step (flatten the decoders)")
+        arr = (_lib.NslamAdamSeg * len(segs))(*[s for s, _, _ in segs])
+        b1, b2 = self.betas
+        with _span("adam"):
+            rc = lib().nslam_adam_step(arr, len(segs), b1, b2, self.eps, int(bool(zero_grad)), ptr(self.ticket),
+                                       stream_ptr(self.device))
+        check(rc, "nslam_adam_step")
+
+    def zero_grad(self, set_to_none=True):
+        for g in self.param_groups:
+            for p in g["params"]:
+                if p.grad is not None:
+                    if set_to_none:
+                        p.grad = None
+                    else:
+                        p.grad.zero_()

@@ -47,8 +47,13 @@ def grids_from(tiny):
     return {k: torch.from_numpy(tiny[k]) for k in ("grid_coarse", "grid_middle", "grid_fine", "grid_color")}
 
 
+def _np(x):
+    if hasattr(x, "detach"):  # torch tensor (any device)
+        x = x.detach().to("cpu", dtype=__import__("torch").float64).numpy()
+    return np.asarray(x, dtype=np.float64).ravel()
+
+
 def rel_l2(a, b):
-    a = np.asarray(a, dtype=np.float64).ravel()
-    b = np.asarray(b, dtype=np.float64).ravel()
+    a, b = _np(a), _np(b)
     den = np.linalg.norm(b)
     return float(np.linalg.norm(a - b) / (den if den > 0 else 1.0))

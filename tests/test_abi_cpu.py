@@ -3,6 +3,7 @@ declares, and the Python pack layout agrees with the C++ one (no GPU calls)."""
 import ctypes
 import os
 import re
+import subprocess
 
 import pytest
 
@@ -25,7 +26,7 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_strerror(pkg):
     L = pkg._lib.lib()
-    assert L.nslam_abi_version() == 3
+    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 4
     assert L.nslam_strerror(0) == b"ok"
     assert b"invalid" in L.nslam_strerror(-1)
 
@@ -61,3 +62,51 @@ def test_no_cpu_fallback(pkg):
     import torch
     with pytest.raises(RuntimeError, match="HIP device"):
         pkg.ops.composite(torch.zeros(2, 4, 4), torch.zeros(2, 4, dtype=torch.float64))
+
+
+def test_struct_layouts_match_header(pkg, tmp_path):
+    """sizeof/offsetof of every ABI struct, compiled by gcc from include/nslam.h, equal the ctypes
+    mirrors in _lib.py."""
+    L = pkg._lib
+    structs = {"nslam_grid": L.NslamGrid, "nslam_dec_grad": L.NslamDecGrad, "nslam_query_cfg": L.NslamQueryCfg,
+               "nslam_frame": L.NslamFrame, "nslam_loss_cfg": L.NslamLossCfg, "nslam_adam_seg": L.NslamAdamSeg}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "nslam.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'  printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f in py._fields_:
+            lines.append(f'  printf("{cname} {f[0]} %zu\\n", offsetof({cname}, {f[0]}));')
+    lines.append("  return 0; }")
+    src = tmp_path / "probe.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {tuple(l.split()[:2]): int(l.split()[2]) for l in out if l}
+    for cname, py in structs.items():
+        assert got[(cname, "size")] == ctypes.sizeof(py), cname
+        for f in py._fields_:
+            assert got[(cname, f[0])] == getattr(py, f[0]).offset, (cname, f[0])
+
+
+def test_v4_entry_points_validate_without_gpu(pkg):
+    L = pkg._lib.lib()
+    lib = pkg._lib
+    fr = (lib.NslamFrame * 1)()
+    assert L.nslam_gather_rays(fr, 0, 10, None, 10, 10, 0, 10, 0, 10, 1.0, 1.0, 0.0, 0.0, None, None,
+                               None, None, None, None, None, None) == -1
+    assert L.nslam_gather_rays(fr, 1, 10, None, 10, 10, 0, 11, 0, 10, 1.0, 1.0, 0.0, 0.0, None, None,
+                               None, None, None, None, None, None) == -1
+    cfg = lib.NslamLossCfg(5, 0, 0, 0.2)
+    assert L.nslam_render_loss(ctypes.byref(cfg), None, None, 4, 48, None, None, None, None, None, None, None,
+                               None, None, 0, None) == -1
+    cfg = lib.NslamLossCfg(lib.LOSS_MAPPER, 0, 0, 0.2)
+    assert L.nslam_render_loss(ctypes.byref(cfg), None, None, 4, 1000, None, None, None, None, None, None, None,
+                               None, None, 0, None) == -2
+    cfg = lib.NslamLossCfg(lib.LOSS_TRACKER, 1, 1, 0.5)
+    assert L.nslam_render_loss_workspace_size(ctypes.byref(cfg), 100) == 101 * 8
+    seg = (lib.NslamAdamSeg * 1)()
+    assert L.nslam_adam_step(seg, 0, 0.9, 0.999, 1e-8, 1, None, None) == -1
+    seg[0].n, seg[0].rows, seg[0].row_len = 4, 16, 6   # row_len % 4 != 0
+    for f in ("param", "grad", "exp_avg", "exp_avg_sq", "step"):
+        setattr(seg[0], f, 64)
+    assert L.nslam_adam_step(seg, 1, 0.9, 0.999, 1e-8, 1, 64, None) == -1
