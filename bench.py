@@ -249,6 +249,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture")
+    ap.add_argument("--pixels", type=int, default=None,
+                    help="override mapping pixels per iteration (scaling studies; the metric uses room0's 1000)")
     ap.add_argument("--path", choices=("fused", "autograd"), default="fused",
                     help="fused engine (default) or the autograd drop-in path")
     args = ap.parse_args()
@@ -260,7 +262,10 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     P = pkg()
-    scene = Room0Scene(dev, rank, path=args.path)
+    cfg = dict(ROOM0)
+    if args.pixels:
+        cfg["pixels"] = args.pixels
+    scene = Room0Scene(dev, rank, cfg=cfg, path=args.path)
     sharded = world > 1
     for _ in range(args.warmup):
         scene.step(sharded=sharded)

@@ -83,6 +83,11 @@ typedef struct nslam_query_cfg {
   const float* rays_d;      /* [M/S][3] float32 */
   const double* z_vals;     /* [M/S][S] float64 */
   int64_t n_samples;        /* S */
+  /* ReLU masks saved by the forward (ABI v4; NULL = none): nslam_query_fwd writes every
+   * evaluated decoder's masks here and nslam_query_bwd then skips the forward recompute of the
+   * decoders that have no parameter gradients (their backward needs only the masks).
+   * nslam_query_saved_size(M) bytes; layout [decoder][tile of 32 points][layer 0..4][64] uint16. */
+  uint16_t* saved_masks;
 } nslam_query_cfg;
 
 /* ---- packing ------------------------------------------------------------------------------
@@ -118,6 +123,16 @@ int nslam_query_fwd(const nslam_query_cfg* cfg, const double* pts, int64_t n_pts
 int nslam_query_bwd(const nslam_query_cfg* cfg, const double* pts, int64_t n_pts, const float* g_raw,
                     double* g_pts, void* ws, size_t ws_bytes, void* stream);
 size_t nslam_query_bwd_workspace_size(const nslam_query_cfg* cfg, int64_t n_pts);
+/* One decoder's share of nslam_query_bwd (ABI v4): its grid gradient, its parameter gradients
+ * and its d/dpts (written, or added when accumulate_pts).  Decoders whose gradients go to
+ * different buffers may run concurrently on different streams (the mapping iteration does:
+ * grids and decoder gradients are disjoint; with need_pts_grad the calls must be ordered).
+ * ws: nslam_query_bwd_decoder_workspace_size(cfg, dec, n_pts) bytes. */
+int nslam_query_bwd_decoder(const nslam_query_cfg* cfg, int32_t dec, int32_t accumulate_pts, const double* pts,
+                            int64_t n_pts, const float* g_raw, double* g_pts, void* ws, size_t ws_bytes,
+                            void* stream);
+size_t nslam_query_bwd_decoder_workspace_size(const nslam_query_cfg* cfg, int32_t dec, int64_t n_pts);
+size_t nslam_query_saved_size(int64_t n_pts);
 
 /* ---- compositing: raw2outputs_nerf_color, src/common.py:204-245 (occupancy mode) ------------ */
 int nslam_composite_fwd(const float* raw, const double* z_vals, int64_t n_rays, int32_t n_samples,

@@ -59,6 +59,7 @@ class NslamQueryCfg(ctypes.Structure):
         ("rays_d", ctypes.c_void_p),
         ("z_vals", ctypes.c_void_p),
         ("n_samples", ctypes.c_int64),
+        ("saved_masks", ctypes.c_void_p),
     ]
 
 
@@ -93,6 +94,7 @@ class NslamAdamSeg(ctypes.Structure):
 # every symbol include/nslam.h declares (tests check that the library exports all of them)
 EXPORTS = (
     "nslam_pack_layout", "nslam_sample_rays", "nslam_query_fwd", "nslam_query_bwd", "nslam_query_bwd_workspace_size",
+    "nslam_query_saved_size", "nslam_query_bwd_decoder", "nslam_query_bwd_decoder_workspace_size",
     "nslam_composite_fwd", "nslam_composite_bwd", "nslam_grid_sample_fwd", "nslam_grid_sample_bwd",
     "nslam_workspace_size", "nslam_strerror", "nslam_abi_version", "nslam_gather_rays", "nslam_render_loss",
     "nslam_render_loss_workspace_size", "nslam_adam_step",
@@ -117,6 +119,11 @@ def lib():
         L.nslam_query_bwd.argtypes = [ctypes.POINTER(NslamQueryCfg), vp, i64, vp, vp, vp, sz, vp]
         L.nslam_query_bwd_workspace_size.argtypes = [ctypes.POINTER(NslamQueryCfg), i64]
         L.nslam_query_bwd_workspace_size.restype = sz
+        L.nslam_query_bwd_decoder.argtypes = [ctypes.POINTER(NslamQueryCfg), i32, i32, vp, i64, vp, vp, vp, sz, vp]
+        L.nslam_query_bwd_decoder_workspace_size.argtypes = [ctypes.POINTER(NslamQueryCfg), i32, i64]
+        L.nslam_query_bwd_decoder_workspace_size.restype = sz
+        L.nslam_query_saved_size.argtypes = [i64]
+        L.nslam_query_saved_size.restype = sz
         L.nslam_composite_fwd.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp]
         L.nslam_composite_bwd.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, vp]
         L.nslam_grid_sample_fwd.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), vp, i64, vp, vp]

@@ -107,6 +107,24 @@ struct Scratch {
 // only the wave's own LDS counter drained (and a compiler memory barrier), not a workgroup barrier.
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// ReLU masks saved by the forward: [decoder][tile][layer][64 lanes] uint16 (one 128-B row per layer)
+__device__ __forceinline__ uint16_t* mask_slot(const QueryKArgs& a, int dec, int64_t tile) {
+  const int64_t ntiles = (a.n + 31) / 32;
+  return a.c.saved_masks + ((size_t)dec * ntiles + tile) * 5 * 64;
+}
+__device__ __forceinline__ void save_masks(const QueryKArgs& a, int dec, int64_t tile, const uint32_t m[5],
+                                           int lane) {
+  if (!a.c.saved_masks) return;
+  uint16_t* s = mask_slot(a, dec, tile);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) s[i * 64 + lane] = (uint16_t)m[i];
+}
+__device__ __forceinline__ void load_masks(const QueryKArgs& a, int dec, int64_t tile, uint32_t m[5], int lane) {
+  const uint16_t* s = mask_slot(a, dec, tile);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) m[i] = s[i * 64 + lane];
+}
+
 // Parameter-gradient slab of one wave, addressed as a raw buffer: every update is a buffer store
 // (or load + store) with the lane-dependent part of the offset in a VGPR and the uniform part
 // (parameter block, row) in soffset, so the ~350 updates per tile cost one address VGPR per block.
@@ -525,6 +543,100 @@ __device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, con
 }
 
 // ------------------------------------------------------------------------------------------
+// Backward from saved ReLU masks (decoders without parameter gradients): no forward recompute,
+// no embedding sin, no feature gather.  dh_4 = Wo^T g; for i = 4..0: dc += FCT_i dh_i and
+// dh_{i-1} = L_iT mask_i(dh_i) (layer 3 through its hidden block); EMBG adds d/dx through the
+// Fourier features from mask_3(dh_3) and mask_0(dh_0).
+// ------------------------------------------------------------------------------------------
+template <int NC, int NOUT, int GOFS, bool EMBG>
+__device__ __forceinline__ void xyz_backward_saved(const float* __restrict__ pk, const uint32_t m[5],
+                                                   const float x[3], const float (&gall)[4], int lane, f32x16& dc,
+                                                   float gx[3]) {
+  const XyzPack L{NC};
+  const int h = lane >> 5;
+  f32x16 dh = zero16();
+#pragma unroll
+  for (int j = 0; j < NOUT; ++j) {
+    const f32x16 w = vec_tile(pk + L.Wo() + 32 * j, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dh[r] += w[r] * gall[GOFS + j];
+  }
+  dc = zero16();
+  gemm_acc(dc, pk + L.FCT(4) * NSLAM_FRAG, dh, lane);
+  f32x16 da = apply_mask(dh, m[4]);
+  dh = zero16();
+  gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
+  gemm_acc(dc, pk + L.FCT(3) * NSLAM_FRAG, dh, lane);
+  const f32x16 da3 = apply_mask(dh, m[3]);
+  dh = zero16();
+  gemm_acc(dh, pk + (L.L3T() + 3) * NSLAM_FRAG, da3, lane);
+  gemm_acc(dc, pk + L.FCT(2) * NSLAM_FRAG, dh, lane);
+  da = apply_mask(dh, m[2]);
+  dh = zero16();
+  gemm_acc(dh, pk + L.L2T() * NSLAM_FRAG, da, lane);
+  gemm_acc(dc, pk + L.FCT(1) * NSLAM_FRAG, dh, lane);
+  da = apply_mask(dh, m[1]);
+  dh = zero16();
+  gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
+  gemm_acc(dc, pk + L.FCT(0) * NSLAM_FRAG, dh, lane);
+  gx[0] = gx[1] = gx[2] = 0.f;
+  if (EMBG) {
+    da = apply_mask(dh, m[0]);
+    const float* FB = pk + L.FB();
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      f32x16 de = zero16();
+      gemm_acc(de, pk + (L.L3T() + b) * NSLAM_FRAG, da3, lane);
+      gemm_acc(de, pk + (L.L0T() + b) * NSLAM_FRAG, da, lane);
+      const f32x16 cs = emb_tile<true>(FB, x, b, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = 32 * b + 8 * i + 4 * h;
+        const f32x4 B0 = *reinterpret_cast<const f32x4*>(FB + k);
+        const f32x4 B1 = *reinterpret_cast<const f32x4*>(FB + 96 + k);
+        const f32x4 B2 = *reinterpret_cast<const f32x4*>(FB + 192 + k);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float gk = de[4 * i + j] * cs[4 * i + j];
+          gx[0] += gk * B0[j];
+          gx[1] += gk * B1[j];
+          gx[2] += gk * B2[j];
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) gx[k] += xor32(gx[k]);
+  }
+}
+
+__device__ __forceinline__ void noxyz_backward_saved(const float* __restrict__ pk, const uint32_t m[5], float g,
+                                                     int lane, f32x16& dc) {
+  const NoXyzPack L;
+  f32x16 dh;
+  {
+    const f32x16 w = vec_tile(pk + L.Wo(), lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dh[r] = w[r] * g;
+  }
+  dc = zero16();
+  f32x16 da = apply_mask(dh, m[4]);
+  dh = zero16();
+  gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
+  da = apply_mask(dh, m[3]);
+  gemm_acc(dc, pk + L.L3T() * NSLAM_FRAG, da, lane);
+  dh = zero16();
+  gemm_acc(dh, pk + (L.L3T() + 1) * NSLAM_FRAG, da, lane);
+  da = apply_mask(dh, m[2]);
+  dh = zero16();
+  gemm_acc(dh, pk + L.L2T() * NSLAM_FRAG, da, lane);
+  da = apply_mask(dh, m[1]);
+  dh = zero16();
+  gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
+  da = apply_mask(dh, m[0]);
+  gemm_acc(dc, pk + L.L0T() * NSLAM_FRAG, da, lane);
+}
+
+// ------------------------------------------------------------------------------------------
 // grid gradient scatter (atomics shaped as two 128-B row segments per wave-instruction) and
 // coordinate gradient through the trilinear weights
 // ------------------------------------------------------------------------------------------
@@ -616,6 +728,7 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd(QueryKArgs a) {
     const float* pk = a.c.packed[NSLAM_DEC_COARSE];
     const NoXyzPack L;
     const f32x16 h4 = noxyz_forward<false>(pk, c, lane, m, nullptr);
+    save_masks(a, NSLAM_DEC_COARSE, tile, m, lane);
     out[3] = out_row(pk + L.Wo(), pk + L.Bo(), 0, h4, lane);
   } else {
     Corners cr;
@@ -625,6 +738,7 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd(QueryKArgs a) {
       const float* pk = a.c.packed[NSLAM_DEC_MIDDLE];
       const XyzPack L{1};
       const f32x16 h4 = xyz_forward<1, false>(pk, cm, q.x, lane, m, nullptr);
+      save_masks(a, NSLAM_DEC_MIDDLE, tile, m, lane);
       out[3] = out_row(pk + L.Wo(), pk + L.Bo(), 0, h4, lane);
     }
     if (STAGE >= NSLAM_STAGE_FINE) {
@@ -633,6 +747,7 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd(QueryKArgs a) {
       const float* pk = a.c.packed[NSLAM_DEC_FINE];
       const XyzPack L{2};
       const f32x16 h4 = xyz_forward<2, false>(pk, cf, q.x, lane, m, nullptr);
+      save_masks(a, NSLAM_DEC_FINE, tile, m, lane);
       out[3] = out_row(pk + L.Wo(), pk + L.Bo(), 0, h4, lane) + out[3];  // fine_occ + middle_occ
     }
     if (STAGE == NSLAM_STAGE_COLOR) {
@@ -641,6 +756,7 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd(QueryKArgs a) {
       const float* pk = a.c.packed[NSLAM_DEC_COLOR];
       const XyzPack L{1};
       const f32x16 h4 = xyz_forward<1, false>(pk, cc, q.x, lane, m, nullptr);
+      save_masks(a, NSLAM_DEC_COLOR, tile, m, lane);
 #pragma unroll
       for (int j = 0; j < 3; ++j) out[j] = out_row(pk + L.Wo(), pk + L.Bo(), j, h4, lane);
     }
@@ -668,11 +784,12 @@ constexpr int kScratchFloats = 2 * TILE_FLOATS + 32 * 4 + 32 * 3 + 32 * 8 * 2;
 constexpr int kWavesBwd = 4;
 constexpr int kMaxSlabs = 4096;  // WG == 2 above this many tiles
 
-template <int DEC, int WG, bool PG, bool FIRST>
+template <int DEC, int WG, bool PG, bool FIRST, bool SAVED>
 __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, const Slab& A, const Scratch& S,
-                                             int lane) {  // Every LDS-accumulator / scratch address is a function of the lane only, i.e. invariant across
-  // the tile loop; letting LICM hoist the ~300 of them pins (and spills) the register file.
-  // Re-derive them per tile.
+                                             int lane) {
+  // Every scratch / slab address is a function of the lane only, i.e. invariant across the tile
+  // loop; letting LICM hoist the ~300 of them pins (and spills) the register file.  Re-derive
+  // them per tile.
   asm volatile("" : "+v"(lane));
   const int h = lane >> 5, p = lane & 31;
   const int64_t idx = tile * 32 + p;
@@ -704,7 +821,18 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
   grid_corners(cr, gr, q);
   f32x16 dc;
   float gx[3] = {0.f, 0.f, 0.f};
-  if (DEC == NSLAM_DEC_COARSE) {
+  if (SAVED) {  // masks from the forward: no recompute (decoders without parameter gradients)
+    uint32_t m[5];
+    load_masks(a, DEC, tile, m, lane);
+    if (DEC == NSLAM_DEC_COARSE)
+      noxyz_backward_saved(pk, m, g[3], lane, dc);
+    else if (DEC == NSLAM_DEC_FINE)
+      xyz_backward_saved<2, 1, 3, PG>(pk, m, q.x, g, lane, dc, gx);
+    else if (DEC == NSLAM_DEC_COLOR)
+      xyz_backward_saved<1, 3, 0, PG>(pk, m, q.x, g, lane, dc, gx);
+    else
+      xyz_backward_saved<1, 1, 3, PG>(pk, m, q.x, g, lane, dc, gx);
+  } else if (DEC == NSLAM_DEC_COARSE) {
     const f32x16 c = gather_tile(gr.data, cr, lane);
     noxyz_backward<WG>(pk, c, g[3], dg, A, S, lane, dc);
   } else if (DEC == NSLAM_DEC_FINE) {
@@ -731,29 +859,37 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
   }
 }
 
-template <int DEC, int WG, bool PG, bool FIRST>
+template <int DEC, int WG, bool PG, bool FIRST, bool SAVED>
 __global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd(QueryKArgs a, float* __restrict__ slab,
                                                                  int acc_floats) {
-  __shared__ __attribute__((aligned(16))) float lds[kWavesBwd * kScratchFloats];
+  // per-wave scratch: the scatter needs sA + corner rows/weights; weight gradients add sX and
+  // the per-point tables (sizing LDS per variant keeps the lean kernels at 5+ waves/SIMD)
+  constexpr int kScr = WG ? kScratchFloats : TILE_FLOATS + 32 * 8 * 2;
+  __shared__ __attribute__((aligned(16))) float lds[kWavesBwd * kScr];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float* sc = lds + wave * kScratchFloats;
+  float* sc = lds + wave * kScr;
   Scratch S;
   S.sA = sc;
-  S.sX = sc + TILE_FLOATS;
-  S.gtab = sc + 2 * TILE_FLOATS;
-  S.xtab = S.gtab + 32 * 4;
-  S.crow = reinterpret_cast<int*>(S.xtab + 32 * 3);
+  if (WG) {
+    S.sX = sc + TILE_FLOATS;
+    S.gtab = sc + 2 * TILE_FLOATS;
+    S.xtab = S.gtab + 32 * 4;
+    S.crow = reinterpret_cast<int*>(S.xtab + 32 * 3);
+  } else {
+    S.sX = S.gtab = S.xtab = nullptr;
+    S.crow = reinterpret_cast<int*>(sc + TILE_FLOATS);
+  }
   S.cw = reinterpret_cast<float*>(S.crow + 32 * 8);
   const int64_t ntiles = (a.n + 31) / 32;
   const int64_t w = (int64_t)blockIdx.x * kWavesBwd + wave;
   const Slab A = make_slab(WG ? slab + (size_t)w * acc_floats : slab, WG ? acc_floats : 0);
   if (WG != 2) {  // one tile per wave (grid covers all tiles)
-    if (w < ntiles) dec_bwd_tile<DEC, WG, PG, FIRST>(a, w, A, S, lane);
+    if (w < ntiles) dec_bwd_tile<DEC, WG, PG, FIRST, SAVED>(a, w, A, S, lane);
     return;
   }
 #pragma nounroll
   for (int64_t tile = w; tile < ntiles; tile += (int64_t)gridDim.x * kWavesBwd)
-    dec_bwd_tile<DEC, WG, PG, FIRST>(a, tile, A, S, lane);
+    dec_bwd_tile<DEC, WG, PG, FIRST, SAVED>(a, tile, A, S, lane);
 }
 
 // base[j] += sum_b slab[b][j].  A workgroup owns 256 parameters (float4 per lane); each of its 16
@@ -847,10 +983,10 @@ int64_t n_slabs(int64_t tiles) {
   return tiles <= cap ? tiles : (cap + kWavesBwd - 1) / kWavesBwd * kWavesBwd;
 }
 
-template <int DEC, int WG, bool PG, bool FIRST>
+template <int DEC, int WG, bool PG, bool FIRST, bool SAVED = false>
 int launch_one(const QueryKArgs& a, float* slab, int acc, int64_t blocks, hipStream_t s) {
-  hipLaunchKernelGGL((k_dec_bwd<DEC, WG, PG, FIRST>), dim3((unsigned)blocks), dim3(64 * kWavesBwd), 0, s, a, slab,
-                     acc);
+  hipLaunchKernelGGL((k_dec_bwd<DEC, WG, PG, FIRST, SAVED>), dim3((unsigned)blocks), dim3(64 * kWavesBwd), 0, s, a,
+                     slab, acc);
   return hip_status();
 }
 
@@ -859,6 +995,9 @@ int launch_dec_bwd(const QueryKArgs& a, bool first, float* slab, hipStream_t s) 
   const int64_t tiles = (a.n + 31) / 32;
   if (WG == 0) {
     const int64_t blocks = (tiles + kWavesBwd - 1) / kWavesBwd;
+    if (a.c.saved_masks)
+      return first ? launch_one<DEC, 0, PG, true, true>(a, nullptr, 0, blocks, s)
+                   : launch_one<DEC, 0, PG, false, true>(a, nullptr, 0, blocks, s);
     return first ? launch_one<DEC, 0, PG, true>(a, nullptr, 0, blocks, s)
                  : launch_one<DEC, 0, PG, false>(a, nullptr, 0, blocks, s);
   }
@@ -903,7 +1042,57 @@ size_t bwd_ws_bytes(const nslam_query_cfg* cfg, int64_t n_pts) {
   return need;
 }
 
+size_t dec_ws_bytes(const nslam_query_cfg* cfg, int dec, int64_t n_pts) {
+  const nslam_dec_grad& dg = cfg->dgrad[dec];
+  if (!dg.base || dg.count <= 0) return 0;
+  return (size_t)n_slabs((n_pts + 31) / 32) * acc_floats_of(dg) * sizeof(float);
+}
+
+bool stage_uses(int stage, int dec) {
+  switch (stage) {
+    case NSLAM_STAGE_COARSE: return dec == NSLAM_DEC_COARSE;
+    case NSLAM_STAGE_MIDDLE: return dec == NSLAM_DEC_MIDDLE;
+    case NSLAM_STAGE_FINE: return dec == NSLAM_DEC_MIDDLE || dec == NSLAM_DEC_FINE;
+    default: return dec != NSLAM_DEC_COARSE;
+  }
+}
+
 }  // namespace
+
+extern "C" int nslam_query_bwd_decoder(const nslam_query_cfg* cfg, int32_t dec, int32_t accumulate_pts,
+                                       const double* pts, int64_t n_pts, const float* g_raw, double* g_pts, void* ws,
+                                       size_t ws_bytes, void* stream) {
+  const int rc = check_cfg(cfg, true);
+  if (rc) return rc;
+  if (dec < 0 || dec > 3 || !stage_uses(cfg->stage, dec)) return NSLAM_EINVAL;
+  if (n_pts < 0 || (n_pts > 0 && ((!pts && !cfg->rays_o) || !g_raw))) return NSLAM_EINVAL;
+  if (cfg->rays_o && (n_pts >= (int64_t(1) << 31) || n_pts % cfg->n_samples)) return NSLAM_EINVAL;
+  if (cfg->need_pts_grad && n_pts > 0 && !g_pts) return NSLAM_EINVAL;
+  if (n_pts == 0) return NSLAM_OK;
+  if (cfg->dgrad[dec].base && cfg->dgrad[dec].count <= 0) return NSLAM_EUNSUPPORTED;
+  const size_t need = dec_ws_bytes(cfg, dec, n_pts);
+  if (ws_bytes < need || (need > 0 && !ws)) return NSLAM_EWORKSPACE;
+  QueryKArgs a{*cfg, pts, n_pts, nullptr, g_raw, g_pts};
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  float* slab = reinterpret_cast<float*>(ws);
+  const bool first = !accumulate_pts;
+  switch (dec) {
+    case NSLAM_DEC_COARSE: return dispatch_dec_bwd<NSLAM_DEC_COARSE>(a, first, slab, s);
+    case NSLAM_DEC_MIDDLE: return dispatch_dec_bwd<NSLAM_DEC_MIDDLE>(a, first, slab, s);
+    case NSLAM_DEC_FINE: return dispatch_dec_bwd<NSLAM_DEC_FINE>(a, first, slab, s);
+    default: return dispatch_dec_bwd<NSLAM_DEC_COLOR>(a, first, slab, s);
+  }
+}
+
+extern "C" size_t nslam_query_bwd_decoder_workspace_size(const nslam_query_cfg* cfg, int32_t dec, int64_t n_pts) {
+  if (!cfg || dec < 0 || dec > 3 || n_pts <= 0) return 0;
+  return dec_ws_bytes(cfg, dec, n_pts);
+}
+
+extern "C" size_t nslam_query_saved_size(int64_t n_pts) {
+  if (n_pts <= 0) return 0;
+  return (size_t)4 * ((n_pts + 31) / 32) * 5 * 64 * sizeof(uint16_t);
+}
 
 extern "C" size_t nslam_query_bwd_workspace_size(const nslam_query_cfg* cfg, int64_t n_pts) {
   if (!cfg || n_pts <= 0) return 0;

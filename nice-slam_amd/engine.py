@@ -74,6 +74,8 @@ class MappingEngine:
         self.decs = {n: FlatDecoder(nice.decoder(n)) for n in names}
         self.dec_bounds = {n: ops._bound_list(nice.decoder(n).bound) for n in names}
         self.oob = ops._bound_list(bound)
+        self._saved = None  # ReLU masks of the last query_fwd (read by query_bwd)
+        self._side = []     # side streams of the concurrent decoder backward
         # one flat gradient buffer for every grid: zeroing is a single memset
         sizes = {k: v.numel() for k, v in c.items()}
         self.gbuf = torch.zeros(sum(sizes.values()), dtype=torch.float32, device=self.device)
@@ -98,26 +100,51 @@ class MappingEngine:
         dg = {n: self.decs[n].grad for n in decs if n in dec_grads}
         cfg = ops._fill_cfg(meta, pairs, packed, dg, False)
         cfg.rays_o, cfg.rays_d, cfg.z_vals, cfg.n_samples = ptr(ro), ptr(rd), ptr(z), z.shape[1]
+        cfg.saved_masks = ptr(self._saved)
         return cfg
 
     def query_fwd(self, stage, ro, rd, z):
+        """raw [N*S, 4]; also saves the ReLU masks the backward of frozen decoders uses."""
         n = z.numel()
         raw = torch.empty(n, 4, dtype=torch.float32, device=z.device)
+        self._saved = torch.empty(lib().nslam_query_saved_size(n), dtype=torch.uint8, device=z.device)
         cfg = self._cfg(stage, ro, rd, z, (), ())
         with ops._span("query_fwd"):
             rc = lib().nslam_query_fwd(ctypes.byref(cfg), None, n, ptr(raw), stream_ptr(z.device))
         check(rc, "nslam_query_fwd")
         return raw
 
-    def query_bwd(self, stage, ro, rd, z, g_raw, grid_grads, dec_grads):
+    def query_bwd(self, stage, ro, rd, z, g_raw, grid_grads, dec_grads, concurrent=True):
+        """Backward into the engine's gradient buffers.  The decoders write disjoint buffers, so
+        each runs as its own launch; with `concurrent` the frozen decoders (mask-only backward,
+        atomics-heavy) run on side streams beside the one with weight gradients (MFMA-heavy) —
+        parallel branches when captured in a hipGraph."""
         n = z.numel()
         cfg = self._cfg(stage, ro, rd, z, grid_grads, dec_grads)
-        wsb = lib().nslam_query_bwd_workspace_size(ctypes.byref(cfg), n)
-        ws = torch.empty(wsb, dtype=torch.uint8, device=z.device) if wsb else None
+        decs = sorted(ops._DEC_FOR_STAGE[stage], key=lambda d: d not in dec_grads)  # weight-grad one first
+        main = torch.cuda.current_stream(z.device)
+        streams = [main]
+        if concurrent:
+            while len(self._side) < len(decs) - 1:
+                self._side.append(torch.cuda.Stream(z.device))
+            streams += self._side[:len(decs) - 1]
+        used = streams[1:]
         with ops._span("query_bwd"):
-            rc = lib().nslam_query_bwd(ctypes.byref(cfg), None, n, ptr(g_raw), None, ptr(ws), wsb,
-                                       stream_ptr(z.device))
-        check(rc, "nslam_query_bwd")
+            for st in used:  # fork: every branch starts from the same point of the main stream
+                st.wait_stream(main)
+                for t in (ro, rd, z, g_raw, self._saved):
+                    t.record_stream(st)
+            for i, name in enumerate(decs):
+                st = streams[i] if concurrent else main
+                d = ops._DEC_ID[name]
+                with torch.cuda.stream(st):
+                    wsb = lib().nslam_query_bwd_decoder_workspace_size(ctypes.byref(cfg), d, n)
+                    ws = torch.empty(wsb, dtype=torch.uint8, device=z.device) if wsb else None
+                    rc = lib().nslam_query_bwd_decoder(ctypes.byref(cfg), d, 0, None, n, ptr(g_raw), None, ptr(ws),
+                                                       wsb, st.cuda_stream)
+                check(rc, "nslam_query_bwd_decoder")
+            for st in used:
+                main.wait_stream(st)
 
     # -- one iteration ---------------------------------------------------------------------------
     def grads_for(self, stage, trainable_decoders):

@@ -192,12 +192,17 @@ class _Query(torch.autograd.Function):
             off += n
         raw = torch.empty(pts.shape[0], 4, dtype=torch.float32, device=pts.device)
         cfg = _fill_cfg(meta, [(g, None) if g is not None else (None, None) for g in grids], packed, {}, False)
+        saved = None
+        if torch.is_grad_enabled() and any(ctx.needs_input_grad):  # ReLU masks for the backward
+            saved = torch.empty(lib().nslam_query_saved_size(pts.shape[0]), dtype=torch.uint8, device=pts.device)
+            cfg.saved_masks = saved.data_ptr()
         with _span("query_fwd"):
             rc = lib().nslam_query_fwd(ctypes.byref(cfg), ptr(pts), pts.shape[0], ptr(raw), stream_ptr(pts.device))
         check(rc, "nslam_query_fwd")
         ctx.meta = meta
         ctx.packed = packed
         ctx.grids = grids
+        ctx.saved_masks = saved
         ctx.save_for_backward(pts)
         return raw
 
@@ -223,6 +228,8 @@ class _Query(torch.autograd.Function):
             off += n
         g_pts = torch.empty_like(pts) if need_pts else None
         cfg = _fill_cfg(meta, pairs, ctx.packed, dgrads, need_pts)
+        if ctx.saved_masks is not None:
+            cfg.saved_masks = ctx.saved_masks.data_ptr()
         wsb = lib().nslam_query_bwd_workspace_size(ctypes.byref(cfg), pts.shape[0])
         ws = torch.empty(wsb, dtype=torch.uint8, device=pts.device) if wsb else None
         with _span("query_bwd"):

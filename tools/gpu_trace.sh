@@ -1,0 +1,6 @@
+set -o pipefail
+OUT=gpurun_out/${1:?tag}
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace -o run -- python bench.py --steps 8 --warmup 3 --no-cpu-baseline ${2:-} > $OUT/trace.log 2>&1 || { tail -20 $OUT/trace.log; exit 1; }
+python tools/timeline.py $OUT/trace/run_kernel_trace.csv > $OUT/timeline.txt && tail -45 $OUT/timeline.txt
