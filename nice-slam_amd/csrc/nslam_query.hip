@@ -107,6 +107,23 @@ struct Scratch {
 // only the wave's own LDS counter drained (and a compiler memory barrier), not a workgroup barrier.
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// Phase timing (debug build only, make phases): lane 0 of each backward wave records s_memtime
+// at marks 0..15 of its tile into g_phase[decoder][wave][16].
+#ifdef NSLAM_PHASES
+constexpr int kPhaseWaves = 1 << 15;
+__device__ unsigned long long g_phase[4 * kPhaseWaves * 16];
+#define PHASE(dec, k)                                                                                     \
+  do {                                                                                                    \
+    const int64_t w_ = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);                     \
+    if ((threadIdx.x & 63) == 0 && w_ < kPhaseWaves)                                                      \
+      g_phase[((size_t)(dec) * kPhaseWaves + w_) * 16 + (k)] = __builtin_amdgcn_s_memtime();              \
+  } while (0)
+#else
+#define PHASE(dec, k) \
+  do {                \
+  } while (0)
+#endif
+
 // ReLU masks saved by the forward: [decoder][tile][layer][64 lanes] uint16 (one 128-B row per layer)
 __device__ __forceinline__ uint16_t* mask_slot(const QueryKArgs& a, int dec, int64_t tile) {
   const int64_t ntiles = (a.n + 31) / 32;
@@ -274,10 +291,12 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
                                              const float x[3], const float (&gall)[4], const nslam_dec_grad& dg,
                                              const Slab& A, const Scratch& S, int lane, f32x16& dc, float gx[3]) {
   const XyzPack L{NC};
+  constexpr int DEC_ = NOUT == 3 ? 3 : (NC == 2 ? 2 : 1);
   const int h = lane >> 5;
   uint32_t m[5];
   f32x16 hs[4];
   const f32x16 h4 = xyz_forward<NC, WG != 0>(pk, cin, x, lane, m, hs);
+  PHASE(DEC_, 4);
 
   // output layer: dh4 = Wo^T g
   f32x16 dh = zero16();
@@ -318,6 +337,7 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
   }
   dc = zero16();
   const float* FB = pk + L.FB();
+  PHASE(DEC_, 5);
 
   // layer 4
   fc_bwd<NC, WG>(pk, L, 4, cin, dh, dg, A, S, lane, dc);
@@ -329,6 +349,7 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
   }
   dh = zero16();
   gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
+  PHASE(DEC_, 6);
   // layer 3 (input = [emb | h2])
   fc_bwd<NC, WG>(pk, L, 3, cin, dh, dg, A, S, lane, dc);
   const f32x16 da3 = apply_mask(dh, m[3]);
@@ -342,6 +363,7 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
   }
   dh = zero16();
   gemm_acc(dh, pk + (L.L3T() + 3) * NSLAM_FRAG, da3, lane);
+  PHASE(DEC_, 7);
   // layer 2
   fc_bwd<NC, WG>(pk, L, 2, cin, dh, dg, A, S, lane, dc);
   da = apply_mask(dh, m[2]);
@@ -352,6 +374,7 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
   }
   dh = zero16();
   gemm_acc(dh, pk + L.L2T() * NSLAM_FRAG, da, lane);
+  PHASE(DEC_, 8);
   // layer 1
   fc_bwd<NC, WG>(pk, L, 1, cin, dh, dg, A, S, lane, dc);
   da = apply_mask(dh, m[1]);
@@ -362,6 +385,7 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
   }
   dh = zero16();
   gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
+  PHASE(DEC_, 9);
   // layer 0 (input = emb)
   fc_bwd<NC, WG>(pk, L, 0, cin, dh, dg, A, S, lane, dc);
   da = apply_mask(dh, m[0]);
@@ -373,6 +397,7 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
     wg_end<WG>(A, dg.b[0], S, lane);
   }
 
+  PHASE(DEC_, 10);
   // Fourier features: de_b = L3T_b da3 + L0T_b da0 ; G = de * cos(theta)
   gx[0] = gx[1] = gx[2] = 0.f;
   if (EMBG) {
@@ -423,6 +448,7 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
 #pragma unroll
     for (int k = 0; k < 3; ++k) gx[k] += xor32(gx[k]);
   }
+  PHASE(DEC_, 11);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -640,13 +666,70 @@ __device__ __forceinline__ void noxyz_backward_saved(const float* __restrict__ p
 // grid gradient scatter (atomics shaped as two 128-B row segments per wave-instruction) and
 // coordinate gradient through the trilinear weights
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void scatter_grid_grad(float* __restrict__ grad, const Corners& cr, const f32x16& dc,
+__device__ __forceinline__ void scatter_grid_grad_uniform(float* __restrict__ grad, const Corners& cr, const f32x16& dc,
                                                   bool valid, const Scratch& S, int lane) {
   // Points of a tile are consecutive samples of (mostly) one ray: runs of samples that fall in the
-  // same cell are summed in registers first, so each run costs 8 row-atomics instead of 8 per
-  // sample (surface samples cluster in 1-3 cells; this is what removes the atomic contention on
-  // the small middle grid).  Half h walks points 16h..16h+15; lane = channel, so every atomic
-  // wave-instruction is one or two 128-B row segments.
+  // same cell are summed in registers first, so a run costs one flush instead of one per sample.
+  // The whole wave walks the tile's 32 points in step (uniform control flow, runs merged over the
+  // whole tile); lane (h, ch) owns channel ch of corners 2j + h, j = 0..3.  Corners 2j and 2j+1
+  // differ only in x, i.e. are adjacent rows of the channels-last grid, so every flush
+  // wave-instruction adds one contiguous 256-B segment — the full-rate shape of a float atomic.
+  const int h = lane >> 5, ch = lane & 31;
+  tstore(S.sA, dc, lane);
+  if (h == 0) {
+    const int p = lane & 31;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      S.crow[p * 8 + k] = cr.row[k];
+      S.cw[p * 8 + k] = valid ? cr.w[k] : 0.f;
+    }
+  }
+  lds_sync();
+  float acc[4], wsum[4];
+  int rows[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    acc[j] = 0.f;
+    wsum[j] = 0.f;
+    rows[j] = 0;
+  }
+  int cur = -1;
+  for (int t = 0; t < 32; ++t) {
+    const int cell = __builtin_amdgcn_readfirstlane(S.crow[t * 8]);  // corner 0 = the cell, always in range
+    if (cell != cur) {
+      if (cur >= 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (wsum[j] != 0.f) unsafeAtomicAdd(grad + (size_t)rows[j] * NSLAM_C_DIM + ch, acc[j]);
+      }
+      cur = cell;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[j] = 0.f;
+        wsum[j] = 0.f;
+        rows[j] = S.crow[t * 8 + 2 * j + h];
+      }
+    }
+    const float v = S.sA[t * TPITCH + ch];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float w = S.cw[t * 8 + 2 * j + h];
+      acc[j] += w * v;
+      wsum[j] += w;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (wsum[j] != 0.f) unsafeAtomicAdd(grad + (size_t)rows[j] * NSLAM_C_DIM + ch, acc[j]);
+  lds_sync();
+}
+
+// Per-half variant (weight-gradient kernels): half h walks points 16h..16h+15 on its own, every
+// flush wave-instruction is one 128-B row segment.  Kept for the register-starved weight-gradient
+// kernels, where the uniform variant above coincided with an illegal-address fault in the fine
+// decoder's kernel (both runs of tests/test_gpu_parity.py eval fine, r1k and r1l).
+__device__ __forceinline__ void scatter_grid_grad_halves(float* __restrict__ grad, const Corners& cr,
+                                                         const f32x16& dc, bool valid, const Scratch& S, int lane) {
   const int h = lane >> 5, ch = lane & 31;
   tstore(S.sA, dc, lane);
   if (h == 0) {
@@ -791,6 +874,7 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
   // loop; letting LICM hoist the ~300 of them pins (and spills) the register file.  Re-derive
   // them per tile.
   asm volatile("" : "+v"(lane));
+  PHASE(DEC, 0);
   const int h = lane >> 5, p = lane & 31;
   const int64_t idx = tile * 32 + p;
   const Pt q = load_point(a, idx);
@@ -817,8 +901,10 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
   // The weight fragments are loop-invariant across the tile loop; hoisting their ~100 loads out of
   // the loop would pin hundreds of registers.  Launder the base pointer per tile so they stay put.
   asm volatile("" : "+s"(pk));
+  PHASE(DEC, 1);
   Corners cr;
   grid_corners(cr, gr, q);
+  PHASE(DEC, 2);
   f32x16 dc;
   float gx[3] = {0.f, 0.f, 0.f};
   if (SAVED) {  // masks from the forward: no recompute (decoders without parameter gradients)
@@ -843,12 +929,20 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
     xyz_backward<2, 1, 3, WG, PG || WG>(pk, cf, q.x, g, dg, A, S, lane, dc, gx);
   } else {
     const f32x16 c[1] = {gather_tile(gr.data, cr, lane)};
+    PHASE(DEC, 3);
     if (DEC == NSLAM_DEC_COLOR)  // the colour decoder's 4th output is overwritten by the combiner
       xyz_backward<1, 3, 0, WG, PG || WG>(pk, c, q.x, g, dg, A, S, lane, dc, gx);
     else
       xyz_backward<1, 1, 3, WG, PG || WG>(pk, c, q.x, g, dg, A, S, lane, dc, gx);
   }
-  if (gr.grad) scatter_grid_grad(gr.grad, cr, dc, q.valid, S, lane);
+  PHASE(DEC, 12);
+  if (gr.grad) {
+    if (WG)
+      scatter_grid_grad_halves(gr.grad, cr, dc, q.valid, S, lane);
+    else
+      scatter_grid_grad_uniform(gr.grad, cr, dc, q.valid, S, lane);
+  }
+  PHASE(DEC, 13);
   if (PG) {
     double gp[3] = {(double)gx[0], (double)gx[1], (double)gx[2]};
     coord_grad(gr, cr, dc, lane, gp);
@@ -857,6 +951,7 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
       for (int k = 0; k < 3; ++k) a.g_pts[idx * 3 + k] = FIRST ? gp[k] : a.g_pts[idx * 3 + k] + gp[k];
     }
   }
+  PHASE(DEC, 14);
 }
 
 template <int DEC, int WG, bool PG, bool FIRST, bool SAVED>
@@ -1024,6 +1119,16 @@ template <int DEC>
 int dispatch_dec_bwd(const QueryKArgs& a, bool first, float* slab, hipStream_t s) {
   const bool wg = a.c.dgrad[DEC].base != nullptr;
   const bool pg = a.c.need_pts_grad != 0;
+  if (wg && pg && a.c.saved_masks) {
+    // Split instead of the combined kernel (which spills ~100 VGPRs): parameter + grid gradients
+    // first, then d/dpts from the saved masks with the grid scatter switched off.
+    int rc = launch_dec_bwd<DEC, 1, false>(a, first, slab, s);
+    if (rc) return rc;
+    QueryKArgs b = a;
+    b.c.grid[DEC].grad = nullptr;
+    b.c.dgrad[DEC].base = nullptr;
+    return launch_dec_bwd<DEC, 0, true>(b, first, nullptr, s);
+  }
   if (wg && pg) return launch_dec_bwd<DEC, 1, true>(a, first, slab, s);
   if (wg) return launch_dec_bwd<DEC, 1, false>(a, first, slab, s);
   if (pg) return launch_dec_bwd<DEC, 0, true>(a, first, slab, s);
@@ -1155,3 +1260,10 @@ extern "C" int nslam_pack_layout(int kind, int nc, int32_t* out, int n) {
   }
   return 4;
 }
+
+#ifdef NSLAM_PHASES
+extern "C" int nslam_debug_phases(unsigned long long* out, int64_t n) {
+  if (n > (int64_t)4 * kPhaseWaves * 16) n = (int64_t)4 * kPhaseWaves * 16;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -76,6 +76,7 @@ class MappingEngine:
         self.oob = ops._bound_list(bound)
         self._saved = None  # ReLU masks of the last query_fwd (read by query_bwd)
         self._side = []     # side streams of the concurrent decoder backward
+        self.concurrent = True
         # one flat gradient buffer for every grid: zeroing is a single memset
         sizes = {k: v.numel() for k, v in c.items()}
         self.gbuf = torch.zeros(sum(sizes.values()), dtype=torch.float32, device=self.device)
@@ -114,12 +115,13 @@ class MappingEngine:
         check(rc, "nslam_query_fwd")
         return raw
 
-    def query_bwd(self, stage, ro, rd, z, g_raw, grid_grads, dec_grads, concurrent=True):
+    def query_bwd(self, stage, ro, rd, z, g_raw, grid_grads, dec_grads, concurrent=None):
         """Backward into the engine's gradient buffers.  The decoders write disjoint buffers, so
         each runs as its own launch; with `concurrent` the frozen decoders (mask-only backward,
         atomics-heavy) run on side streams beside the one with weight gradients (MFMA-heavy) —
         parallel branches when captured in a hipGraph."""
         n = z.numel()
+        concurrent = self.concurrent if concurrent is None else concurrent
         cfg = self._cfg(stage, ro, rd, z, grid_grads, dec_grads)
         decs = sorted(ops._DEC_FOR_STAGE[stage], key=lambda d: d not in dec_grads)  # weight-grad one first
         main = torch.cuda.current_stream(z.device)

@@ -1,0 +1,55 @@
+"""Per-phase cycle breakdown of the backward tile (instrumented build, make -C nice-slam_amd/csrc phases).
+
+NSLAM_LIB=nice-slam_amd/libnslam_phases.so python tools/probes/phases.py
+Runs room0 colour-stage mapping iterations with sequential decoder launches and prints, per
+decoder kernel, the distribution over waves of the cycles between consecutive s_memtime marks.
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, REPO)
+os.environ.setdefault("NSLAM_LIB", os.path.join(REPO, "nice-slam_amd", "libnslam_phases.so"))
+import bench  # noqa: E402
+
+NAMES = {0: "start", 1: "point+g", 2: "corners", 3: "gather", 4: "fwd recompute", 5: "out layer(+dWo)",
+         6: "layer4", 7: "layer3", 8: "layer2", 9: "layer1", 10: "layer0", 11: "fourier", 12: "pre-scatter",
+         13: "scatter", 14: "end"}
+
+
+def main():
+    dev = torch.device("cuda:0")
+    P = bench.pkg()
+    scene = bench.Room0Scene(dev, 0, path="fused")
+    scene.engine.concurrent = False
+    for _ in range(4):
+        scene.step()
+    torch.cuda.synchronize()
+    L = P._lib.lib()
+    L.nslam_debug_phases.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    W = 1 << 15
+    buf = np.zeros(4 * W * 16, dtype=np.uint64)
+    assert L.nslam_debug_phases(buf.ctypes.data, buf.size) == 0
+    buf = buf.reshape(4, W, 16).astype(np.int64)
+    tiles = (scene.cfg["pixels"] * 48 + 31) // 32
+    for d, nm in ((1, "middle"), (2, "fine"), (3, "color")):
+        t = buf[d, :tiles]
+        marks = [k for k in range(16) if (t[:, k] != 0).all()]
+        print(f"== {nm} decoder backward: {tiles} waves, marks {marks}")
+        tot = t[:, marks[-1]] - t[:, marks[0]]
+        st = t[:, marks[0]] - t[:, marks[0]].min()
+        print(f"   wave total cycles: median {np.median(tot):.0f}  p10 {np.percentile(tot, 10):.0f}  "
+              f"p90 {np.percentile(tot, 90):.0f};  start spread p50 {np.median(st):.0f} max {st.max():.0f}; "
+              f"kernel span {(t[:, marks[-1]].max() - t[:, marks[0]].min()):.0f}")
+        for a, b in zip(marks[:-1], marks[1:]):
+            dt = t[:, b] - t[:, a]
+            print(f"   {NAMES[a]:>16s} -> {NAMES[b]:<16s} median {np.median(dt):8.0f}  mean {dt.mean():8.0f}  "
+                  f"({100 * np.median(dt) / max(np.median(tot), 1):5.1f}%)")
+
+
+if __name__ == "__main__":
+    main()
