@@ -137,6 +137,8 @@ class Room0Scene:
                 [{"params": [self.engine.decs["color"].param], "lr": cfg["lr"]["decoders"]}] +
                 [{"params": [self.grids[k]], "lr": cfg["lr"][k[5:]], "rows": self.rows[k]}
                  for k in ("grid_middle", "grid_fine", "grid_color")])
+            # ray-sharded: all-reduce only the frustum rows Adam reads (+ colour-decoder grads)
+            self.exchange = P.distributed.SparseGradExchange(self.engine, self.rows)
         else:
             params = [{"params": list(self.nice.color_decoder.parameters()), "lr": cfg["lr"]["decoders"]},
                       {"params": [self.grids["grid_middle"]], "lr": cfg["lr"]["middle"]},
@@ -170,7 +172,7 @@ class Room0Scene:
         _, keep = self.engine.iteration(
             stage, self.frames, pix, n, (H, W), (cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"]), self.opt,
             trainable_decoders=("color",), gt_max=(lambda g: D.global_max(g)) if sharded else None,
-            allreduce=(lambda gs: D.allreduce_tensors(gs)) if sharded else None)
+            exchange=self.exchange if sharded else None)
         return keep.sum() * (cfg["n_strat"] + cfg["n_surf"])
 
     def step_autograd(self, stage="color", sharded=False):
@@ -242,6 +244,79 @@ def cpu_baseline(scene, budget_s=20.0):
                       f"1 warm-up, oracle/nslam_oracle.py on {threads} host threads, {dt:.1f} s"}
 
 
+def stress_grid_query(dev, side=512, rays=65536, samples=64, reps=10):
+    """The grid-query kernel alone at BASELINE.json's HBM-roofline stress shape:
+    one fine grid of side³ voxels × 32 ch fp32 (512³: 16 GiB, far beyond the 256 MiB Infinity
+    Cache), 65536 rays × 64 samples through it (random origins and directions in the unit cube,
+    samples evenly spaced to the exit), nslam_grid_sample_fwd timed with HIP events on its stream.
+    Algorithmic bytes per point: 8 corners × 128 B read + 128 B feature row written + 12 B coords."""
+    P = pkg()
+    g = torch.Generator(device=dev).manual_seed(7)
+    grid = torch.empty(1, side, side, side, 32, device=dev).normal_(0.0, 1e-4, generator=g).permute(0, 4, 1, 2, 3)
+    o = torch.rand(rays, 3, device=dev, generator=g) * 2 - 1
+    d = torch.randn(rays, 3, device=dev, generator=g)
+    d = d / d.norm(dim=1, keepdim=True)
+    t = torch.maximum((1 - o) / d, (-1 - o) / d).min(1).values              # exit distance (>0)
+    z = torch.linspace(0.0, 1.0, samples, device=dev)[None] * t[:, None]
+    coords = (o[:, None] + d[:, None] * z[..., None]).clamp_(-1, 1).reshape(-1, 3).contiguous()
+    n = coords.shape[0]
+    out = torch.empty(n, 32, device=dev)
+    P.ops.grid_sample_fwd(grid, coords, out)                                  # warm-up
+    P.ops.TIMER = P.ops.KernelTimer()
+    for _ in range(reps):
+        P.ops.grid_sample_fwd(grid, coords, out)
+    tm = P.ops.TIMER.summary()["grid_fwd"]
+    P.ops.TIMER = None
+    bpp = 8 * 128 + 128 + 12
+    achieved = n * bpp / (tm["avg_ms"] * 1e-3) / 1e9
+    del grid, out, coords
+    torch.cuda.empty_cache()
+    return {"kernel": "k_grid_fwd (nslam_grid_sample_fwd)", "bound": "hbm", "achieved": achieved,
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+            "avg_launch_ms": tm["avg_ms"], "points": n, "bytes_per_point": bpp,
+            "workload": f"grid [1,32,{side},{side},{side}] fp32 channels-last (16 GiB), {rays} rays x {samples} "
+                        "samples, random rays through the cube"}
+
+
+def reference_gpu_baseline(scene, budget_s=4.0):
+    """The reference's PyTorch path ON THE GPU, for the ≥10x target of BASELINE.json: the oracle's
+    restatement of Renderer.render_batch_ray + Mapper loss (the same torch ops the reference issues:
+    F.grid_sample, nn.Linear, cumprod, autograd, torch.optim.Adam) on the same device-resident
+    workload.  It omits the reference's per-iteration masked-grid copies (Mapper.py:394-401,
+    511-519), so it is if anything faster than the reference."""
+    from oracle import nslam_oracle as orc
+    dev = scene.dev
+    bound = scene.bound.to(dev)
+    grids = {k: v.detach().clone().requires_grad_(True) for k, v in scene.grids.items()}
+    sd = {k: v.detach().clone() for k, v in scene.nice.state_dict().items()}
+    for k in list(sd):
+        if k.startswith("color_decoder."):
+            sd[k].requires_grad_(True)
+    opt = torch.optim.Adam([v for v in sd.values() if v.requires_grad] + list(grids.values()), lr=0.005)
+    samples, iters = 0, 0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while iters < 3 or (time.perf_counter() - t0 < budget_s and iters < 400):
+        if iters == 2:  # two warm-up iterations
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+        ro, rd, gt, gc = scene.sample_batch()
+        keep = orc.inside_mask(ro, rd, gt, bound)
+        ro, rd, gt, gc = ro[keep], rd[keep], gt[keep], gc[keep]
+        opt.zero_grad()
+        d, v, c = orc.render_batch_ray(sd, grids, rd, ro, "color", bound, gt)
+        orc.mapper_loss(d, c, gt, gc, "color").backward()
+        opt.step()
+        if iters >= 2:
+            samples += ro.shape[0] * 48
+        iters += 1
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"value": samples / dt, "unit": "ray-samples/s", "ms_per_step": dt / (iters - 2) * 1e3,
+            "sample": f"{iters - 2} colour-stage mapping iterations after 2 warm-ups: oracle/nslam_oracle.py "
+                      "(torch ops of the reference path) on the GPU, eager"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -249,6 +324,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture")
+    ap.add_argument("--no-stress", action="store_true", help="skip the 512^3 grid-query HBM measurement")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="process-group backend for N>1 (gloo: rehearse the sharded path on one GPU, eager)")
     ap.add_argument("--pixels", type=int, default=None,
                     help="override mapping pixels per iteration (scaling studies; the metric uses room0's 1000)")
     ap.add_argument("--path", choices=("fused", "autograd"), default="fused",
@@ -257,9 +335,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.backend == "gloo":  # rehearsal of the sharded path with several ranks on one GPU
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     P = pkg()
     cfg = dict(ROOM0)
@@ -271,7 +354,7 @@ def main():
         scene.step(sharded=sharded)
     torch.cuda.synchronize()
     graph, mode = None, "eager"
-    if not args.eager:
+    if not args.eager and not (world > 1 and args.backend == "gloo"):
         try:  # capture one whole mapping iteration as a hipGraph (removes per-op host launch cost)
             side = torch.cuda.Stream()
             side.wait_stream(torch.cuda.current_stream())
@@ -340,7 +423,7 @@ def main():
             "config": {"workload": "Replica room0 mapping iteration, colour stage: 1000 pixels x 48 samples "
                                    "(5-frame window x 200), grids middle/fine/colour, Adam",
                        "global_batch": int(round(pts_per_step)) * world, "seq_len": 48,
-                       "parallelism": f"rays sharded dp{world}, RCCL all-reduce of gradients"},
+                       "parallelism": f"rays sharded dp{world}, RCCL all-reduce of the frustum-row gradients"},
             "roofline": {"kernel": dom_name, "bound": "mfma", "achieved": achieved, "peak": F32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / F32_PEAK_TFLOPS, "traffic": None,
                          "avg_launch_ms": dom["avg_ms"],
@@ -350,8 +433,17 @@ def main():
             "query_fwd_hbm_frac": (pts_per_step * BYTES_FWD_PER_SAMPLE / (qf["avg_ms"] * 1e-3) / 1e9) / HBM_PEAK_GBS,
             "query_bwd_ms": qb["avg_ms"],
         }
+        if sharded and args.path == "fused":
+            keys, dn = scene.engine.grads_for("color", ("color",))
+            out["exchange_bytes_per_step"] = scene.exchange.payload_bytes(keys, dn)
+            out["dense_grad_bytes_per_step"] = scene.engine.gbuf.numel() * 4
+        if world == 1 and not args.no_stress:
+            out["grid_query_stress"] = stress_grid_query(dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(scene)
+            ref = reference_gpu_baseline(scene)
+            out["reference_gpu_path"] = ref
+            out["vs_reference_gpu_path"] = out["value"] / ref["value"]
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

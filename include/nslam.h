@@ -205,8 +205,8 @@ size_t nslam_render_loss_workspace_size(const nslam_loss_cfg* cfg, int64_t n_ray
  * (Mapper.py:314-333), updated in place in the dense grid with state for the selected rows only
  * (exp_avg/exp_avg_sq are [n][row_len], in row-list order).  Like torch, every segment has its
  * own step count (`step`, a device float, 0 before the first update): the launch uses step+1
- * and the last workgroup to finish advances every segment's step (graph-replay safe); `ticket`
- * is a device uint32 the caller zero-initialises once.  Pass only segments that have a gradient
+ * and a second single-wave launch advances every segment's step (graph-replay safe); `ticket`
+ * is unused since ABI v5 (may be NULL).  Pass only segments that have a gradient
  * this iteration (torch skips parameters whose .grad is None).  With zero_grad the grad entries
  * read are reset to 0. */
 #define NSLAM_ADAM_MAX_SEGS 16
@@ -223,6 +223,18 @@ typedef struct nslam_adam_seg {
 } nslam_adam_seg;
 int nslam_adam_step(const nslam_adam_seg* segs, int32_t n_segs, float beta1, float beta2, float eps,
                     int32_t zero_grad, uint32_t* ticket, void* stream);
+
+/* Sparse gradient exchange of a ray-sharded mapping iteration (ABI v5).  Only the frustum-
+ * selected grid rows reach Adam (Mapper.py:314-333,394-401,504), so only they need summing across
+ * ranks: nslam_rows_pack copies rows[i] (row_len floats each, row_len % 4 == 0, 16-byte aligned
+ * grid and out) of `grid` to out[i*row_len ...] and appends the n_tail floats of `tail` (the
+ * decoder gradients); the caller all-reduces `out` (n_rows*row_len + n_tail floats) and
+ * nslam_rows_unpack writes it back.  Row indices are in units of row_len floats from `grid`, so
+ * one call covers every grid of a flat gradient buffer. */
+int nslam_rows_pack(const float* grid, const int32_t* rows, int64_t n_rows, int32_t row_len, const float* tail,
+                    int64_t n_tail, float* out, void* stream);
+int nslam_rows_unpack(const float* in, const int32_t* rows, int64_t n_rows, int32_t row_len, float* grid,
+                      float* tail, int64_t n_tail, void* stream);
 
 enum { NSLAM_WS_SAMPLER = 0 };
 size_t nslam_workspace_size(int which, int64_t n);

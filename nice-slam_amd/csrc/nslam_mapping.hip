@@ -92,7 +92,6 @@ struct AdamArgs {
   int32_t nseg;
   float b1, b2, eps;
   int32_t zero_grad;
-  uint32_t* ticket;
 };
 
 constexpr int kAdamThreads = 256;
@@ -167,20 +166,73 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam(AdamArgs a) {
       if (a.zero_grad) *reinterpret_cast<f32x4*>(sg.grad + base) = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
-  // the last workgroup to finish advances every segment's step (all have read theirs by then)
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    const unsigned tk = atomicAdd(a.ticket, 1u);
-    if (tk == gridDim.x - 1) {
-      for (int k = 0; k < a.nseg; ++k) *a.seg[k].step += 1.f;
-      *a.ticket = 0u;
-      __threadfence();
-    }
+}
+
+// Every segment's step advances after the update kernel, in its own single-wave launch (stream
+// order makes it see all reads of the old count).  The previous last-workgroup ticket needed a
+// device-scope release fence (an L2 writeback on gfx950's per-XCD L2s) in every workgroup.
+__global__ __launch_bounds__(64) void k_adam_steps(AdamArgs a) {
+  if (threadIdx.x < (unsigned)a.nseg) *a.seg[threadIdx.x].step += 1.f;
+}
+
+// ------------------------------------------------------------------------------------------
+// sparse gradient exchange (ray-sharded mapping)
+// ------------------------------------------------------------------------------------------
+// Only the frustum-selected rows of a grid gradient reach Adam (Mapper.py:314-333,394-401), so
+// only they are summed across ranks: pack them (+ the dense decoder gradients) into one buffer,
+// all-reduce it, unpack.  One float4 (rows) or float (tail) per thread; pure HBM copy.
+template <bool PACK>
+__global__ __launch_bounds__(256) void k_rows_xfer(float* __restrict__ grid, const int32_t* __restrict__ rows,
+                                                   int64_t n_rows, int q, float* __restrict__ tail, int64_t n_tail,
+                                                   float* __restrict__ buf) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t nv = n_rows * q;
+  if (e < nv) {
+    const int64_t ri = e / q, part = e - ri * q;
+    f32x4* gp = reinterpret_cast<f32x4*>(grid + ((int64_t)rows[ri] * q + part) * 4);
+    f32x4* bp = reinterpret_cast<f32x4*>(buf + e * 4);
+    if (PACK)
+      *bp = *gp;
+    else
+      *gp = *bp;
+  } else if (e - nv < n_tail) {
+    const int64_t t = e - nv;
+    if (PACK)
+      buf[nv * 4 + t] = tail[t];
+    else
+      tail[t] = buf[nv * 4 + t];
   }
 }
 
+int rows_xfer(bool pack, float* grid, const int32_t* rows, int64_t n_rows, int32_t row_len, float* tail,
+              int64_t n_tail, float* buf, void* stream) {
+  if (n_rows < 0 || n_tail < 0 || row_len <= 0 || row_len % 4) return NSLAM_EINVAL;
+  if ((n_rows > 0 && (!grid || !rows)) || (n_tail > 0 && !tail) || (n_rows + n_tail > 0 && !buf)) return NSLAM_EINVAL;
+  if (n_rows > 0 && ((((uintptr_t)grid) | ((uintptr_t)buf)) & 15)) return NSLAM_EINVAL;
+  const int64_t work = n_rows * (row_len / 4) + n_tail;
+  if (work == 0) return NSLAM_OK;
+  if ((work + 255) / 256 >= (int64_t(1) << 31)) return NSLAM_EUNSUPPORTED;
+  const dim3 g((unsigned)((work + 255) / 256));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (pack)
+    hipLaunchKernelGGL(k_rows_xfer<true>, g, dim3(256), 0, s, grid, rows, n_rows, row_len / 4, tail, n_tail, buf);
+  else
+    hipLaunchKernelGGL(k_rows_xfer<false>, g, dim3(256), 0, s, grid, rows, n_rows, row_len / 4, tail, n_tail, buf);
+  return hip_status();
+}
+
 }  // namespace
+
+extern "C" int nslam_rows_pack(const float* grid, const int32_t* rows, int64_t n_rows, int32_t row_len,
+                               const float* tail, int64_t n_tail, float* out, void* stream) {
+  return rows_xfer(true, const_cast<float*>(grid), rows, n_rows, row_len, const_cast<float*>(tail), n_tail, out,
+                   stream);
+}
+
+extern "C" int nslam_rows_unpack(const float* in, const int32_t* rows, int64_t n_rows, int32_t row_len, float* grid,
+                                 float* tail, int64_t n_tail, void* stream) {
+  return rows_xfer(false, grid, rows, n_rows, row_len, tail, n_tail, const_cast<float*>(in), stream);
+}
 
 extern "C" int nslam_gather_rays(const nslam_frame* frames, int32_t n_frames, int64_t n_per, const int64_t* pix,
                                  int32_t H, int32_t W, int32_t h0, int32_t h1, int32_t w0, int32_t w1, float fx,
@@ -226,7 +278,7 @@ extern "C" int nslam_gather_rays(const nslam_frame* frames, int32_t n_frames, in
 
 extern "C" int nslam_adam_step(const nslam_adam_seg* segs, int32_t n_segs, float beta1, float beta2, float eps,
                                int32_t zero_grad, uint32_t* ticket, void* stream) {
-  if (!segs || n_segs <= 0 || n_segs > NSLAM_ADAM_MAX_SEGS || !ticket) return NSLAM_EINVAL;
+  if (!segs || n_segs <= 0 || n_segs > NSLAM_ADAM_MAX_SEGS) return NSLAM_EINVAL;
   AdamArgs a{};
   int64_t blocks = 0;
   for (int s = 0; s < n_segs; ++s) {
@@ -250,10 +302,11 @@ extern "C" int nslam_adam_step(const nslam_adam_seg* segs, int32_t n_segs, float
   a.b2 = beta2;
   a.eps = eps;
   a.zero_grad = zero_grad;
-  a.ticket = ticket;
+  (void)ticket;
   if (blocks == 0) return NSLAM_EINVAL;  // every segment empty: nothing would advance the steps
   if (blocks >= (int64_t(1) << 31)) return NSLAM_EUNSUPPORTED;
-  hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(kAdamThreads), 0, reinterpret_cast<hipStream_t>(stream),
-                     a);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(kAdamThreads), 0, s, a);
+  hipLaunchKernelGGL(k_adam_steps, dim3(1), dim3(64), 0, s, a);
   return hip_status();
 }

@@ -987,29 +987,39 @@ __global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd(QueryKArgs a, flo
     dec_bwd_tile<DEC, WG, PG, FIRST, SAVED>(a, tile, A, S, lane);
 }
 
-// base[j] += sum_b slab[b][j].  A workgroup owns 256 parameters (float4 per lane); each of its 16
-// waves sums every 16th slab and the 16 partials are combined in LDS in a fixed order:
-// deterministic, with 16x the memory-level parallelism of a one-thread-per-parameter loop.
-__global__ __launch_bounds__(1024) void k_slab_reduce(const float* __restrict__ slab, int64_t nslab, int acc_floats,
-                                                      int count, float* __restrict__ base) {
-  __shared__ f32x4 part[16][64];
-  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int j = (blockIdx.x * 64 + c) * 4;
-  f32x4 s = {0.f, 0.f, 0.f, 0.f};
-  if (j < count)
-    for (int64_t b = g; b < nslab; b += 16) s += *reinterpret_cast<const f32x4*>(slab + b * acc_floats + j);
-  part[g][c] = s;
+// base[j] += sum_b slab[b][j].  A workgroup owns 64 parameters; lane (r, c) of a wave reads the
+// float4 c of slab r of every 64th slab group, so the 16 waves x 4 lane rows keep 64 slab streams
+// in flight per workgroup (~count/64 workgroups fill the chip; a wave load is 4 x 256-B
+// segments).  The 64 partials are combined in LDS in a fixed order: deterministic.
+constexpr int kReduceWaves = 16;
+__global__ __launch_bounds__(64 * kReduceWaves) void k_slab_reduce(const float* __restrict__ slab, int64_t nslab,
+                                                                   int acc_floats, int count,
+                                                                   float* __restrict__ base) {
+  __shared__ f32x4 part[kReduceWaves * 4][16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = lane & 15, r = wave * 4 + (lane >> 4);  // r: slab stream 0..63
+  const int j = (blockIdx.x * 16 + c) * 4;
+  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
+  if (j < count) {
+    const float* p = slab + j;
+    int64_t b = r;
+    for (; b + 64 < nslab; b += 128) {
+      s0 += *reinterpret_cast<const f32x4*>(p + b * acc_floats);
+      s1 += *reinterpret_cast<const f32x4*>(p + (b + 64) * acc_floats);
+    }
+    if (b < nslab) s0 += *reinterpret_cast<const f32x4*>(p + b * acc_floats);
+  }
+  part[r][c] = s0 + s1;
   __syncthreads();
-  if (g == 0 && j < count) {
+  if (threadIdx.x < 16 && j < count) {
     f32x4 t = part[0][c];
-#pragma unroll
-    for (int k = 1; k < 16; ++k) t += part[k][c];
+#pragma unroll 8
+    for (int k = 1; k < kReduceWaves * 4; ++k) t += part[k][c];
 #pragma unroll
     for (int e = 0; e < 4; ++e)
       if (j + e < count) base[j + e] += t[e];
   }
 }
-
 
 bool grid_ok(const nslam_grid& g) {
   return g.data && g.dims[0] > 0 && g.dims[1] > 0 && g.dims[2] > 0 && (((uintptr_t)g.data) & 15) == 0;
@@ -1110,8 +1120,8 @@ int launch_dec_bwd(const QueryKArgs& a, bool first, float* slab, hipStream_t s) 
                : launch_one<DEC, 2, PG, false>(a, slab, acc, blocks, s);
   }
   if (rc) return rc;
-  hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((dg.count + 255) / 256)), dim3(1024), 0, s, slab, nslab, acc,
-                     (int)dg.count, dg.base);
+  hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((dg.count + 63) / 64)), dim3(64 * kReduceWaves), 0, s, slab,
+                     nslab, acc, (int)dg.count, dg.base);
   return hip_status();
 }
 

@@ -65,5 +65,64 @@ def allreduce_tensors(grads, group=None, bucket_bytes: int = 64 << 20):
     flush()
 
 
+class SparseGradExchange:
+    """Frustum-compacted gradient all-reduce for the fused mapping engine (ray sharding).
+
+    Adam only reads the frustum-selected rows of each grid gradient (Mapper.py:314-333,394-401,504;
+    room0: ~5 % of the fine/colour grids), so the payload of the per-iteration exchange is those
+    rows plus the dense decoder gradients: ~2.4 MiB instead of the 46 MiB dense room0 grids.
+    nslam_rows_pack gathers them from the engine's flat grid-gradient buffer into one contiguous
+    buffer, ONE all_reduce(SUM) sums it over ranks (RCCL over xGMI; capturable in a hipGraph), and
+    nslam_rows_unpack writes it back.  Rows outside the frustum keep this rank's partial sums:
+    Adam never reads them (the reference discards them at Mapper.py:511-519).
+
+    rows: {grid key: int32 row indices} (the FusedAdam group "rows"); pack/unpack default to the
+    HIP entry points (ops.rows_pack / ops.rows_unpack) and are injectable for CPU tests.
+    """
+
+    def __init__(self, engine, rows, group=None, pack=None, unpack=None):
+        from . import ops
+        self.engine, self.group = engine, group
+        self.pack = pack or ops.rows_pack
+        self.unpack = unpack or ops.rows_unpack
+        offs, off = {}, 0
+        for k, v in engine.c.items():  # flat buffer order = engine.ggrad order
+            offs[k] = off
+            off += v.numel() // 32
+        self.rows = {k: (r.to(torch.int64) + offs[k]).to(torch.int32) for k, r in rows.items()}
+        self._plan = {}
+
+    def plan(self, keys, dnames):
+        """(flat row list, [(decoder grad, offset)], payload buffer) for the grids in `keys` and
+        the decoders `dnames` (cached per stage)."""
+        k = (tuple(keys), tuple(dnames))
+        if k not in self._plan:
+            rl = [self.rows[g] for g in keys if g in self.rows]
+            dev = self.engine.gbuf.device
+            rows = torch.cat(rl) if rl else torch.zeros(0, dtype=torch.int32, device=dev)
+            tails, off = [], rows.numel() * 32
+            for n in dnames:
+                g = self.engine.decs[n].grad
+                tails.append((g, off))
+                off += g.numel()
+            self._plan[k] = (rows, tails, torch.empty(off, dtype=torch.float32, device=dev))
+        return self._plan[k]
+
+    def payload_bytes(self, keys, dnames):
+        return self.plan(keys, dnames)[2].numel() * 4
+
+    def __call__(self, keys, dnames):
+        rows, tails, buf = self.plan(keys, dnames)
+        gbuf = self.engine.gbuf
+        self.pack(gbuf, rows, None, buf)
+        for g, off in tails:
+            self.pack(None, None, g, buf[off:off + g.numel()])
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1:
+            dist.all_reduce(buf, group=self.group)
+        self.unpack(buf, rows, gbuf, None)
+        for g, off in tails:
+            self.unpack(buf[off:off + g.numel()], None, None, g)
+
+
 def optimizer_params(opt):
     return [p for grp in opt.param_groups for p in grp["params"]]

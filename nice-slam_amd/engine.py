@@ -162,13 +162,15 @@ class MappingEngine:
         return g
 
     def iteration(self, stage, frames, pix, n_per, hw, intrinsics, optimizer, trainable_decoders=("color",),
-                  gt_max=None, allreduce=None, use_gt_in_sampler=True):
+                  gt_max=None, allreduce=None, use_gt_in_sampler=True, exchange=None):
         """One mapping iteration; returns (ray_loss f64 [N], keep uint8 [N]) as device tensors.
 
         frames: [(depth, color, c2w)] of the window; pix: int64 [len(frames)*n_per] randint
         indices over the full image; hw = (H, W); intrinsics = (fx, fy, cx, cy).
         gt_max: callable(gt_depth) → device scalar for a ray-sharded job (all-reduced max);
-        allreduce: callable(list of grads) run before Adam (ray sharding).
+        allreduce: callable(list of grads) run before Adam (ray sharding, dense);
+        exchange: callable(grid keys, decoder names) run before Adam instead — the frustum-compacted
+        exchange (distributed.SparseGradExchange).
         """
         H, W = hw
         fx, fy, cx, cy = intrinsics
@@ -185,7 +187,9 @@ class MappingEngine:
             self.decs[n].grad.zero_()
         self.query_bwd(stage, ro, rd, z, g_raw, keys, dnames)
         grads = self.adam_grads(stage, trainable_decoders)
-        if allreduce is not None:  # the grid gradients as one flat buffer, plus the decoder gradients
+        if exchange is not None:  # frustum-compacted all-reduce (distributed.SparseGradExchange)
+            exchange(keys, dnames)
+        elif allreduce is not None:  # the grid gradients as one flat buffer, plus the decoder gradients
             allreduce([self.gbuf] + [self.decs[n].grad for n in dnames])
         optimizer.step(grads=grads)
         for n in dnames:

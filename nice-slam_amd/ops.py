@@ -340,6 +340,28 @@ class _GridSample(torch.autograd.Function):
         return gg, gc
 
 
+def grid_sample_fwd(grid, coords, out):
+    """nslam_grid_sample_fwd without autograd: out [M,32] = trilinear features of the normalised
+    coords [M,3] in a channels-last grid (bench / bulk-query form; grid_sample() is the
+    differentiable drop-in)."""
+    if not grid.is_contiguous(memory_format=torch.channels_last_3d):
+        raise ValueError("grid must be channels-last")
+    dims = (ctypes.c_int32 * 3)(grid.shape[2], grid.shape[3], grid.shape[4])
+    with _span("grid_fwd"):
+        rc = lib().nslam_grid_sample_fwd(ptr(grid), dims, ptr(coords), coords.shape[0], ptr(out),
+                                         stream_ptr(coords.device))
+    check(rc, "nslam_grid_sample_fwd")
+
+
+def grid_sample_bwd(grid, coords, gout, ggrid, gcoords=None):
+    """nslam_grid_sample_bwd without autograd: ggrid += scatter of gout (atomics); gcoords = d/dcoords."""
+    dims = (ctypes.c_int32 * 3)(grid.shape[2], grid.shape[3], grid.shape[4])
+    with _span("grid_bwd"):
+        rc = lib().nslam_grid_sample_bwd(ptr(grid), dims, ptr(coords), coords.shape[0], ptr(gout), ptr(ggrid),
+                                         ptr(gcoords), stream_ptr(coords.device))
+    check(rc, "nslam_grid_sample_bwd")
+
+
 def grid_sample(grid, coords):
     """[M,32] trilinear features of normalised coords [M,3] (x,y,z) — F.grid_sample semantics."""
     return _GridSample.apply(grid, coords)
@@ -424,6 +446,26 @@ def render_loss(raw, z, gt_depth, gt_color, keep=None, mode="mapper", use_color=
     return depth, var, color, ray_loss, g_raw
 
 
+def rows_pack(grid_flat, rows, tail, out):
+    """nslam_rows_pack: out = [grid_flat.view(-1, 32)[rows], tail] (either part may be None)."""
+    n = rows.numel() if rows is not None else 0
+    nt = tail.numel() if tail is not None else 0
+    with _span("rows_xfer"):
+        rc = lib().nslam_rows_pack(ptr(grid_flat) if n else None, ptr(rows) if n else None, n, 32, ptr(tail), nt,
+                                   ptr(out), stream_ptr(out.device))
+    check(rc, "nslam_rows_pack")
+
+
+def rows_unpack(buf, rows, grid_flat, tail):
+    """nslam_rows_unpack: the inverse of rows_pack."""
+    n = rows.numel() if rows is not None else 0
+    nt = tail.numel() if tail is not None else 0
+    with _span("rows_xfer"):
+        rc = lib().nslam_rows_unpack(ptr(buf), ptr(rows) if n else None, n, 32, ptr(grid_flat) if n else None,
+                                     ptr(tail), nt, stream_ptr(buf.device))
+    check(rc, "nslam_rows_unpack")
+
+
 class FusedAdam:
     """torch.optim.Adam (betas, eps; no weight decay / amsgrad) stepping every parameter segment
     in one HIP launch (nslam_adam_step).  Construction mirrors torch:
@@ -499,7 +541,7 @@ class FusedAdam:
         arr = (_lib.NslamAdamSeg * len(segs))(*[s for s, _, _ in segs])
         b1, b2 = self.betas
         with _span("adam"):
-            rc = lib().nslam_adam_step(arr, len(segs), b1, b2, self.eps, int(bool(zero_grad)), ptr(self.ticket),
+            rc = lib().nslam_adam_step(arr, len(segs), b1, b2, self.eps, int(bool(zero_grad)), None,
                                        stream_ptr(self.device))
         check(rc, "nslam_adam_step")
 

@@ -10,7 +10,9 @@ NICE-SLAM's volumetric-rendering hot path. It is the CHECKER for the HIP path:
     ``tests/test_oracle_golden.py``.
 
 Every function cites the reference file:line it restates (paths relative to the reference repo).
-Torch is used here purely as a numeric library on CPU (autograd gives the VJPs the tests compare).
+Torch is used here purely as a numeric library (autograd gives the VJPs the tests compare). It runs
+on CPU as the checker; bench.py's baseline leg also runs it on the device, as the stand-in for the
+reference's own PyTorch-on-GPU path (the same torch ops the reference issues).
 """
 from __future__ import annotations
 
@@ -100,7 +102,7 @@ def mlp_no_xyz(sd, pre, feat):
 def nice_raw(sd, p64, grids, stage, bound, coarse_bound=None):
     """NICE.forward stage combiner, src/conv_onet/models/decoder.py:312-342 → raw [P,4] f32."""
     P = p64.shape[0]
-    zeros = torch.zeros(P, 3, dtype=torch.float32)
+    zeros = torch.zeros(P, 3, dtype=torch.float32, device=p64.device)
     if stage == "coarse":
         cb = coarse_bound if coarse_bound is not None else bound * 2
         occ = mlp_no_xyz(sd, "coarse_decoder.", grid_features(p64, grids["grid_coarse"], cb))[:, 0]
@@ -142,7 +144,8 @@ def sample_z(rays_o, rays_d, gt_depth, bound, n_strat, n_surf, lindisp=False, gt
     gt_max: max(gt_depth) of the FULL batch when this call sees only a shard of it."""
     with torch.no_grad():
         far_bb = far_bound(rays_o, rays_d, bound)[:, None] + 0.01
-        t_s = torch.linspace(0.0, 1.0, n_strat)
+        dev = rays_o.device
+        t_s = torch.linspace(0.0, 1.0, n_strat, device=dev)
         if gt_depth is None:
             n_surf = 0
             near = 0.01
@@ -157,9 +160,9 @@ def sample_z(rays_o, rays_d, gt_depth, bound, n_strat, n_surf, lindisp=False, gt
         else:
             z = near * (1.0 - t_s) + far * t_s
         if n_surf > 0:
-            t_u = torch.linspace(0.0, 1.0, n_surf).double()
+            t_u = torch.linspace(0.0, 1.0, n_surf, device=dev).double()
             pos = (gt > 0)[:, 0]
-            zs = torch.zeros(gt.shape[0], n_surf, dtype=torch.float64)
+            zs = torch.zeros(gt.shape[0], n_surf, dtype=torch.float64, device=dev)
             g = gt[pos]
             zs[pos] = (0.95 * g) * (1.0 - t_u) + (1.05 * g) * t_u
             zs[~pos] = 0.001 * (1.0 - t_u) + gmax * t_u

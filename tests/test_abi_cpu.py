@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_strerror(pkg):
     L = pkg._lib.lib()
-    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 4
+    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 5
     assert L.nslam_strerror(0) == b"ok"
     assert b"invalid" in L.nslam_strerror(-1)
 
@@ -56,6 +56,10 @@ def test_argument_validation_without_gpu(pkg):
     assert L.nslam_grid_sample_fwd(None, dims, None, 5, None, None) == -1
     lo = (ctypes.c_double * 3)(0, 0, 0)
     assert L.nslam_sample_rays(None, None, None, None, 3, lo, lo, None, 500, None, 0, 0, None, None, 0, None) == -2
+    assert L.nslam_rows_pack(None, None, 4, 30, None, 0, None, None) == -1      # row_len % 4
+    assert L.nslam_rows_pack(None, None, 4, 32, None, 0, None, None) == -1      # NULL grid/rows
+    assert L.nslam_rows_unpack(None, None, 0, 32, None, None, 5, None) == -1    # NULL tail
+    assert L.nslam_rows_pack(None, None, 0, 32, None, 0, None, None) == 0       # empty: no launch
 
 
 def test_no_cpu_fallback(pkg):

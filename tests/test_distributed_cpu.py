@@ -95,3 +95,75 @@ def test_shard_range_covers_everything():
             assert rs[0][0] == 0 and rs[-1][1] == n
             assert all(rs[i][1] == rs[i + 1][0] for i in range(w - 1))
             assert max(e - s for s, e in rs) - min(e - s for s, e in rs) <= 1
+
+
+# ---- frustum-compacted gradient exchange (distributed.SparseGradExchange) ---------------------
+
+def _torch_rows_pack(grid_flat, rows, tail, out):
+    """CPU restatement of nslam_rows_pack (include/nslam.h) for the host-logic test."""
+    n = rows.numel() if rows is not None else 0
+    if n:
+        out[:n * 32].copy_(grid_flat.view(-1, 32)[rows.long()].reshape(-1))
+    if tail is not None:
+        out[n * 32:n * 32 + tail.numel()].copy_(tail)
+
+
+def _torch_rows_unpack(buf, rows, grid_flat, tail):
+    n = rows.numel() if rows is not None else 0
+    if n:
+        grid_flat.view(-1, 32)[rows.long()] = buf[:n * 32].view(-1, 32)
+    if tail is not None:
+        tail.copy_(buf[n * 32:n * 32 + tail.numel()])
+
+
+class _FakeEngine:
+    """The engine attributes SparseGradExchange reads: grids `c`, flat `gbuf`, decoder grads."""
+
+    def __init__(self, shapes, n_dec, rank):
+        from types import SimpleNamespace
+        g = torch.Generator().manual_seed(100 + rank)
+        self.c = {k: torch.zeros(1, 32, *s).contiguous(memory_format=torch.channels_last_3d) for k, s in shapes.items()}
+        self.gbuf = torch.randn(sum(v.numel() for v in self.c.values()), generator=g)
+        self.decs = {"color": SimpleNamespace(grad=torch.randn(n_dec, generator=g))}
+
+
+def _exchange_worker(rank, world, port, out_path):
+    import sys
+    sys.path.insert(0, REPO)
+    import importlib
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    D = importlib.import_module("nice-slam_amd").distributed
+    shapes = {"grid_middle": (3, 4, 5), "grid_fine": (5, 6, 7), "grid_color": (5, 6, 7)}
+    rows = {"grid_middle": torch.tensor([0, 7, 59], dtype=torch.int32),
+            "grid_fine": torch.tensor([1, 2, 3, 100, 209], dtype=torch.int32),
+            "grid_color": torch.tensor([5, 150], dtype=torch.int32)}
+    eng = _FakeEngine(shapes, 37, rank)
+    before_g, before_d = eng.gbuf.clone(), eng.decs["color"].grad.clone()
+    ex = D.SparseGradExchange(eng, rows, pack=_torch_rows_pack, unpack=_torch_rows_unpack)
+    keys = ("grid_middle", "grid_fine", "grid_color")
+    ex(keys, ("color",))
+    torch.save({"before_g": before_g, "before_d": before_d, "after_g": eng.gbuf, "after_d": eng.decs["color"].grad,
+                "bytes": ex.payload_bytes(keys, ("color",))}, f"{out_path}.{rank}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sparse_exchange_sums_frustum_rows_only(tmp_path):
+    out = str(tmp_path / "ex")
+    mp.spawn(_exchange_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    r = [torch.load(f"{out}.{k}") for k in range(2)]
+    off = {"grid_middle": 0, "grid_fine": 60, "grid_color": 270}   # rows of 32 floats
+    sel = {"grid_middle": [0, 7, 59], "grid_fine": [1, 2, 3, 100, 209], "grid_color": [5, 150]}
+    flat_rows = sorted(off[k] + i for k in sel for i in sel[k])
+    assert r[0]["bytes"] == (len(flat_rows) * 32 + 37) * 4
+    total_g = r[0]["before_g"].view(-1, 32) + r[1]["before_g"].view(-1, 32)
+    for k in range(2):
+        after = r[k]["after_g"].view(-1, 32)
+        before = r[k]["before_g"].view(-1, 32)
+        m = torch.zeros(after.shape[0], dtype=torch.bool)
+        m[flat_rows] = True
+        assert torch.equal(after[m], total_g[m])          # frustum rows: summed over ranks
+        assert torch.equal(after[~m], before[~m])         # other rows: untouched
+        assert torch.equal(r[k]["after_d"], r[0]["before_d"] + r[1]["before_d"])

@@ -230,3 +230,48 @@ def test_engine_loss_decreases(tiny):
         rl, _ = eng.iteration("color", frames, pix, 200, (96, 128), (sc.fx, sc.fy, sc.cx, sc.cy), opt)
         losses.append(float(rl.sum()))
     assert losses[-1] < losses[0]
+
+
+def test_rows_pack_unpack_bitexact():
+    """nslam_rows_pack / nslam_rows_unpack (the sparse gradient exchange) vs torch indexing."""
+    g = torch.Generator(device=DEV).manual_seed(9)
+    grid = torch.randn(5000 * 32, device=DEV, generator=g)
+    rows = torch.randperm(5000, device=DEV, generator=g)[:1234].to(torch.int32)
+    tail = torch.randn(1001, device=DEV, generator=g)
+    buf = torch.full((1234 * 32 + 1001 + 3,), float("nan"), device=DEV)
+    P.ops.rows_pack(grid, rows, None, buf)
+    P.ops.rows_pack(None, None, tail, buf[1234 * 32:1234 * 32 + 1001])
+    torch.cuda.synchronize()
+    assert torch.equal(buf[:1234 * 32].view(-1, 32), grid.view(-1, 32)[rows.long()])
+    assert torch.equal(buf[1234 * 32:1234 * 32 + 1001], tail)
+    buf2 = torch.randn(buf.shape, device=DEV, generator=g)
+    grid2, tail2 = grid.clone(), tail.clone()
+    P.ops.rows_unpack(buf2, rows, grid2, None)
+    P.ops.rows_unpack(buf2[1234 * 32:1234 * 32 + 1001], None, None, tail2)
+    torch.cuda.synchronize()
+    ref = grid.clone().view(-1, 32)
+    ref[rows.long()] = buf2[:1234 * 32].view(-1, 32)
+    assert torch.equal(grid2.view(-1, 32), ref)
+    assert torch.equal(tail2, buf2[1234 * 32:1234 * 32 + 1001])
+
+
+def test_sparse_exchange_single_rank_is_identity(tiny):
+    """world size 1 (no process group): the frustum-compacted exchange (pack → [no collective] →
+    unpack) leaves an engine iteration's gradients bit-identical."""
+    sc, frames = _frames(tiny)
+    pix = torch.randint(96 * 128, (3 * 100,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(6))
+    nice, c = _nice(sc)
+    eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV)
+    opt = P.ops.FusedAdam([{"params": [eng.decs["color"].param], "lr": 0.0}] +
+                          [{"params": [c[k]], "lr": 0.0} for k in ("grid_middle", "grid_fine", "grid_color")])
+    eng.iteration("color", frames, pix, 100, (96, 128), (sc.fx, sc.fy, sc.cx, sc.cy), opt)
+    rows = {k: torch.arange(0, c[k].shape[2:].numel(), 3, device=DEV, dtype=torch.int32)
+            for k in ("grid_middle", "grid_fine", "grid_color")}
+    ex = P.distributed.SparseGradExchange(eng, rows)
+    keys, dn = eng.grads_for("color", ("color",))
+    g0, d0 = eng.gbuf.clone(), eng.decs["color"].grad.clone()
+    assert float(g0.abs().sum()) > 0 and float(d0.abs().sum()) > 0
+    ex(keys, dn)
+    torch.cuda.synchronize()
+    assert torch.equal(eng.gbuf, g0) and torch.equal(eng.decs["color"].grad, d0)
+    assert ex.payload_bytes(keys, dn) == (sum(r.numel() for r in rows.values()) * 32 + d0.numel()) * 4
