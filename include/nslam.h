@@ -114,6 +114,13 @@ int nslam_sample_rays(const float* rays_o, const float* rays_d, const float* gt_
 /* ---- fused point query ------------------------------------------------------------------------
  * raw[M][4] float32 for pts[M][3] float64 (Renderer.eval_points incl. `ret[~mask,3]=100`). */
 int nslam_query_fwd(const nslam_query_cfg* cfg, const double* pts, int64_t n_pts, float* raw, void* stream);
+/* The same result with the decoders evaluated by separate workgroups (ABI v5): fine and colour
+ * stages launch 2-3x the waves of nslam_query_fwd (latency hiding at mapping batch sizes) and
+ * combine fine + middle occupancy afterwards.  ws: nslam_query_fwd_workspace_size(cfg, M) bytes
+ * (0 for the coarse and middle stages, which fall through to nslam_query_fwd). */
+int nslam_query_fwd_ws(const nslam_query_cfg* cfg, const double* pts, int64_t n_pts, float* raw, void* ws,
+                       size_t ws_bytes, void* stream);
+size_t nslam_query_fwd_workspace_size(const nslam_query_cfg* cfg, int64_t n_pts);
 
 /* Backward of nslam_query_fwd for cotangent g_raw[M][4]: accumulates grid gradients into
  * cfg->grid[i].grad (atomics, caller zero-initialises), adds parameter gradients into

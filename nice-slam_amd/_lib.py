@@ -98,6 +98,7 @@ EXPORTS = (
     "nslam_composite_fwd", "nslam_composite_bwd", "nslam_grid_sample_fwd", "nslam_grid_sample_bwd",
     "nslam_workspace_size", "nslam_strerror", "nslam_abi_version", "nslam_gather_rays", "nslam_render_loss",
     "nslam_render_loss_workspace_size", "nslam_adam_step", "nslam_rows_pack", "nslam_rows_unpack",
+    "nslam_query_fwd_ws", "nslam_query_fwd_workspace_size",
 )
 
 _lib = None
@@ -116,6 +117,9 @@ def lib():
         L.nslam_pack_layout.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int32), ctypes.c_int]
         L.nslam_sample_rays.argtypes = [vp, vp, vp, vp, i64, dp, dp, vp, i32, vp, i32, i32, vp, vp, sz, vp]
         L.nslam_query_fwd.argtypes = [ctypes.POINTER(NslamQueryCfg), vp, i64, vp, vp]
+        L.nslam_query_fwd_ws.argtypes = [ctypes.POINTER(NslamQueryCfg), vp, i64, vp, vp, sz, vp]
+        L.nslam_query_fwd_workspace_size.argtypes = [ctypes.POINTER(NslamQueryCfg), i64]
+        L.nslam_query_fwd_workspace_size.restype = sz
         L.nslam_query_bwd.argtypes = [ctypes.POINTER(NslamQueryCfg), vp, i64, vp, vp, vp, sz, vp]
         L.nslam_query_bwd_workspace_size.argtypes = [ctypes.POINTER(NslamQueryCfg), i64]
         L.nslam_query_bwd_workspace_size.restype = sz

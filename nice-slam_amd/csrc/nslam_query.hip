@@ -855,6 +855,78 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd(QueryKArgs a) {
   }
 }
 
+// Decoder-parallel forward (fine and colour stages): each workgroup evaluates ONE decoder for its
+// 4 tiles, so a launch has 2-3x the waves of k_query_fwd (room0 mapping: 4500 instead of 1500 on
+// 1024 SIMDs) and every wave a third of the serial MFMA/gather chain.  Parts are interleaved
+// over blockIdx (heavy fine and light middle/colour workgroups mix on every CU):
+//   part 0  middle: occ_mid[p] = inside ? middle_occ : 100
+//   part 1  fine:   raw[p][3]  = inside ? fine_occ : 0     (fine stage: the whole row)
+//   part 2  colour: raw[p][0..2]
+// and k_occ_combine then forms raw[p][3] = fine_occ + middle_occ (decoder.py:331-334, the
+// reference's operand order) — exactly 100 outside the bound (0 + 100; Renderer.py:57).
+template <int STAGE>
+__global__ __launch_bounds__(256, 2) void k_query_fwd_parts(QueryKArgs a, float* __restrict__ occ_mid) {
+  constexpr int NPARTS = STAGE == NSLAM_STAGE_COLOR ? 3 : 2;
+  const int part = (int)(blockIdx.x % NPARTS);
+  const int lane = threadIdx.x & 63;
+  const int64_t tile = (int64_t)(blockIdx.x / NPARTS) * 4 + (threadIdx.x >> 6);
+  if (tile * 32 >= a.n) return;  // wave-uniform
+  const int h = lane >> 5;
+  const int64_t idx = tile * 32 + (lane & 31);
+  const Pt q = load_point(a, idx);
+  uint32_t m[5];
+  Corners cr;
+  grid_corners(cr, a.c.grid[NSLAM_DEC_MIDDLE], q);
+  const f32x16 cm = gather_tile(a.c.grid[NSLAM_DEC_MIDDLE].data, cr, lane);
+  if (part == 0) {
+    const float* pk = a.c.packed[NSLAM_DEC_MIDDLE];
+    const XyzPack L{1};
+    const f32x16 cms[1] = {cm};
+    const f32x16 h4 = xyz_forward<1, false>(pk, cms, q.x, lane, m, nullptr);
+    save_masks(a, NSLAM_DEC_MIDDLE, tile, m, lane);
+    float o = out_row(pk + L.Wo(), pk + L.Bo(), 0, h4, lane);
+    if (!q.inside) o = 100.f;
+    if (h == 0 && q.valid) occ_mid[idx] = o;
+  } else if (part == 1) {
+    grid_corners(cr, a.c.grid[NSLAM_DEC_FINE], q);
+    const f32x16 cf[2] = {gather_tile(a.c.grid[NSLAM_DEC_FINE].data, cr, lane), cm};
+    const float* pk = a.c.packed[NSLAM_DEC_FINE];
+    const XyzPack L{2};
+    const f32x16 h4 = xyz_forward<2, false>(pk, cf, q.x, lane, m, nullptr);
+    save_masks(a, NSLAM_DEC_FINE, tile, m, lane);
+    float o = out_row(pk + L.Wo(), pk + L.Bo(), 0, h4, lane);
+    if (!q.inside) o = 0.f;
+    if (h == 0 && q.valid) {
+      if (STAGE == NSLAM_STAGE_COLOR) {
+        a.raw[idx * 4 + 3] = o;
+      } else {
+        f32x4 v = {0.f, 0.f, 0.f, o};
+        *reinterpret_cast<f32x4*>(a.raw + idx * 4) = v;
+      }
+    }
+  } else if (STAGE == NSLAM_STAGE_COLOR) {
+    grid_corners(cr, a.c.grid[NSLAM_DEC_COLOR], q);
+    const f32x16 cc[1] = {gather_tile(a.c.grid[NSLAM_DEC_COLOR].data, cr, lane)};
+    const float* pk = a.c.packed[NSLAM_DEC_COLOR];
+    const XyzPack L{1};
+    const f32x16 h4 = xyz_forward<1, false>(pk, cc, q.x, lane, m, nullptr);
+    save_masks(a, NSLAM_DEC_COLOR, tile, m, lane);
+    float o[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) o[j] = out_row(pk + L.Wo(), pk + L.Bo(), j, h4, lane);
+    if (h == 0 && q.valid) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) a.raw[idx * 4 + j] = o[j];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_occ_combine(float* __restrict__ raw, const float* __restrict__ occ_mid,
+                                                     int64_t n) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p < n) raw[p * 4 + 3] = raw[p * 4 + 3] + occ_mid[p];
+}
+
 // One backward launch per decoder: the decoder's forward is recomputed, its grid gradient is
 // scattered, its parameter gradients are accumulated and its share of d/dpts is added into g_pts
 // (launches on one stream are ordered and each point is owned by one lane pair: plain
@@ -1066,6 +1138,32 @@ extern "C" int nslam_query_fwd(const nslam_query_cfg* cfg, const double* pts, in
     case NSLAM_STAGE_FINE: hipLaunchKernelGGL(k_query_fwd<NSLAM_STAGE_FINE>, grid, block, 0, s, a); break;
     default: hipLaunchKernelGGL(k_query_fwd<NSLAM_STAGE_COLOR>, grid, block, 0, s, a); break;
   }
+  return hip_status();
+}
+
+extern "C" size_t nslam_query_fwd_workspace_size(const nslam_query_cfg* cfg, int64_t n_pts) {
+  if (!cfg || n_pts <= 0 || cfg->stage < NSLAM_STAGE_FINE || cfg->stage > NSLAM_STAGE_COLOR) return 0;
+  return ((size_t)n_pts * sizeof(float) + 255) & ~(size_t)255;
+}
+
+extern "C" int nslam_query_fwd_ws(const nslam_query_cfg* cfg, const double* pts, int64_t n_pts, float* raw, void* ws,
+                                  size_t ws_bytes, void* stream) {
+  const size_t need = nslam_query_fwd_workspace_size(cfg, n_pts);
+  if (need == 0) return nslam_query_fwd(cfg, pts, n_pts, raw, stream);  // coarse / middle: one decoder
+  const int rc = check_cfg(cfg, false);
+  if (rc) return rc;
+  if (!ws || ws_bytes < need) return NSLAM_EWORKSPACE;
+  if ((!pts && !cfg->rays_o) || !raw || (((uintptr_t)raw) & 15)) return NSLAM_EINVAL;
+  if (cfg->rays_o && (n_pts >= (int64_t(1) << 31) || n_pts % cfg->n_samples)) return NSLAM_EINVAL;
+  QueryKArgs a{*cfg, pts, n_pts, raw, nullptr, nullptr};
+  const int64_t groups = ((n_pts + 31) / 32 + 3) / 4;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  float* occ = reinterpret_cast<float*>(ws);
+  if (cfg->stage == NSLAM_STAGE_FINE)
+    hipLaunchKernelGGL(k_query_fwd_parts<NSLAM_STAGE_FINE>, dim3((unsigned)(groups * 2)), dim3(256), 0, s, a, occ);
+  else
+    hipLaunchKernelGGL(k_query_fwd_parts<NSLAM_STAGE_COLOR>, dim3((unsigned)(groups * 3)), dim3(256), 0, s, a, occ);
+  hipLaunchKernelGGL(k_occ_combine, dim3((unsigned)((n_pts + 255) / 256)), dim3(256), 0, s, raw, occ, n_pts);
   return hip_status();
 }
 

@@ -110,9 +110,7 @@ class MappingEngine:
         raw = torch.empty(n, 4, dtype=torch.float32, device=z.device)
         self._saved = torch.empty(lib().nslam_query_saved_size(n), dtype=torch.uint8, device=z.device)
         cfg = self._cfg(stage, ro, rd, z, (), ())
-        with ops._span("query_fwd"):
-            rc = lib().nslam_query_fwd(ctypes.byref(cfg), None, n, ptr(raw), stream_ptr(z.device))
-        check(rc, "nslam_query_fwd")
+        ops.query_fwd_launch(cfg, None, n, raw)
         return raw
 
     def query_bwd(self, stage, ro, rd, z, g_raw, grid_grads, dec_grads, concurrent=None):

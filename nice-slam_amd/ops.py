@@ -196,9 +196,7 @@ class _Query(torch.autograd.Function):
         if torch.is_grad_enabled() and any(ctx.needs_input_grad):  # ReLU masks for the backward
             saved = torch.empty(lib().nslam_query_saved_size(pts.shape[0]), dtype=torch.uint8, device=pts.device)
             cfg.saved_masks = saved.data_ptr()
-        with _span("query_fwd"):
-            rc = lib().nslam_query_fwd(ctypes.byref(cfg), ptr(pts), pts.shape[0], ptr(raw), stream_ptr(pts.device))
-        check(rc, "nslam_query_fwd")
+        query_fwd_launch(cfg, pts, pts.shape[0], raw)
         ctx.meta = meta
         ctx.packed = packed
         ctx.grids = grids
@@ -338,6 +336,23 @@ class _GridSample(torch.autograd.Function):
             check(lib().nslam_grid_sample_bwd(ptr(g), dims, ptr(c), c.shape[0], ptr(gout.contiguous().float()),
                                               ptr(gg), ptr(gc), stream_ptr(c.device)), "nslam_grid_sample_bwd")
         return gg, gc
+
+
+SPLIT_FWD = True  # decoder-parallel forward (nslam_query_fwd_ws); False: one wave runs every decoder
+
+
+def query_fwd_launch(cfg, pts, n, raw, split=None):
+    """nslam_query_fwd_ws (decoder-parallel) or nslam_query_fwd (one fused chain per wave)."""
+    split = SPLIT_FWD if split is None else split
+    wsb = lib().nslam_query_fwd_workspace_size(ctypes.byref(cfg), n) if split else 0
+    with _span("query_fwd"):
+        if wsb:
+            ws = torch.empty(wsb, dtype=torch.uint8, device=raw.device)
+            rc = lib().nslam_query_fwd_ws(ctypes.byref(cfg), ptr(pts), n, ptr(raw), ptr(ws), wsb,
+                                          stream_ptr(raw.device))
+        else:
+            rc = lib().nslam_query_fwd(ctypes.byref(cfg), ptr(pts), n, ptr(raw), stream_ptr(raw.device))
+    check(rc, "nslam_query_fwd")
 
 
 def grid_sample_fwd(grid, coords, out):

@@ -275,3 +275,27 @@ def test_sparse_exchange_single_rank_is_identity(tiny):
     torch.cuda.synchronize()
     assert torch.equal(eng.gbuf, g0) and torch.equal(eng.decs["color"].grad, d0)
     assert ex.payload_bytes(keys, dn) == (sum(r.numel() for r in rows.values()) * 32 + d0.numel()) * 4
+
+
+@pytest.mark.parametrize("stage", ["middle", "fine", "color"])
+def test_decoder_parallel_forward_bitexact(tiny, stage):
+    """nslam_query_fwd_ws (one decoder per workgroup + occupancy combine) == nslam_query_fwd
+    (every decoder in one wave), raw and saved ReLU masks, pts form incl. out-of-bound points."""
+    sc, frames = _frames(tiny)
+    nice, c = _nice(sc)
+    g = torch.Generator(device=DEV).manual_seed(11)
+    lo, hi = sc.bound[:, 0].to(DEV), sc.bound[:, 1].to(DEV)
+    pts = (lo - 0.2 + (hi - lo + 0.4) * torch.rand(3001, 3, device=DEV, dtype=torch.float64, generator=g))
+    outs = []
+    for split in (False, True):
+        P.ops.SPLIT_FWD = split
+        try:
+            with torch.enable_grad():
+                gl = {k: v.detach().clone().requires_grad_(True) for k, v in c.items()}
+                raw = nice(pts, gl, stage=stage, oob_bound=sc.bound)
+            outs.append(raw.detach().clone())
+        finally:
+            P.ops.SPLIT_FWD = True
+    inside = ((pts > lo) & (pts < hi)).all(1)
+    assert bool((~inside).any()) and bool(inside.any())
+    assert torch.equal(outs[0], outs[1])
