@@ -78,7 +78,8 @@ typedef struct nslam_query_cfg {
   nslam_dec_grad dgrad[4];  /* parameter-gradient destinations                            */
   /* Ray form of the point list (ABI v4): when rays_o != NULL the points are generated in-kernel
    * as pts[r*S + s] = rays_o[r] + rays_d[r] * z_vals[r][s] in float64 (Renderer.py:172-174,
-   * float32 rays promoted), the `pts` argument is ignored and need_pts_grad must be 0. */
+   * float32 rays promoted) and the `pts` argument is ignored.  The backward's g_pts (ABI v5: also
+   * in ray form) is d loss / d pts per generated point, [M][3] float64. */
   const float* rays_o;      /* [M/S][3] float32 */
   const float* rays_d;      /* [M/S][3] float32 */
   const double* z_vals;     /* [M/S][S] float64 */

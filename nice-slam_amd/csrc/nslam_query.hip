@@ -1109,7 +1109,6 @@ int check_cfg(const nslam_query_cfg* c, bool bwd) {
   }
   if (c->rays_o) {
     if (!c->rays_d || !c->z_vals || c->n_samples <= 0) return NSLAM_EINVAL;
-    if (bwd && c->need_pts_grad) return NSLAM_EUNSUPPORTED;
   }
   return NSLAM_OK;
 }

@@ -27,6 +27,7 @@ import torch
 
 from . import _lib, ops
 from ._lib import check, lib, ptr, stream_ptr
+from .common import get_camera_from_tensor
 
 _GRID_OF = {"coarse": "grid_coarse", "middle": "grid_middle", "fine": "grid_fine", "color": "grid_color"}
 
@@ -66,7 +67,7 @@ class MappingEngine:
     """Fused mapping iterations over shared grids `c` (dict of [1,32,Z,Y,X] channels-last grids)
     and a NICE decoder stack, for the stage schedule of Mapper.optimize_map."""
 
-    def __init__(self, nice, c, bound, n_strat, n_surf, lindisp=False, w_color=0.2, device="cuda"):
+    def __init__(self, nice, c, bound, n_strat, n_surf, lindisp=False, w_color=0.2, device="cuda", grid_grads=True):
         self.nice, self.c, self.bound = nice, c, bound
         self.n_strat, self.n_surf, self.lindisp, self.w_color = n_strat, n_surf, lindisp, w_color
         self.device = torch.device(device)
@@ -78,12 +79,14 @@ class MappingEngine:
         self._side = []     # side streams of the concurrent decoder backward
         self.concurrent = True
         # one flat gradient buffer for every grid: zeroing is a single memset
-        sizes = {k: v.numel() for k, v in c.items()}
+        sizes = {k: v.numel() if grid_grads else 0 for k, v in c.items()}
         self.gbuf = torch.zeros(sum(sizes.values()), dtype=torch.float32, device=self.device)
         self.ggrad, off = {}, 0
         for k, v in c.items():
             if not v.is_contiguous(memory_format=torch.channels_last_3d):
                 raise ValueError(f"{k} must be channels-last (ops.channels_last)")
+            if not grid_grads:  # tracking: grids are constants (Tracker.py:138-141)
+                continue
             Z, Y, X = v.shape[2:]
             self.ggrad[k] = self.gbuf[off:off + sizes[k]].view(1, Z, Y, X, 32).permute(0, 4, 1, 2, 3)
             off += sizes[k]
@@ -113,14 +116,19 @@ class MappingEngine:
         ops.query_fwd_launch(cfg, None, n, raw)
         return raw
 
-    def query_bwd(self, stage, ro, rd, z, g_raw, grid_grads, dec_grads, concurrent=None):
+    def query_bwd(self, stage, ro, rd, z, g_raw, grid_grads, dec_grads, concurrent=None, pts_grad=False):
         """Backward into the engine's gradient buffers.  The decoders write disjoint buffers, so
         each runs as its own launch; with `concurrent` the frozen decoders (mask-only backward,
         atomics-heavy) run on side streams beside the one with weight gradients (MFMA-heavy) —
-        parallel branches when captured in a hipGraph."""
+        parallel branches when captured in a hipGraph.
+
+        pts_grad: also return d loss / d pts [N*S, 3] float64 (tracking, bundle adjustment): every
+        decoder writes its share into its own buffer (so the branches stay independent) and the
+        shares are summed afterwards."""
         n = z.numel()
         concurrent = self.concurrent if concurrent is None else concurrent
         cfg = self._cfg(stage, ro, rd, z, grid_grads, dec_grads)
+        cfg.need_pts_grad = int(bool(pts_grad))
         decs = sorted(ops._DEC_FOR_STAGE[stage], key=lambda d: d not in dec_grads)  # weight-grad one first
         main = torch.cuda.current_stream(z.device)
         streams = [main]
@@ -129,6 +137,7 @@ class MappingEngine:
                 self._side.append(torch.cuda.Stream(z.device))
             streams += self._side[:len(decs) - 1]
         used = streams[1:]
+        gp = [torch.empty(n, 3, dtype=torch.float64, device=z.device) for _ in decs] if pts_grad else None
         with ops._span("query_bwd"):
             for st in used:  # fork: every branch starts from the same point of the main stream
                 st.wait_stream(main)
@@ -140,11 +149,19 @@ class MappingEngine:
                 with torch.cuda.stream(st):
                     wsb = lib().nslam_query_bwd_decoder_workspace_size(ctypes.byref(cfg), d, n)
                     ws = torch.empty(wsb, dtype=torch.uint8, device=z.device) if wsb else None
-                    rc = lib().nslam_query_bwd_decoder(ctypes.byref(cfg), d, 0, None, n, ptr(g_raw), None, ptr(ws),
-                                                       wsb, st.cuda_stream)
+                    rc = lib().nslam_query_bwd_decoder(ctypes.byref(cfg), d, 0, None, n, ptr(g_raw),
+                                                       ptr(gp[i]) if pts_grad else None, ptr(ws), wsb, st.cuda_stream)
                 check(rc, "nslam_query_bwd_decoder")
+                if pts_grad and st is not main:
+                    gp[i].record_stream(st)
             for st in used:
                 main.wait_stream(st)
+        if pts_grad:
+            out = gp[0]
+            for g in gp[1:]:
+                out += g
+            return out
+        return None
 
     # -- one iteration ---------------------------------------------------------------------------
     def grads_for(self, stage, trainable_decoders):
@@ -193,6 +210,87 @@ class MappingEngine:
         for n in dnames:
             self.decs[n].repack()
         return ray_loss, keep
+
+
+def camera_dirs(pix, n_per, n_frames, window, intrinsics, device):
+    """Camera-frame ray directions of select_uv pixel draws (src/common.py:80-84, 113-134):
+    dirs = ((i-cx)/fx, -(j-cy)/fy, -1) for window index k -> (j, i) = (h0 + k // ww, w0 + k % ww)."""
+    h0, h1, w0, w1 = window
+    fx, fy, cx, cy = intrinsics
+    ww = w1 - w0
+    i = (pix % ww + w0).to(torch.float32)
+    j = (pix // ww + h0).to(torch.float32)
+    d = torch.stack([(i - cx) / fx, -(j - cy) / fy, -torch.ones_like(i)], -1)
+    return d.view(n_frames, n_per, 3)
+
+
+def c2w_grads(g_pts, z, dirs):
+    """d loss / d c2w[:3, :4] per frame from d loss / d pts, through pts = o + d·z
+    (Renderer.py:172-174), rays_o = t and rays_d = R·dir (common.py:80-89):
+    g_t = sum_{r,s} g_pts, g_R = sum_r (sum_s z g_pts) dirᵀ.  dirs [F, n, 3] → [F, 3, 4]."""
+    F, n = dirs.shape[:2]
+    gp = g_pts.view(F, n, -1, 3)
+    g_ro = gp.sum(2).float()
+    g_rd = (gp * z.view(F, n, -1, 1)).sum(2).float()
+    g_R = torch.einsum("fnm,fnk->fmk", g_rd, dirs)
+    return torch.cat([g_R, g_ro.sum(1)[..., None]], 2)
+
+
+class TrackingEngine:
+    """Tracker.optimize_cam_in_batch (src/Tracker.py:71-128) on the HIP kernels, without host
+    synchronisation: one camera iteration is
+
+        c2w = get_camera_from_tensor(cam)              (autograd on the 7-vector only)
+        pixels → rays + inside mask                    nslam_gather_rays
+        sampler, decoders (ray form, ReLU masks saved) nslam_sample_rays, nslam_query_fwd_ws
+        compositing + tracker loss + their backward    nslam_render_loss (mode TRACKER, median)
+        d loss / d pts, frozen decoders                nslam_query_bwd_decoder (mask-only, 3 branches)
+        pts → rays → c2w → cam                         c2w_grads + autograd through quad2rotation
+        Adam on the camera                             ops.FusedAdam (device step count)
+
+    so `iters` iterations can be captured in one hipGraph.  Grids and decoders are constants
+    (Tracker.py:138-141): no grid or weight gradients are formed.  As in the reference, dropped
+    rays (inside mask) carry no loss and the handle_dynamic median is over kept rays only.
+    """
+
+    def __init__(self, nice, c, bound, n_strat, n_surf, hw, intrinsics, ignore_edge=(20, 20), w_color=0.5,
+                 handle_dynamic=True, use_color=True, device="cuda"):
+        self.eng = MappingEngine(nice, c, bound, n_strat, n_surf, device=device, grid_grads=False)
+        self.bound, self.n_strat, self.n_surf = bound, n_strat, n_surf
+        self.H, self.W = hw
+        self.intr = intrinsics
+        he, we = ignore_edge
+        self.window = (he, self.H - he, we, self.W - we)
+        self.w_color, self.handle_dynamic, self.use_color = w_color, handle_dynamic, use_color
+        self.device = torch.device(device)
+
+    def n_window(self):
+        h0, h1, w0, w1 = self.window
+        return (h1 - h0) * (w1 - w0)
+
+    def iteration(self, cam, depth, color, pix, optimizer):
+        """One camera iteration on frame (depth [H,W], color [H,W,3]) with pixel draws `pix`
+        (int64 [n], select_uv indices into the edge-cropped window).  cam: [7] leaf tensor whose
+        .grad the optimizer reads.  Returns the loss (device f64 scalar) of the pose BEFORE the step."""
+        fx, fy, cx, cy = self.intr
+        n = pix.numel()
+        with torch.enable_grad():
+            c2w = get_camera_from_tensor(cam)
+        ro, rd, gd, gc, keep = ops.gather_rays([(depth, color, c2w.detach())], pix, n, self.H, self.W, self.window,
+                                               fx, fy, cx, cy, self.bound)
+        z = ops.sample_z(ro, rd, gd, self.bound, self.n_strat, self.n_surf)
+        raw = self.eng.query_fwd("color", ro, rd, z)
+        _, _, _, ray_loss, g_raw = ops.render_loss(raw, z, gd, gc, keep, mode="tracker", use_color=self.use_color,
+                                                   handle_dynamic=self.handle_dynamic, w_color=self.w_color)
+        g_pts = self.eng.query_bwd("color", ro, rd, z, g_raw, (), (), pts_grad=True)
+        g_c2w = c2w_grads(g_pts, z, camera_dirs(pix, n, 1, self.window, self.intr, pix.device))[0]
+        (g_cam,) = torch.autograd.grad(c2w, cam, g_c2w)
+        if cam.grad is None:
+            cam.grad = g_cam
+        else:
+            cam.grad.copy_(g_cam)
+        optimizer.step()
+        return ray_loss.sum()
 
 
 def frustum_rows(mask_xyz: torch.Tensor) -> torch.Tensor:

@@ -48,6 +48,8 @@ class Tracker(object):
         self.c = {}
         self.decoders = None
         self._bound_dev = None
+        self.fused = True     # track_frame on engine.TrackingEngine (no host sync per iteration)
+        self._engine = None
 
     def _inside_mask(self, rays_o, rays_d, gt_depth):
         """Tracker.py:95-100: keep rays whose AABB exit distance >= gt depth."""
@@ -96,6 +98,21 @@ class Tracker(object):
             for key, val in self.shared_c.items():
                 self.c[key] = val.detach().clone().to(self.device)
             self.prev_mapping_idx = self.mapping_idx[0].clone()
+            self._engine = None  # re-bound to the new snapshot on first use
+
+    def engine(self):
+        """TrackingEngine over the current decoder/grid snapshot."""
+        if self._engine is None:
+            from .engine import TrackingEngine
+            from .ops import channels_last
+            r = self.renderer
+            c = {k: channels_last(v) for k, v in self.c.items() if k != "grid_coarse"}
+            self._engine = TrackingEngine(self.decoders, c, self.bound, r.N_samples, r.N_surface, (self.H, self.W),
+                                          (self.fx, self.fy, self.cx, self.cy),
+                                          ignore_edge=(self.ignore_edge_H, self.ignore_edge_W),
+                                          w_color=self.w_color_loss, handle_dynamic=self.handle_dynamic,
+                                          use_color=self.use_color_in_tracking, device=self.device)
+        return self._engine
 
     def track_frame(self, idx, gt_color, gt_depth, gt_c2w, pre_c2w=None, prev2_c2w=None):
         """Per-frame camera estimate (Tracker.py:184-256, without sync/visualisation) → c2w [4,4]."""
@@ -120,11 +137,35 @@ class Tracker(object):
             camera_tensor = camera_tensor.clone().requires_grad_(True)
             optimizer = torch.optim.Adam([camera_tensor], lr=self.cam_lr)
         best, best_loss = None, np.inf
+        if self.fused and not self.seperate_LR:
+            return self._track_fused(camera_tensor, gt_color, gt_depth)
         for _ in range(self.num_cam_iters):
             if self.seperate_LR:
                 camera_tensor = torch.cat([quad, T], 0)
             loss = self.optimize_cam_in_batch(camera_tensor, gt_color, gt_depth, self.tracking_pixels, optimizer)
             if loss < best_loss:
                 best_loss, best = loss, camera_tensor.clone().detach()
+        bottom = torch.tensor([[0, 0, 0, 1.0]], dtype=torch.float32, device=device)
+        return torch.cat([get_camera_from_tensor(best), bottom], 0)
+
+    def _track_fused(self, camera_tensor, gt_color, gt_depth):
+        """The camera loop of track_frame (Tracker.py:225-250) on the TrackingEngine: the best pose
+        (lowest pre-step loss → the pose right after that step, as the reference keeps it) is
+        selected on the device; one host sync at the end."""
+        from .ops import FusedAdam
+        eng = self.engine()
+        device = self.device
+        cam = camera_tensor.detach().clone().requires_grad_(True)
+        opt = FusedAdam([{"params": [cam], "lr": self.cam_lr}])
+        best = cam.detach().clone()
+        best_loss = torch.full((), float("inf"), dtype=torch.float64, device=device)
+        depth = gt_depth.float().contiguous()
+        color = gt_color.float().contiguous()
+        for _ in range(self.num_cam_iters):
+            pix = torch.randint(eng.n_window(), (self.tracking_pixels,), device=device, generator=self.generator)
+            loss = eng.iteration(cam, depth, color, pix, opt)
+            better = loss < best_loss
+            best_loss = torch.where(better, loss, best_loss)
+            best = torch.where(better, cam.detach(), best)
         bottom = torch.tensor([[0, 0, 0, 1.0]], dtype=torch.float32, device=device)
         return torch.cat([get_camera_from_tensor(best), bottom], 0)

@@ -299,3 +299,60 @@ def test_decoder_parallel_forward_bitexact(tiny, stage):
     inside = ((pts > lo) & (pts < hi)).all(1)
     assert bool((~inside).any()) and bool(inside.any())
     assert torch.equal(outs[0], outs[1])
+
+
+def test_tracking_engine_matches_oracle(tiny):
+    """TrackingEngine (fused camera iteration, Tracker.py:71-128) vs the oracle's autograd replica on
+    the same pixel draws: per-iteration losses, first camera gradient, camera after 3 steps."""
+    import copy
+
+    from test_gpu_dropins import oracle_samples
+    sc = Scene(tiny)
+    slam = sc.slam(base_cfg())
+    eng = P.engine.TrackingEngine(copy.deepcopy(slam.shared_decoders), slam.shared_c, sc.bound, 32, 16,
+                                  (sc.H, sc.W), (sc.fx, sc.fy, sc.cx, sc.cy), ignore_edge=(20, 20), w_color=0.5,
+                                  handle_dynamic=True, use_color=True, device=DEV)
+    cam0 = P.common.get_tensor_from_camera(sc.c2w).cuda()
+    cam = cam0.clone().requires_grad_(True)
+    opt = P.ops.FusedAdam([{"params": [cam], "lr": 0.001}])
+    g = torch.Generator().manual_seed(11)
+    pixs = [torch.randint(eng.n_window(), (200,), generator=g) for _ in range(3)]
+    losses, grads = [], []
+    for k in range(3):
+        losses.append(float(eng.iteration(cam, sc.depth.cuda(), sc.color.cuda(), pixs[k].cuda(), opt)))
+        grads.append(cam.grad.detach().clone())
+    camo = cam0.cpu().clone().requires_grad_(True)
+    opto = torch.optim.Adam([camo], lr=0.001)
+    ref, ref_grads = [], []
+    for k in range(3):
+        opto.zero_grad()
+        c2w = orc.camera_from_tensor(camo)
+        ro, rd, gd, gc = oracle_samples(sc, pixs[k], 20, sc.H - 20, 20, sc.W - 20, c2w, sc.depth, sc.color)
+        keep = orc.inside_mask(ro, rd, gd, sc.bound)
+        ro, rd, gd, gc = ro[keep], rd[keep], gd[keep], gc[keep]
+        d, v, c = orc.render_batch_ray(sc.sd, sc.grids, rd, ro, "color", sc.bound, gd)
+        loss = orc.tracker_loss(d, v, c, gd, gc)
+        loss.backward()
+        ref_grads.append(camo.grad.detach().clone())
+        opto.step()
+        ref.append(float(loss))
+    np.testing.assert_allclose(losses, ref, rtol=2e-4)
+    assert rel_l2(grads[0], ref_grads[0]) < 1e-3
+    assert rel_l2(cam.detach().cpu() - cam0.cpu(), camo.detach() - cam0.cpu()) < 1e-2
+
+
+def test_tracker_track_frame_fused_matches_loop(tiny):
+    """Tracker.track_frame on the TrackingEngine == the reference loop over optimize_cam_in_batch
+    (same generator ⇒ same pixel draws; device-side best-pose selection vs loss.item())."""
+    cfg = base_cfg()
+    sc = Scene(tiny)
+    outs = []
+    for fused in (False, True):
+        slam = sc.slam(cfg)
+        tr = P.Tracker(cfg, None, slam, generator=torch.Generator(device=DEV).manual_seed(4))
+        tr.fused = fused
+        c2w = torch.cat([sc.c2w, torch.tensor([[0, 0, 0, 1.0]])], 0).cuda()
+        pre = c2w.clone()
+        pre[:3, 3] += 0.02
+        outs.append(tr.track_frame(1, sc.color.cuda(), sc.depth.cuda(), c2w, pre_c2w=pre))
+    assert torch.allclose(outs[0], outs[1], atol=5e-4), (outs[0] - outs[1]).abs().max()
