@@ -37,6 +37,40 @@ FLOP_FWD_PER_SAMPLE = 2 * (15479 + 20599 + 15575)   # SURVEY §8(a10) MACs, colo
 BYTES_FWD_PER_SAMPLE = 3 * 1024                      # 3 trilinear lookups × 8 corners × 128 B
 F32_PEAK_TFLOPS = 157.3                              # MI355X dense fp32 (MFMA = VALU rate)
 HBM_PEAK_GBS = 8000.0
+# Algorithmic work per ray-sample of each timed C-ABI launch of the colour-stage mapping
+# iteration: (FLOPs, HBM bytes).  Forward: the three decoders' MACs and three
+# 1024-B trilinear lookups.  Backward per decoder: the colour decoder (optimised) needs input and
+# weight gradients = 2× its forward MACs; the frozen middle/fine decoders need input gradients
+# only = 1× their MACs (mask-only backward, no recompute); each scatters one 8-corner gradient
+# into its grid = 1024 B read + 1024 B written (float-atomic RMW).
+KERNEL_WORK = {
+    "query_fwd": (FLOP_FWD_PER_SAMPLE, BYTES_FWD_PER_SAMPLE),
+    "query_bwd.color": (2 * 2 * 15575, 2048),
+    "query_bwd.fine": (2 * 20599, 2048),
+    "query_bwd.middle": (2 * 15479, 2048),
+}
+# rocprofv3 kernel names behind each span (for the PMC traffic of profiles/*traffic*.json)
+SPAN_KERNELS = {
+    "query_fwd": ("k_query_fwd", "k_occ_combine"),
+    "query_bwd.color": ("k_dec_bwd<3,", "k_slab_reduce"),
+    "query_bwd.fine": ("k_dec_bwd<2,",),
+    "query_bwd.middle": ("k_dec_bwd<1,",),
+}
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r01_traffic.json")
+
+
+def pmc_traffic(span):
+    """HBM bytes per launch of `span` from the committed PMC summary (tools/traffic.py: separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this bench, FETCH_SIZE doubled per the
+    MI355X guide's gfx950 correction), or None when absent."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            kern = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    pats = SPAN_KERNELS.get(span, ())
+    hits = [v["hbm_bytes_per_launch"] for k, v in kern.items() if any(k.startswith(p) for p in pats)]
+    return sum(hits) if hits else None
 
 
 def pkg():
@@ -317,6 +351,81 @@ def reference_gpu_baseline(scene, budget_s=4.0):
                       "(torch ops of the reference path) on the GPU, eager"}
 
 
+def kernel_roofline(name, avg_ms, pts):
+    """Roofline of one timed launch: algorithmic FLOPs and bytes (KERNEL_WORK × ray-samples per
+    launch) over its HIP-event average; the bound is whichever roof (fp32 MFMA, HBM) the
+    algorithmic work would hit first."""
+    fl, by = KERNEL_WORK[name]
+    t = avg_ms * 1e-3
+    tflops, gbs = pts * fl / t / 1e12, pts * by / t / 1e9
+    mfma = fl / (F32_PEAK_TFLOPS * 1e12) >= by / (HBM_PEAK_GBS * 1e9)
+    achieved, peak, unit = (tflops, F32_PEAK_TFLOPS, "TFLOP/s") if mfma else (gbs, HBM_PEAK_GBS, "GB/s")
+    return {"kernel": name, "bound": "mfma" if mfma else "hbm", "achieved": achieved, "peak": peak, "unit": unit,
+            "frac": achieved / peak, "traffic": pmc_traffic(name), "avg_launch_ms": avg_ms,
+            "ray_samples_per_launch": pts, "flop_per_sample": fl, "bytes_per_sample": by,
+            "traffic_note": "HBM bytes per launch: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, "
+                            "profiles/r01_traffic.json"}
+
+
+def room0_frame_rate(scene, reps=20):
+    """frames/s on Replica room0 (BASELINE metric) from measured iteration times:
+    per frame 10 tracking iterations × 200 pixels (replica.yaml tracking, edges 100 px) and 12
+    mapping iterations × 1000 pixels (60 iterations every 5 frames, stage split middle 25 / fine 12
+    / colour 23 of 60: Mapper.py:403-419).  Each iteration type is captured in a hipGraph and
+    replayed `reps` times.  'sequential' = tracker and mapper on one stream back to back (a lower
+    bound; the reference runs them as concurrent processes)."""
+    P = pkg()
+    cfg = scene.cfg
+    H, W = cfg["H"], cfg["W"]
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            fn()
+        torch.cuda.current_stream().wait_stream(side)
+        try:
+            with torch.cuda.graph(g):
+                fn()
+            run, mode = g.replay, "hipgraph"
+        except Exception:  # pragma: no cover - eager fallback
+            run, mode = fn, "eager"
+        run()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            run()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps * 1e3, mode
+
+    ms = {}
+    for stage in ("middle", "fine", "color"):
+        ms["map_" + stage], _ = timed(lambda: scene.step(stage=stage))
+    import copy
+    te = P.engine.TrackingEngine(copy.deepcopy(scene.nice), scene.grids, scene.bound, cfg["n_strat"], cfg["n_surf"],
+                                 (H, W), (cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"]), ignore_edge=(100, 100),
+                                 w_color=0.5, handle_dynamic=True, use_color=True, device=scene.dev)
+    cam = P.common.get_tensor_from_camera(scene.c2w[0]).to(scene.dev).requires_grad_(True)
+    opt = P.ops.FusedAdam([{"params": [cam], "lr": 0.001}])
+    nwin = te.n_window()
+
+    def track():
+        pix = torch.randint(nwin, (200,), device=scene.dev)
+        te.iteration(cam, scene.depth[0], scene.color[0], pix, opt)
+
+    ms["track"], tmode = timed(track)
+    t_map = (25 * ms["map_middle"] + 12 * ms["map_fine"] + 23 * ms["map_color"]) / 60.0
+    t_frame = 10 * ms["track"] + 12 * t_map
+    return {"frames_per_s": 1e3 / t_frame, "frames_per_s_concurrent": 1e3 / max(10 * ms["track"], 12 * t_map),
+            "ms_per_iteration": {k: round(v, 4) for k, v in ms.items()}, "tracking_launch_mode": tmode,
+            "note": "sequential: 10 tracking + 12 mapping iterations per frame on one GPU stream; concurrent: "
+                    "tracker and mapper overlapped as the reference's processes (max of the two)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -325,6 +434,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture")
     ap.add_argument("--no-stress", action="store_true", help="skip the 512^3 grid-query HBM measurement")
+    ap.add_argument("--no-frames", action="store_true", help="skip the room0 frames/s (tracking + mapping stages)")
     ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                     help="process-group backend for N>1 (gloo: rehearse the sharded path on one GPU, eager)")
     ap.add_argument("--pixels", type=int, default=None,
@@ -407,12 +517,11 @@ def main():
         pts_per_step = samples / args.steps
         qf = timers.get("query_fwd", {"avg_ms": float("nan")})
         qb = timers.get("query_bwd", {"avg_ms": float("nan")})
-        dom_name, dom = max(((k, v) for k, v in timers.items()), key=lambda kv: kv[1]["total_ms"])
-        if dom_name == "query_bwd":
-            flops = pts_per_step * 2 * FLOP_FWD_PER_SAMPLE  # algorithmic minimum ≈ 2× fwd MACs
-        else:
-            flops = pts_per_step * FLOP_FWD_PER_SAMPLE
-        achieved = flops / (dom["avg_ms"] * 1e-3) / 1e12
+        # the dominant single launch (query_bwd is the span over its concurrent branches)
+        dom_name, dom = max(((k, v) for k, v in timers.items() if k in KERNEL_WORK),
+                            key=lambda kv: kv[1]["total_ms"])
+        roof = kernel_roofline(dom_name, dom["avg_ms"], pts_per_step)
+        per_kernel = {k: kernel_roofline(k, v["avg_ms"], pts_per_step) for k, v in timers.items() if k in KERNEL_WORK}
         out = {
             "metric": "ray-samples/sec (fwd+bwd) per mapping iter; frames/sec on Replica room0",
             "value": samples_all / dt_max, "unit": "ray-samples/s", "n_gpus": world, "steps": args.steps,
@@ -424,11 +533,8 @@ def main():
                                    "(5-frame window x 200), grids middle/fine/colour, Adam",
                        "global_batch": int(round(pts_per_step)) * world, "seq_len": 48,
                        "parallelism": f"rays sharded dp{world}, RCCL all-reduce of the frustum-row gradients"},
-            "roofline": {"kernel": dom_name, "bound": "mfma", "achieved": achieved, "peak": F32_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved / F32_PEAK_TFLOPS, "traffic": None,
-                         "avg_launch_ms": dom["avg_ms"],
-                         "note": "fp32 MFMA (v_mfma_f32_32x32x2_f32); algorithmic FLOPs per ray-sample "
-                                 f"{FLOP_FWD_PER_SAMPLE} fwd / {2 * FLOP_FWD_PER_SAMPLE} bwd"},
+            "roofline": roof,
+            "kernel_rooflines": per_kernel,
             "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in timers.items()},
             "query_fwd_hbm_frac": (pts_per_step * BYTES_FWD_PER_SAMPLE / (qf["avg_ms"] * 1e-3) / 1e9) / HBM_PEAK_GBS,
             "query_bwd_ms": qb["avg_ms"],
@@ -437,6 +543,8 @@ def main():
             keys, dn = scene.engine.grads_for("color", ("color",))
             out["exchange_bytes_per_step"] = scene.exchange.payload_bytes(keys, dn)
             out["dense_grad_bytes_per_step"] = scene.engine.gbuf.numel() * 4
+        if world == 1 and not args.no_frames and args.path == "fused":
+            out["room0"] = room0_frame_rate(scene)
         if world == 1 and not args.no_stress:
             out["grid_query_stress"] = stress_grid_query(dev)
         if world == 1 and not args.no_cpu_baseline:

@@ -75,7 +75,7 @@ __global__ __launch_bounds__(256) void k_composite_fwd(const float* __restrict__
                                                        int64_t n, int S, double* __restrict__ depth,
                                                        double* __restrict__ var, float* __restrict__ color) {
   const int lane = threadIdx.x & 63;
-  const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t ray = (int64_t)blockIdx.x * 4 + wave_id();
   if (ray >= n) return;
   const float* rr = raw + ray * (int64_t)S * 4;
   const double* zz = zv + ray * (int64_t)S;
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(256) void k_composite_bwd(const float* __restrict__
                                                        const double* __restrict__ gvar,
                                                        const float* __restrict__ gcol, float* __restrict__ graw) {
   const int lane = threadIdx.x & 63;
-  const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t ray = (int64_t)blockIdx.x * 4 + wave_id();
   if (ray >= n) return;
   const float* rr = raw + ray * (int64_t)S * 4;
   const double* zz = zv + ray * (int64_t)S;
@@ -260,7 +260,7 @@ struct LossArgs {
 template <int PASS>
 __global__ __launch_bounds__(256) void k_render_loss(LossArgs a) {
   const int lane = threadIdx.x & 63;
-  const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t ray = (int64_t)blockIdx.x * 4 + wave_id();
   if (ray >= a.n) return;
   const int S = a.S;
   const float* rr = a.raw + ray * (int64_t)S * 4;

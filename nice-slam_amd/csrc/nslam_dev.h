@@ -76,6 +76,10 @@ struct NoXyzPack {  // MLP_no_xyz (decoder.py:206-274), coarse level
 // ------------------------------------------------------------------------------------------
 // MFMA tile helpers
 // ------------------------------------------------------------------------------------------
+// Wave index inside the workgroup as a wave-uniform (SGPR) value: LLVM's divergence analysis
+// treats threadIdx.x >> 6 as divergent, which would push every tile / slab address derived from
+// it into VGPRs (and buffer resources into waterfall loops).
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 __device__ __forceinline__ int fidx(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {

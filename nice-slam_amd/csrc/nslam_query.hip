@@ -798,7 +798,7 @@ __device__ __forceinline__ void coord_grad(const nslam_grid& g, const Corners& c
 template <int STAGE>
 __global__ __launch_bounds__(256, 2) void k_query_fwd(QueryKArgs a) {
   const int lane = threadIdx.x & 63;
-  const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t tile = (int64_t)blockIdx.x * 4 + wave_id();
   if (tile * 32 >= a.n) return;  // wave-uniform
   const int h = lane >> 5;
   const Pt q = load_point(a, tile * 32 + (lane & 31));
@@ -869,7 +869,7 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd_parts(QueryKArgs a, float*
   constexpr int NPARTS = STAGE == NSLAM_STAGE_COLOR ? 3 : 2;
   const int part = (int)(blockIdx.x % NPARTS);
   const int lane = threadIdx.x & 63;
-  const int64_t tile = (int64_t)(blockIdx.x / NPARTS) * 4 + (threadIdx.x >> 6);
+  const int64_t tile = (int64_t)(blockIdx.x / NPARTS) * 4 + wave_id();
   if (tile * 32 >= a.n) return;  // wave-uniform
   const int h = lane >> 5;
   const int64_t idx = tile * 32 + (lane & 31);
@@ -1033,7 +1033,7 @@ __global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd(QueryKArgs a, flo
   // the per-point tables (sizing LDS per variant keeps the lean kernels at 5+ waves/SIMD)
   constexpr int kScr = WG ? kScratchFloats : TILE_FLOATS + 32 * 8 * 2;
   __shared__ __attribute__((aligned(16))) float lds[kWavesBwd * kScr];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = wave_id();
   float* sc = lds + wave * kScr;
   Scratch S;
   S.sA = sc;
@@ -1068,7 +1068,7 @@ __global__ __launch_bounds__(64 * kReduceWaves) void k_slab_reduce(const float* 
                                                                    int acc_floats, int count,
                                                                    float* __restrict__ base) {
   __shared__ f32x4 part[kReduceWaves * 4][16];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = wave_id();
   const int c = lane & 15, r = wave * 4 + (lane >> 4);  // r: slab stream 0..63
   const int j = (blockIdx.x * 16 + c) * 4;
   f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;

@@ -131,7 +131,7 @@ __global__ __launch_bounds__(128) void k_sample(SamplerArgs a) {
 // broken by lane), i.e. exactly the ascending order torch.sort produces — no serial merge.
 __global__ __launch_bounds__(256) void k_sample_wave(SamplerArgs a) {
   const int lane = threadIdx.x & 63;
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t r = (int64_t)blockIdx.x * 4 + wave_id();
   if (r >= a.n) return;
   double tmin = 0.0;
 #pragma unroll

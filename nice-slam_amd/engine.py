@@ -149,8 +149,10 @@ class MappingEngine:
                 with torch.cuda.stream(st):
                     wsb = lib().nslam_query_bwd_decoder_workspace_size(ctypes.byref(cfg), d, n)
                     ws = torch.empty(wsb, dtype=torch.uint8, device=z.device) if wsb else None
-                    rc = lib().nslam_query_bwd_decoder(ctypes.byref(cfg), d, 0, None, n, ptr(g_raw),
-                                                       ptr(gp[i]) if pts_grad else None, ptr(ws), wsb, st.cuda_stream)
+                    with ops._span("query_bwd." + name):  # this branch alone, on its own stream
+                        rc = lib().nslam_query_bwd_decoder(ctypes.byref(cfg), d, 0, None, n, ptr(g_raw),
+                                                           ptr(gp[i]) if pts_grad else None, ptr(ws), wsb,
+                                                           st.cuda_stream)
                 check(rc, "nslam_query_bwd_decoder")
                 if pts_grad and st is not main:
                     gp[i].record_stream(st)
