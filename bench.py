@@ -165,8 +165,9 @@ class Room0Scene:
         if path == "fused":
             for t in self.grids.values():
                 t.requires_grad_(False)
+            # grid gradients accumulate only on the frustum-selected rows Adam optimises (compact)
             self.engine = P.engine.MappingEngine(self.nice, self.grids, self.bound, cfg["n_strat"], cfg["n_surf"],
-                                                 w_color=cfg["w_color"], device=dev)
+                                                 w_color=cfg["w_color"], device=dev, rows=self.rows)
             self.opt = P.ops.FusedAdam(
                 [{"params": [self.engine.decs["color"].param], "lr": cfg["lr"]["decoders"]}] +
                 [{"params": [self.grids[k]], "lr": cfg["lr"][k[5:]], "rows": self.rows[k]}
@@ -542,7 +543,7 @@ def main():
         if sharded and args.path == "fused":
             keys, dn = scene.engine.grads_for("color", ("color",))
             out["exchange_bytes_per_step"] = scene.exchange.payload_bytes(keys, dn)
-            out["dense_grad_bytes_per_step"] = scene.engine.gbuf.numel() * 4
+            out["dense_grad_bytes_per_step"] = sum(v.numel() for v in scene.grids.values()) * 4
         if world == 1 and not args.no_frames and args.path == "fused":
             out["room0"] = room0_frame_rate(scene)
         if world == 1 and not args.no_stress:

@@ -52,6 +52,11 @@ typedef struct nslam_grid {
   int32_t pad_;
   double lo[3];      /* x, y, z lower bound (float64, as the reference)                      */
   double hi[3];      /* x, y, z upper bound                                                  */
+  /* ABI v6, frustum-compacted gradient: slot == NULL -> `grad` is a dense grid like `data`; else
+   * `grad` is [n_rows][32] for the frustum-selected voxels (Mapper.py:314-333) and slot[Z*Y*X]
+   * maps a voxel row to its compact row (-1: not selected, its gradient is not formed — the
+   * reference optimises only the masked vector, Mapper.py:394-401). */
+  const int32_t* slot;
 } nslam_grid;
 
 /* Where a decoder's parameter gradients go: `base` is a flat float32 buffer and the offsets are
@@ -228,6 +233,9 @@ typedef struct nslam_adam_seg {
   int64_t n;
   int32_t row_len;
   float lr;
+  int32_t grad_rows; /* ABI v6, row-masked segments: 1 = grad is compact [n][row_len] in row-list order
+                        (the frustum-compacted gradient of nslam_grid.slot); 0 = grad is dense like param */
+  int32_t pad_;
 } nslam_adam_seg;
 int nslam_adam_step(const nslam_adam_seg* segs, int32_t n_segs, float beta1, float beta2, float eps,
                     int32_t zero_grad, uint32_t* ticket, void* stream);

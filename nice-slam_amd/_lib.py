@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NSLAM_LIB") or os.path.join(_HERE, "libnslam.so")  # NSLAM_LIB: instrumented builds
 
 NSLAM_OK = 0
-ABI_VERSION = 5
+ABI_VERSION = 6
 STAGES = {"coarse": 0, "middle": 1, "fine": 2, "color": 3}
 DEC_COARSE, DEC_MIDDLE, DEC_FINE, DEC_COLOR = 0, 1, 2, 3
 
@@ -29,6 +29,7 @@ class NslamGrid(ctypes.Structure):
         ("pad_", ctypes.c_int32),
         ("lo", ctypes.c_double * 3),
         ("hi", ctypes.c_double * 3),
+        ("slot", ctypes.c_void_p),  # ABI v6: frustum-compacted gradient (NULL = dense)
     ]
 
 
@@ -88,6 +89,8 @@ class NslamAdamSeg(ctypes.Structure):
         ("n", ctypes.c_int64),
         ("row_len", ctypes.c_int32),
         ("lr", ctypes.c_float),
+        ("grad_rows", ctypes.c_int32),  # ABI v6: compact [n][row_len] gradient of a row-masked segment
+        ("pad_", ctypes.c_int32),
     ]
 
 

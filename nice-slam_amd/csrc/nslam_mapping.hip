@@ -149,7 +149,8 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam(AdamArgs a) {
       const int64_t base = (int64_t)sg.rows[ri] * sg.row_len + part * 4;
       const int64_t sbase = ri * sg.row_len + part * 4;
       f32x4 p = *reinterpret_cast<const f32x4*>(sg.param + base);
-      const f32x4 g = *reinterpret_cast<const f32x4*>(sg.grad + base);
+      const int64_t gbase = sg.grad_rows ? sbase : base;
+      const f32x4 g = *reinterpret_cast<const f32x4*>(sg.grad + gbase);
       f32x4 m = *reinterpret_cast<const f32x4*>(sg.exp_avg + sbase);
       f32x4 v = *reinterpret_cast<const f32x4*>(sg.exp_avg_sq + sbase);
 #pragma unroll
@@ -163,7 +164,7 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam(AdamArgs a) {
       *reinterpret_cast<f32x4*>(sg.param + base) = p;
       *reinterpret_cast<f32x4*>(sg.exp_avg + sbase) = m;
       *reinterpret_cast<f32x4*>(sg.exp_avg_sq + sbase) = v;
-      if (a.zero_grad) *reinterpret_cast<f32x4*>(sg.grad + base) = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (a.zero_grad) *reinterpret_cast<f32x4*>(sg.grad + gbase) = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
 }

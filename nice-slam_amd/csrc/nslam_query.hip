@@ -99,8 +99,9 @@ struct Scratch {
   float* sX;    // [32][33] transposed input tile
   float* gtab;  // [32][4]  per-point output cotangents
   float* xtab;  // [32][3]  per-point x (float)
-  int* crow;    // [32][8]
+  int* crow;    // [32][8]  corner rows (grad slots when the grid gradient is frustum-compacted)
   float* cw;    // [32][8]
+  int* ccell;   // [32]     cell of each point (corner-0 row): the run-merge key
 };
 
 // Scratch is wave-private: ordering LDS writes before other lanes' reads of the same wave needs
@@ -666,8 +667,35 @@ __device__ __forceinline__ void noxyz_backward_saved(const float* __restrict__ p
 // grid gradient scatter (atomics shaped as two 128-B row segments per wave-instruction) and
 // coordinate gradient through the trilinear weights
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void scatter_grid_grad_uniform(float* __restrict__ grad, const Corners& cr, const f32x16& dc,
-                                                  bool valid, const Scratch& S, int lane) {
+// Stage a tile's corner rows / weights for the scatter.  With a slot map (ABI v6: frustum-
+// compacted grid gradient, Mapper.py:314-333) corner row r accumulates into compact row slot[r];
+// corners outside the frustum selection (slot -1) get weight 0, i.e. no atomic: the reference
+// never forms their gradient (its optimised tensor is the masked vector, Mapper.py:394-401).
+__device__ __forceinline__ void stage_corners(const Corners& cr, const int32_t* __restrict__ slot, bool valid,
+                                              const Scratch& S, int lane) {
+  if (lane < 32) {
+    const int p = lane;
+    S.ccell[p] = cr.row[0];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      int r = cr.row[k];
+      float w = valid ? cr.w[k] : 0.f;
+      if (slot) {
+        r = slot[r];
+        if (r < 0) {
+          r = 0;
+          w = 0.f;
+        }
+      }
+      S.crow[p * 8 + k] = r;
+      S.cw[p * 8 + k] = w;
+    }
+  }
+}
+
+__device__ __forceinline__ void scatter_grid_grad_uniform(float* __restrict__ grad, const int32_t* __restrict__ slot,
+                                                          const Corners& cr, const f32x16& dc, bool valid,
+                                                          const Scratch& S, int lane) {
   // Points of a tile are consecutive samples of (mostly) one ray: runs of samples that fall in the
   // same cell are summed in registers first, so a run costs one flush instead of one per sample.
   // The whole wave walks the tile's 32 points in step (uniform control flow, runs merged over the
@@ -676,14 +704,7 @@ __device__ __forceinline__ void scatter_grid_grad_uniform(float* __restrict__ gr
   // wave-instruction adds one contiguous 256-B segment — the full-rate shape of a float atomic.
   const int h = lane >> 5, ch = lane & 31;
   tstore(S.sA, dc, lane);
-  if (h == 0) {
-    const int p = lane & 31;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      S.crow[p * 8 + k] = cr.row[k];
-      S.cw[p * 8 + k] = valid ? cr.w[k] : 0.f;
-    }
-  }
+  stage_corners(cr, slot, valid, S, lane);
   lds_sync();
   float acc[4], wsum[4];
   int rows[4];
@@ -695,7 +716,7 @@ __device__ __forceinline__ void scatter_grid_grad_uniform(float* __restrict__ gr
   }
   int cur = -1;
   for (int t = 0; t < 32; ++t) {
-    const int cell = __builtin_amdgcn_readfirstlane(S.crow[t * 8]);  // corner 0 = the cell, always in range
+    const int cell = __builtin_amdgcn_readfirstlane(S.ccell[t]);
     if (cell != cur) {
       if (cur >= 0) {
 #pragma unroll
@@ -728,18 +749,12 @@ __device__ __forceinline__ void scatter_grid_grad_uniform(float* __restrict__ gr
 // flush wave-instruction is one 128-B row segment.  Kept for the register-starved weight-gradient
 // kernels, where the uniform variant above coincided with an illegal-address fault in the fine
 // decoder's kernel (both runs of tests/test_gpu_parity.py eval fine, r1k and r1l).
-__device__ __forceinline__ void scatter_grid_grad_halves(float* __restrict__ grad, const Corners& cr,
-                                                         const f32x16& dc, bool valid, const Scratch& S, int lane) {
+__device__ __forceinline__ void scatter_grid_grad_halves(float* __restrict__ grad, const int32_t* __restrict__ slot,
+                                                         const Corners& cr, const f32x16& dc, bool valid,
+                                                         const Scratch& S, int lane) {
   const int h = lane >> 5, ch = lane & 31;
   tstore(S.sA, dc, lane);
-  if (h == 0) {
-    const int p = lane & 31;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      S.crow[p * 8 + k] = cr.row[k];
-      S.cw[p * 8 + k] = valid ? cr.w[k] : 0.f;
-    }
-  }
+  stage_corners(cr, slot, valid, S, lane);
   lds_sync();
   float acc[8], wsum[8];
   int rows[8];
@@ -752,7 +767,7 @@ __device__ __forceinline__ void scatter_grid_grad_halves(float* __restrict__ gra
   int cur = -1;
   for (int t = 0; t < 16; ++t) {
     const int pp = 16 * h + t;
-    const int cell = S.crow[pp * 8];
+    const int cell = S.ccell[pp];
     if (cell != cur) {
       if (cur >= 0) {
 #pragma unroll
@@ -935,7 +950,7 @@ __global__ __launch_bounds__(256) void k_occ_combine(float* __restrict__ raw, co
 // tiles over pre-zeroed slabs) and k_slab_reduce sums the slabs in a fixed order
 // (deterministic).  LDS holds only each wave's transpose scratch: LDS float atomics
 // (ds_add_f32, one RMW per lane) were the bottleneck of the previous shared-accumulator design.
-constexpr int kScratchFloats = 2 * TILE_FLOATS + 32 * 4 + 32 * 3 + 32 * 8 * 2;
+constexpr int kScratchFloats = 2 * TILE_FLOATS + 32 * 4 + 32 * 3 + 32 * 8 * 2 + 32;
 constexpr int kWavesBwd = 4;
 constexpr int kMaxSlabs = 4096;  // WG == 2 above this many tiles
 
@@ -1010,9 +1025,9 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
   PHASE(DEC, 12);
   if (gr.grad) {
     if (WG)
-      scatter_grid_grad_halves(gr.grad, cr, dc, q.valid, S, lane);
+      scatter_grid_grad_halves(gr.grad, gr.slot, cr, dc, q.valid, S, lane);
     else
-      scatter_grid_grad_uniform(gr.grad, cr, dc, q.valid, S, lane);
+      scatter_grid_grad_uniform(gr.grad, gr.slot, cr, dc, q.valid, S, lane);
   }
   PHASE(DEC, 13);
   if (PG) {
@@ -1031,7 +1046,7 @@ __global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd(QueryKArgs a, flo
                                                                  int acc_floats) {
   // per-wave scratch: the scatter needs sA + corner rows/weights; weight gradients add sX and
   // the per-point tables (sizing LDS per variant keeps the lean kernels at 5+ waves/SIMD)
-  constexpr int kScr = WG ? kScratchFloats : TILE_FLOATS + 32 * 8 * 2;
+  constexpr int kScr = WG ? kScratchFloats : TILE_FLOATS + 32 * 8 * 2 + 32;
   __shared__ __attribute__((aligned(16))) float lds[kWavesBwd * kScr];
   const int lane = threadIdx.x & 63, wave = wave_id();
   float* sc = lds + wave * kScr;
@@ -1047,6 +1062,7 @@ __global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd(QueryKArgs a, flo
     S.crow = reinterpret_cast<int*>(sc + TILE_FLOATS);
   }
   S.cw = reinterpret_cast<float*>(S.crow + 32 * 8);
+  S.ccell = reinterpret_cast<int*>(S.cw + 32 * 8);
   const int64_t ntiles = (a.n + 31) / 32;
   const int64_t w = (int64_t)blockIdx.x * kWavesBwd + wave;
   const Slab A = make_slab(WG ? slab + (size_t)w * acc_floats : slab, WG ? acc_floats : 0);

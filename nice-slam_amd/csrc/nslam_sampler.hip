@@ -243,4 +243,4 @@ extern "C" const char* nslam_strerror(int code) {
   }
 }
 
-extern "C" int nslam_abi_version(void) { return 5; }
+extern "C" int nslam_abi_version(void) { return 6; }

@@ -94,13 +94,20 @@ class SparseGradExchange:
 
     def plan(self, keys, dnames):
         """(flat row list, [(decoder grad, offset)], payload buffer) for the grids in `keys` and
-        the decoders `dnames` (cached per stage)."""
+        the decoders `dnames` (cached per stage).  An engine with frustum-compacted gradients
+        (engine.rows) already holds exactly the rows to exchange: its compact grid gradients
+        join the decoder gradients as plain copies (row list empty)."""
         k = (tuple(keys), tuple(dnames))
         if k not in self._plan:
-            rl = [self.rows[g] for g in keys if g in self.rows]
             dev = self.engine.gbuf.device
+            compact = [g for g in keys if g in getattr(self.engine, "rows", {})]
+            rl = [self.rows[g] for g in keys if g in self.rows and g not in compact]
             rows = torch.cat(rl) if rl else torch.zeros(0, dtype=torch.int32, device=dev)
             tails, off = [], rows.numel() * 32
+            for g in compact:
+                t = self.engine.ggrad[g]
+                tails.append((t, off))
+                off += t.numel()
             for n in dnames:
                 g = self.engine.decs[n].grad
                 tails.append((g, off))
@@ -114,14 +121,16 @@ class SparseGradExchange:
     def __call__(self, keys, dnames):
         rows, tails, buf = self.plan(keys, dnames)
         gbuf = self.engine.gbuf
-        self.pack(gbuf, rows, None, buf)
+        if rows.numel():
+            self.pack(gbuf, rows, None, buf)
         for g, off in tails:
-            self.pack(None, None, g, buf[off:off + g.numel()])
+            self.pack(None, None, g.reshape(-1), buf[off:off + g.numel()])
         if dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1:
             dist.all_reduce(buf, group=self.group)
-        self.unpack(buf, rows, gbuf, None)
+        if rows.numel():
+            self.unpack(buf, rows, gbuf, None)
         for g, off in tails:
-            self.unpack(buf[off:off + g.numel()], None, None, g)
+            self.unpack(buf[off:off + g.numel()], None, None, g.reshape(-1))
 
 
 def optimizer_params(opt):

@@ -67,7 +67,8 @@ class MappingEngine:
     """Fused mapping iterations over shared grids `c` (dict of [1,32,Z,Y,X] channels-last grids)
     and a NICE decoder stack, for the stage schedule of Mapper.optimize_map."""
 
-    def __init__(self, nice, c, bound, n_strat, n_surf, lindisp=False, w_color=0.2, device="cuda", grid_grads=True):
+    def __init__(self, nice, c, bound, n_strat, n_surf, lindisp=False, w_color=0.2, device="cuda", grid_grads=True,
+                 rows=None):
         self.nice, self.c, self.bound = nice, c, bound
         self.n_strat, self.n_surf, self.lindisp, self.w_color = n_strat, n_surf, lindisp, w_color
         self.device = torch.device(device)
@@ -78,17 +79,42 @@ class MappingEngine:
         self._saved = None  # ReLU masks of the last query_fwd (read by query_bwd)
         self._side = []     # side streams of the concurrent decoder backward
         self.concurrent = True
-        # one flat gradient buffer for every grid: zeroing is a single memset
-        sizes = {k: v.numel() if grid_grads else 0 for k, v in c.items()}
-        self.gbuf = torch.zeros(sum(sizes.values()), dtype=torch.float32, device=self.device)
-        self.ggrad, off = {}, 0
+        self.priority = False  # concurrent: run the weight-gradient branch on a high-priority stream
+        self._hi = None
         for k, v in c.items():
             if not v.is_contiguous(memory_format=torch.channels_last_3d):
                 raise ValueError(f"{k} must be channels-last (ops.channels_last)")
-            if not grid_grads:  # tracking: grids are constants (Tracker.py:138-141)
+        self.grid_grads = grid_grads
+        self.set_rows(rows)
+
+    def set_rows(self, rows):
+        """Grid-gradient layout.  rows=None: dense gradients (one flat buffer for every grid, so
+        zeroing is a single memset).  rows={grid key: int32 voxel rows} (the frustum selection of
+        Mapper.py:314-333, the FusedAdam group "rows"): those grids accumulate a COMPACT gradient
+        [n_rows][32] in row-list order through a voxel→slot map (ABI v6 nslam_grid.slot); the
+        scatter skips every other voxel, whose gradient the reference never forms (it optimises
+        the masked vector, Mapper.py:394-401).  Adam then reads the compact rows directly and the
+        ray-sharded exchange all-reduces them as they are."""
+        c = self.c
+        self.rows = dict(rows) if rows else {}
+        self.slot = {}
+        sizes = {}
+        for k, v in c.items():
+            sizes[k] = 0 if not self.grid_grads else (self.rows[k].numel() * 32 if k in self.rows else v.numel())
+        self.gbuf = torch.zeros(sum(sizes.values()), dtype=torch.float32, device=self.device)
+        self.ggrad, off = {}, 0
+        for k, v in c.items():
+            if not self.grid_grads:  # tracking: grids are constants (Tracker.py:138-141)
                 continue
             Z, Y, X = v.shape[2:]
-            self.ggrad[k] = self.gbuf[off:off + sizes[k]].view(1, Z, Y, X, 32).permute(0, 4, 1, 2, 3)
+            if k in self.rows:
+                r = self.rows[k]
+                slot = torch.full((Z * Y * X,), -1, dtype=torch.int32, device=self.device)
+                slot[r.long()] = torch.arange(r.numel(), dtype=torch.int32, device=self.device)
+                self.slot[k] = slot
+                self.ggrad[k] = self.gbuf[off:off + sizes[k]].view(-1, 32)
+            else:
+                self.ggrad[k] = self.gbuf[off:off + sizes[k]].view(1, Z, Y, X, 32).permute(0, 4, 1, 2, 3)
             off += sizes[k]
 
     # -- query in ray form ---------------------------------------------------------------------
@@ -96,10 +122,11 @@ class MappingEngine:
         decs = ops._DEC_FOR_STAGE[stage]
         meta = ops.QueryMeta(stage, decs, {n: self.decs[n].packer for n in decs},
                              {n: self.dec_bounds[n] for n in decs}, self.oob, None)
-        pairs = [(None, None)] * 4
+        pairs = [(None, None, None)] * 4
         for n in decs:
             key = _GRID_OF[n]
-            pairs[ops._DEC_ID[n]] = (self.c[key], self.ggrad[key] if key in grid_grads else None)
+            gg = key in grid_grads
+            pairs[ops._DEC_ID[n]] = (self.c[key], self.ggrad[key] if gg else None, self.slot.get(key) if gg else None)
         packed = {n: self.decs[n].packed for n in decs}
         dg = {n: self.decs[n].grad for n in decs if n in dec_grads}
         cfg = ops._fill_cfg(meta, pairs, packed, dg, False)
@@ -135,8 +162,12 @@ class MappingEngine:
         if concurrent:
             while len(self._side) < len(decs) - 1:
                 self._side.append(torch.cuda.Stream(z.device))
+            if self.priority:  # the critical (MFMA-heavy) branch gets its waves dispatched first
+                if self._hi is None:
+                    self._hi = torch.cuda.Stream(z.device, priority=-1)
+                streams = [self._hi]
             streams += self._side[:len(decs) - 1]
-        used = streams[1:]
+        used = [st for st in streams if st is not main]
         gp = [torch.empty(n, 3, dtype=torch.float64, device=z.device) for _ in decs] if pts_grad else None
         with ops._span("query_bwd"):
             for st in used:  # fork: every branch starts from the same point of the main stream

@@ -164,9 +164,11 @@ def _fill_cfg(meta, grids, packed, dgrads, need_pts_grad):
         cfg.bound_lo[k], cfg.bound_hi[k] = lo[k], hi[k]
     for name in meta.decs:
         d = _DEC_ID[name]
-        g, gg = grids[d]
+        g, gg = grids[d][:2]
+        slot = grids[d][2] if len(grids[d]) > 2 else None
         cfg.grid[d].data = g.data_ptr()
         cfg.grid[d].grad = gg.data_ptr() if gg is not None else None
+        cfg.grid[d].slot = slot.data_ptr() if slot is not None else None
         cfg.grid[d].dims[0], cfg.grid[d].dims[1], cfg.grid[d].dims[2] = g.shape[2], g.shape[3], g.shape[4]
         blo, bhi = meta.dec_bounds[name]
         for k in range(3):
@@ -533,10 +535,16 @@ class FusedAdam:
                 s.param, s.grad = ptr(p.data), ptr(gr)
                 s.exp_avg, s.exp_avg_sq, s.step = ptr(st["exp_avg"]), ptr(st["exp_avg_sq"]), ptr(st["step"])
                 if rows is not None:
+                    # grad: dense like the grid, or compact [n_rows][32] in row-list order (engine
+                    # frustum-compacted gradients, ABI v6)
+                    compact = gr.dim() == 2
+                    if compact and not (gr.is_contiguous() and gr.shape == (rows.numel(), p.shape[1])):
+                        raise ValueError("compact grid gradient must be [n_rows, 32] contiguous")
                     if not (p.is_contiguous(memory_format=torch.channels_last_3d) and
-                            gr.is_contiguous(memory_format=torch.channels_last_3d)):
+                            (compact or gr.is_contiguous(memory_format=torch.channels_last_3d))):
                         raise ValueError("row-masked Adam needs channels-last grid and grad")
                     s.rows, s.n, s.row_len = ptr(rows), rows.numel(), p.shape[1]
+                    s.grad_rows = int(compact)
                 else:  # elementwise over storage: any dense layout shared by param, grad and state
                     dense = p.is_contiguous() or p.is_contiguous(memory_format=torch.channels_last_3d)
                     if not (dense and gr.stride() == p.stride() and st["exp_avg"].stride() == p.stride()):

@@ -167,3 +167,43 @@ def test_sparse_exchange_sums_frustum_rows_only(tmp_path):
         assert torch.equal(after[m], total_g[m])          # frustum rows: summed over ranks
         assert torch.equal(after[~m], before[~m])         # other rows: untouched
         assert torch.equal(r[k]["after_d"], r[0]["before_d"] + r[1]["before_d"])
+
+
+def _compact_exchange_worker(rank, world, port, out_path):
+    """Engine with frustum-compacted gradients (engine.rows set): the compact [n_rows, 32] grid
+    gradients and the decoder gradients are summed over ranks as they are."""
+    import sys
+    sys.path.insert(0, REPO)
+    import importlib
+    from types import SimpleNamespace
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    D = importlib.import_module("nice-slam_amd").distributed
+    g = torch.Generator().manual_seed(200 + rank)
+    rows = {"grid_middle": torch.tensor([0, 7, 59], dtype=torch.int32),
+            "grid_fine": torch.tensor([1, 2, 3, 100, 209], dtype=torch.int32)}
+    gbuf = torch.randn(8 * 32, generator=g)
+    eng = SimpleNamespace(c={"grid_middle": None, "grid_fine": None}, gbuf=gbuf, rows=rows,
+                          ggrad={"grid_middle": gbuf[:96].view(-1, 32), "grid_fine": gbuf[96:].view(-1, 32)},
+                          decs={"color": SimpleNamespace(grad=torch.randn(11, generator=g))})
+    before_g, before_d = gbuf.clone(), eng.decs["color"].grad.clone()
+    ex = D.SparseGradExchange.__new__(D.SparseGradExchange)
+    ex.engine, ex.group, ex.rows, ex._plan = eng, None, {}, {}
+    ex.pack, ex.unpack = _torch_rows_pack, _torch_rows_unpack
+    keys = ("grid_middle", "grid_fine")
+    ex(keys, ("color",))
+    torch.save({"before_g": before_g, "before_d": before_d, "after_g": gbuf, "after_d": eng.decs["color"].grad,
+                "bytes": ex.payload_bytes(keys, ("color",))}, f"{out_path}.{rank}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_compact_exchange_sums_compact_rows(tmp_path):
+    out = str(tmp_path / "cx")
+    mp.spawn(_compact_exchange_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    r = [torch.load(f"{out}.{k}") for k in range(2)]
+    assert r[0]["bytes"] == (8 * 32 + 11) * 4
+    for k in range(2):
+        assert torch.equal(r[k]["after_g"], r[0]["before_g"] + r[1]["before_g"])
+        assert torch.equal(r[k]["after_d"], r[0]["before_d"] + r[1]["before_d"])

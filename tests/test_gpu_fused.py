@@ -218,6 +218,37 @@ def test_engine_iteration_matches_autograd_path(tiny):
     assert rel_l2(eng.decs["color"].grad, ref) < 1e-5
 
 
+def test_engine_compact_gradients_match_dense(tiny):
+    """Frustum-compacted grid gradients (engine rows → voxel slot map, ABI v6) == the dense
+    gradients on the selected rows, and the row-masked Adam over them updates the grids like the
+    dense path (Mapper.py:314-333,394-401: only the masked vector is optimised)."""
+    sc, frames = _frames(tiny)
+    pix = torch.randint(96 * 128, (3 * 150,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(12))
+    keys = ("grid_middle", "grid_fine", "grid_color")
+    out = {}
+    for compact in (False, True):
+        nice, c = _nice(sc)
+        g = torch.Generator(device=DEV).manual_seed(3)
+        rows = {k: torch.nonzero(torch.rand(c[k].shape[2:].numel(), device=DEV, generator=g) < 0.4)
+                .reshape(-1).to(torch.int32) for k in keys}
+        eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV, rows=rows if compact else None)
+        opt = P.ops.FusedAdam([{"params": [eng.decs["color"].param], "lr": 0.005}] +
+                              [{"params": [c[k]], "lr": 0.005, "rows": rows[k]} for k in keys])
+        eng.iteration("color", frames, pix, 150, (96, 128), (sc.fx, sc.fy, sc.cx, sc.cy), opt)
+        gr = {}
+        for k in keys:
+            gg = eng.ggrad[k]
+            gr[k] = gg.clone() if compact else gg.permute(0, 2, 3, 4, 1).reshape(-1, 32)[rows[k].long()].clone()
+        out[compact] = (gr, {k: c[k].detach().clone() for k in keys}, eng.decs["color"].param.detach().clone())
+        if compact:
+            assert eng.gbuf.numel() == sum(r.numel() for r in rows.values()) * 32
+    for k in keys:
+        assert float(out[False][0][k].abs().sum()) > 0, k
+        assert rel_l2(out[True][0][k], out[False][0][k]) < 1e-6, k
+        assert rel_l2(out[True][1][k], out[False][1][k]) < 1e-6, k
+    assert rel_l2(out[True][2], out[False][2]) < 1e-6
+
+
 def test_engine_loss_decreases(tiny):
     sc, frames = _frames(tiny)
     nice, c = _nice(sc)

@@ -1,0 +1,72 @@
+"""Grid-gradient scatter statistics of the room0 colour-stage mapping batch: per grid, how many
+corner contributions a 32-point tile issues (8 per point), how many remain after merging runs of
+identical cells (what the kernels do), after merging identical corner rows per tile, and how
+many fall on frustum-selected rows (the only rows Adam reads, Mapper.py:314-333).
+
+python tools/probes/scatter_stats.py   (on the GPU box)
+"""
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, REPO)
+import bench  # noqa: E402
+
+
+def corners(pts, lo, hi, dims):
+    """channels-last row of the 8 trilinear corners of each point (align_corners=True, border)."""
+    Z, Y, X = dims
+    n = (pts - lo) / (hi - lo) * 2 - 1
+    sz = torch.tensor([X - 1, Y - 1, Z - 1], dtype=pts.dtype, device=pts.device)
+    f = ((n + 1) / 2 * sz).clamp(min=0)
+    f = torch.minimum(f, sz)
+    i0 = f.floor().long()
+    i0 = torch.minimum(i0, (sz - 1).long().clamp(min=0))
+    rows = []
+    for dz in (0, 1):
+        for dy in (0, 1):
+            for dx in (0, 1):
+                x, y, z = i0[:, 0] + dx, i0[:, 1] + dy, i0[:, 2] + dz
+                rows.append((z * Y + y) * X + x)
+    return torch.stack(rows, 1), (i0[:, 2] * Y + i0[:, 1]) * X + i0[:, 0]
+
+
+def main():
+    dev = torch.device("cuda:0")
+    P = bench.pkg()
+    sc = bench.Room0Scene(dev, 0, path="fused")
+    cfg = sc.cfg
+    F, H, W = cfg["window"], cfg["H"], cfg["W"]
+    n = cfg["pixels"] // F
+    pix = torch.randint(H * W, (F * n,), device=dev)
+    ro, rd, gd, gc, keep = P.ops.gather_rays(sc.frames, pix, n, H, W, (0, H, 0, W), cfg["fx"], cfg["fy"], cfg["cx"],
+                                             cfg["cy"], sc.bound)
+    z = P.ops.sample_z(ro, rd, gd, sc.bound, 32, 16)
+    pts = (ro.double()[:, None] + rd.double()[:, None] * z[..., None]).reshape(-1, 3)
+    kept = keep.bool().repeat_interleave(48)
+    lo, hi = sc.bound[:, 0].to(dev), sc.bound[:, 1].to(dev)
+    for key in ("grid_middle", "grid_fine", "grid_color"):
+        dims = sc.grids[key].shape[2:]
+        rows, cell = corners(pts, lo, hi, dims)
+        m = torch.zeros(dims[0] * dims[1] * dims[2], dtype=torch.bool, device=dev)
+        m[sc.rows[key].long()] = True
+        T = rows.shape[0] // 32
+        rt, ct, kt = rows[:T * 32].view(T, 32, 8), cell[:T * 32].view(T, 32), kept[:T * 32].view(T, 32)
+        total = int(kt.sum()) * 8
+        new_run = torch.ones_like(ct, dtype=torch.bool)
+        new_run[:, 1:] = ct[:, 1:] != ct[:, :-1]
+        runs = int((new_run & kt).sum()) * 8
+        uniq = 0
+        for t in range(0, T, 1):
+            r = rt[t][kt[t]].reshape(-1)
+            uniq += int(torch.unique(r).numel())
+        inmask = int((m[rt.reshape(-1)].view(T, 32, 8) & kt[..., None]).sum())
+        print(f"{key:12s} dims {tuple(dims)} frustum rows {int(m.sum())}/{m.numel()}  corner contributions {total}  "
+              f"after run-merge {runs} ({runs / total:.2f})  unique rows per tile {uniq} ({uniq / total:.2f})  "
+              f"on frustum rows {inmask} ({inmask / total:.2f})", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,58 @@
+"""Mapping-iteration time (hipGraph replay) under engine variants: sequential / concurrent decoder
+backward, with or without a high-priority stream for the weight-gradient branch.
+
+python tools/probes/step_variants.py   (on the GPU box)
+"""
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, REPO)
+import bench  # noqa: E402
+
+
+def graph_ms(fn, reps=100):
+    for _ in range(3):
+        fn()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        fn()
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        fn()
+    g.replay()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        g.replay()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps * 1e3
+
+
+def main():
+    dev = torch.device("cuda:0")
+    P = bench.pkg()
+    sc = bench.Room0Scene(dev, 0, path="fused")
+    eng = sc.engine
+    variants = [("sequential", False, False), ("concurrent", True, False), ("concurrent+priority", True, True)]
+    for rnd in range(2):
+        for name, conc, prio in variants:
+            eng.concurrent, eng.priority = conc, prio
+            us = graph_ms(lambda: sc.step())
+            P.ops.TIMER = P.ops.KernelTimer()
+            for _ in range(20):
+                sc.step()
+            t = P.ops.TIMER.summary()
+            P.ops.TIMER = None
+            ks = " ".join(f"{k}={v['avg_ms'] * 1e3:.0f}" for k, v in t.items() if k.startswith("query_bwd"))
+            print(f"[{rnd}] {name:22s} step {us:7.1f} us   eager: {ks}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
