@@ -162,6 +162,8 @@ class Room0Scene:
                                       cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"])
             self.rows[k] = P.engine.frustum_rows(m)
         self.path = path
+        self.kept = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.rank = rank
         if path == "fused":
             for t in self.grids.values():
                 t.requires_grad_(False)
@@ -195,20 +197,20 @@ class Room0Scene:
         return rays_o, rays_d, depth, color
 
     def step(self, stage="color", sharded=False):
-        """One colour-stage mapping iteration, no host synchronisation (hipGraph-capturable);
-        returns the number of kept ray-samples (device tensor)."""
+        """One colour-stage mapping iteration, no host synchronisation (hipGraph-capturable).
+        Pixels are drawn inside the gather kernel (uniform over the image, like select_uv) and
+        the gather kernel adds the kept-ray count into self.kept: kept ray-samples over a run =
+        self.kept × samples per ray, read once after the timed region."""
         if self.path != "fused":
             return self.step_autograd(stage, sharded)
         cfg = self.cfg
         D = pkg().distributed
         F, H, W = cfg["window"], cfg["H"], cfg["W"]
         n = cfg["pixels"] // F
-        pix = torch.randint(H * W, (F * n,), device=self.dev)
-        _, keep = self.engine.iteration(
-            stage, self.frames, pix, n, (H, W), (cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"]), self.opt,
+        self.engine.iteration(
+            stage, self.frames, None, n, (H, W), (cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"]), self.opt,
             trainable_decoders=("color",), gt_max=(lambda g: D.global_max(g)) if sharded else None,
-            exchange=self.exchange if sharded else None)
-        return keep.sum() * (cfg["n_strat"] + cfg["n_surf"])
+            exchange=self.exchange if sharded else None, n_kept=self.kept, seed=1000 + self.rank)
 
     def step_autograd(self, stage="color", sharded=False):
         """The same iteration through the autograd drop-in path (dense Adam, torch glue ops).
@@ -239,7 +241,7 @@ class Room0Scene:
         if sharded:
             D.allreduce_grads(D.optimizer_params(self.opt))
         self.opt.step()
-        return keep.sum() * (cfg["n_strat"] + cfg["n_surf"])
+        self.kept += keep.sum()
 
 
 class _Slam:
@@ -475,29 +477,28 @@ def main():
             torch.cuda.current_stream().wait_stream(side)
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
-                g_samples = scene.step(sharded=sharded)
+                scene.step(sharded=sharded)
             graph.replay()
             torch.cuda.synchronize()
             mode = "hipgraph"
         except Exception as e:  # pragma: no cover - fall back to eager launches
             print(f"graph capture failed, eager mode: {e!r}", file=sys.stderr)
             graph = None
+    scene.kept.zero_()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    acc = torch.zeros((), dtype=torch.int64, device=dev)
     for _ in range(args.steps):
         if graph is not None:
             graph.replay()
-            acc += g_samples
         else:
-            acc += scene.step(sharded=sharded)
+            scene.step(sharded=sharded)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    samples = int(acc)
+    samples = int(scene.kept) * (cfg["n_strat"] + cfg["n_surf"])
     # per-kernel durations: HIP events around each C-ABI launch, on the launching stream, over
     # extra eager steps of the same kernels (events cannot bracket single kernels inside a replay)
     P.ops.TIMER = P.ops.KernelTimer()

@@ -94,6 +94,11 @@ typedef struct nslam_query_cfg {
    * decoders that have no parameter gradients (their backward needs only the masks).
    * nslam_query_saved_size(M) bytes; layout [decoder][tile of 32 points][layer 0..4][64] uint16. */
   uint16_t* saved_masks;
+  /* ABI v7: nslam_query_fwd_ws with defer_occ = 1 leaves raw[...,3] = the fine occupancy and the
+   * middle occupancy in ws (float [M]) instead of adding them in a separate pass: the consumer
+   * adds it on read (nslam_loss_cfg.occ_add = ws), saving a launch per query. */
+  int32_t defer_occ;
+  int32_t pad2_;
 } nslam_query_cfg;
 
 /* ---- packing ------------------------------------------------------------------------------
@@ -176,7 +181,19 @@ typedef struct nslam_frame {
   const float* c2w;   /* [3 or 4][4] float32 row-major camera-to-world */
 } nslam_frame;
 
-/* get_samples (src/common.py:92-134: get_sample_uv + select_uv + get_rays_from_uv) for
+/* In-kernel pixel draws (ABI v7): with pix == NULL and draw != NULL the select_uv indices are drawn
+ * on the device — uniform over the window, from a counter-based splitmix64 stream keyed by
+ * (seed, *counter, ray), NOT torch.randint's Philox sequence — and *counter advances by one per
+ * call (the last workgroup bumps it, stream-ordered), so a hipGraph replay draws fresh pixels
+ * without host RNG work.  ticket: device uint32, zero-initialised once, reserved for the call. */
+typedef struct nslam_draw {
+  uint64_t seed;
+  uint64_t* counter;
+  uint32_t* ticket;
+} nslam_draw;
+
+/* n_kept (ABI v7, device int64, may be NULL) is incremented by the number of kept rays.
+ * get_samples (src/common.py:92-134: get_sample_uv + select_uv + get_rays_from_uv) for
  * n_frames frames (HOST array, <= NSLAM_MAX_FRAMES) x n_per pixels each, plus the inside-mask
  * prefilter of Mapper.py:469-481 / Tracker.py:93-104.  pix[f*n_per + k] is select_uv's randint
  * index into the frame's window [h0,h1) x [w0,w1) (row-major over the window).  Outputs are
@@ -186,7 +203,8 @@ typedef struct nslam_frame {
 int nslam_gather_rays(const nslam_frame* frames, int32_t n_frames, int64_t n_per, const int64_t* pix,
                       int32_t H, int32_t W, int32_t h0, int32_t h1, int32_t w0, int32_t w1, float fx, float fy,
                       float cx, float cy, const double* bound_lo, const double* bound_hi, float* rays_o,
-                      float* rays_d, float* gt_depth, float* gt_color, uint8_t* keep, void* stream);
+                      float* rays_d, float* gt_depth, float* gt_color, uint8_t* keep, const struct nslam_draw* draw,
+                      int64_t* n_kept, void* stream);
 
 /* Rendering loss fused with compositing and its backward (the loss is a sum of per-ray terms).
  *   mode NSLAM_LOSS_MAPPER (Mapper.py:487-501):
@@ -204,6 +222,8 @@ typedef struct nslam_loss_cfg {
   int32_t use_color;
   int32_t handle_dynamic;
   float w_color;
+  const float* occ_add; /* ABI v7: NULL, or [N*S] float added to raw[...,3] on read (the middle
+                           occupancy of a deferred-combine query, decoder.py:331-334 order) */
 } nslam_loss_cfg;
 int nslam_render_loss(const nslam_loss_cfg* cfg, const float* raw, const double* z_vals, int64_t n_rays,
                       int32_t n_samples, const float* gt_depth, const float* gt_color, const uint8_t* keep,
@@ -236,6 +256,11 @@ typedef struct nslam_adam_seg {
   int32_t grad_rows; /* ABI v6, row-masked segments: 1 = grad is compact [n][row_len] in row-list order
                         (the frustum-compacted gradient of nslam_grid.slot); 0 = grad is dense like param */
   int32_t pad_;
+  /* ABI v7, dense segments: after the update param[e] is also stored to mirror[mirror_idx[2e]] and
+   * mirror[mirror_idx[2e+1]] (-1 = none): the MFMA-packed copy of a decoder (nslam_pack_layout)
+   * stays current without a re-pack pass.  mirror == NULL: no mirror. */
+  const int32_t* mirror_idx;
+  float* mirror;
 } nslam_adam_seg;
 int nslam_adam_step(const nslam_adam_seg* segs, int32_t n_segs, float beta1, float beta2, float eps,
                     int32_t zero_grad, uint32_t* ticket, void* stream);

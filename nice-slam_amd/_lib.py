@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NSLAM_LIB") or os.path.join(_HERE, "libnslam.so")  # NSLAM_LIB: instrumented builds
 
 NSLAM_OK = 0
-ABI_VERSION = 6
+ABI_VERSION = 7
 STAGES = {"coarse": 0, "middle": 1, "fine": 2, "color": 3}
 DEC_COARSE, DEC_MIDDLE, DEC_FINE, DEC_COLOR = 0, 1, 2, 3
 
@@ -61,6 +61,8 @@ class NslamQueryCfg(ctypes.Structure):
         ("z_vals", ctypes.c_void_p),
         ("n_samples", ctypes.c_int64),
         ("saved_masks", ctypes.c_void_p),
+        ("defer_occ", ctypes.c_int32),  # ABI v7
+        ("pad2_", ctypes.c_int32),
     ]
 
 
@@ -75,7 +77,11 @@ class NslamFrame(ctypes.Structure):
 
 class NslamLossCfg(ctypes.Structure):
     _fields_ = [("mode", ctypes.c_int32), ("use_color", ctypes.c_int32), ("handle_dynamic", ctypes.c_int32),
-                ("w_color", ctypes.c_float)]
+                ("w_color", ctypes.c_float), ("occ_add", ctypes.c_void_p)]
+
+
+class NslamDraw(ctypes.Structure):  # ABI v7 in-kernel pixel draws
+    _fields_ = [("seed", ctypes.c_uint64), ("counter", ctypes.c_void_p), ("ticket", ctypes.c_void_p)]
 
 
 class NslamAdamSeg(ctypes.Structure):
@@ -91,6 +97,8 @@ class NslamAdamSeg(ctypes.Structure):
         ("lr", ctypes.c_float),
         ("grad_rows", ctypes.c_int32),  # ABI v6: compact [n][row_len] gradient of a row-masked segment
         ("pad_", ctypes.c_int32),
+        ("mirror_idx", ctypes.c_void_p),  # ABI v7: packed-copy slots [n][2] of a dense segment
+        ("mirror", ctypes.c_void_p),
     ]
 
 
@@ -142,7 +150,7 @@ def lib():
         L.nslam_abi_version.restype = ctypes.c_int
         f32 = ctypes.c_float
         L.nslam_gather_rays.argtypes = [ctypes.POINTER(NslamFrame), i32, i64, vp, i32, i32, i32, i32, i32, i32,
-                                        f32, f32, f32, f32, dp, dp, vp, vp, vp, vp, vp, vp]
+                                        f32, f32, f32, f32, dp, dp, vp, vp, vp, vp, vp, ctypes.POINTER(NslamDraw), vp, vp]
         L.nslam_render_loss.argtypes = [ctypes.POINTER(NslamLossCfg), vp, vp, i64, i32, vp, vp, vp, vp, vp, vp, vp,
                                         vp, vp, sz, vp]
         L.nslam_render_loss_workspace_size.argtypes = [ctypes.POINTER(NslamLossCfg), i64]

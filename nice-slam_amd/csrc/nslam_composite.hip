@@ -54,11 +54,14 @@ struct RaySample {
 };
 
 // Fill chunk `c` of a ray: alpha, factor, exclusive transmittance, weight.  carry = T entering.
+// occ (may be NULL): the middle occupancy of a deferred-combine query, added to raw[...,3] in the
+// reference's operand order (fine + middle, decoder.py:331-334) — what k_occ_combine would store.
 __device__ __forceinline__ RaySample load_sample(const float* raw, const double* z, int S, int k, int lane,
-                                                 float& carry) {
+                                                 float& carry, const float* occ = nullptr) {
   RaySample s;
   const bool act = k < S;
   s.raw = act ? *reinterpret_cast<const f32x4*>(raw + (size_t)k * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+  if (occ && act) s.raw[3] = s.raw[3] + occ[k];
   s.z = act ? z[k] : 0.0;
   s.a = act ? sigmoid10(s.raw[3]) : 0.f;
   s.f = act ? (1.f - s.a) + 1e-10f : 1.f;
@@ -179,13 +182,13 @@ struct RayOut {
 };
 
 __device__ __forceinline__ RayOut ray_fwd(const float* rr, const double* zz, int S, int nch, RaySample (&sm)[kMaxS / 64],
-                                          int lane) {
+                                          int lane, const float* occ = nullptr) {
   float carry = 1.f;
   RayOut o{0.0, 0.0, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int c = 0; c < kMaxS / 64; ++c) {
     if (c >= nch) break;
-    sm[c] = load_sample(rr, zz, S, c * 64 + lane, lane, carry);
+    sm[c] = load_sample(rr, zz, S, c * 64 + lane, lane, carry, occ);
     o.c0 += sm[c].w * sm[c].raw[0];
     o.c1 += sm[c].w * sm[c].raw[1];
     o.c2 += sm[c].w * sm[c].raw[2];
@@ -267,7 +270,7 @@ __global__ __launch_bounds__(256) void k_render_loss(LossArgs a) {
   const double* zz = a.z + ray * (int64_t)S;
   const int nch = (S + 63) / 64;
   RaySample sm[kMaxS / 64];
-  const RayOut o = ray_fwd(rr, zz, S, nch, sm, lane);
+  const RayOut o = ray_fwd(rr, zz, S, nch, sm, lane, a.cfg.occ_add ? a.cfg.occ_add + ray * (int64_t)S : nullptr);
   const bool kp = a.keep ? a.keep[ray] != 0 : true;
   const float gt = a.gt[ray];
   if (PASS != 2 && lane == 0) {

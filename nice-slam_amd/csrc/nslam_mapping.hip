@@ -29,18 +29,61 @@ struct GatherArgs {
   double lo[3], hi[3];
   float *ro, *rd, *gd, *gc;
   uint8_t* keep;
+  nslam_draw draw;  // pix == NULL: in-kernel draws
+  int64_t wn;       // window size (h1-h0)*(w1-w0)
+  int64_t* n_kept;
 };
+
+// splitmix64 finaliser: a counter-based stream (seed, draw counter, ray) -> 64 uniform bits
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+  x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+  return x ^ (x >> 31);
+}
 
 // torch.max / torch.min propagate NaN
 __device__ __forceinline__ double nanmax(double a, double b) { return (a > b || a != a) ? a : b; }
 __device__ __forceinline__ double nanmin(double a, double b) { return (a < b || a != a) ? a : b; }
 
+__device__ bool gather_one(const GatherArgs& a, int64_t ray, int64_t kpix, uint64_t ctr);
+
 __global__ __launch_bounds__(256) void k_gather_rays(GatherArgs a) {
   const int64_t ray = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (ray >= a.n) return;
+  __shared__ uint64_t ctr;
+  __shared__ int wkept[4];
+  if (a.pix && threadIdx.x == 0) ctr = 0;
+  if (!a.pix) {  // in-kernel draws: every workgroup reads the counter before the last one bumps it
+    if (threadIdx.x == 0) ctr = __hip_atomic_load(a.draw.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      // the read above completed (its value is in LDS); count this workgroup in, last one advances
+      const uint32_t t = __hip_atomic_fetch_add(a.draw.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == gridDim.x - 1) {
+        __hip_atomic_store(a.draw.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(a.draw.counter, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  bool kp = false;
+  if (ray < a.n) kp = gather_one(a, ray, a.pix ? a.pix[ray] : 0, ctr);
+  if (a.n_kept) {  // kept-ray count: wave ballot, one atomic per workgroup
+    const int cnt = __popcll(__ballot(kp));
+    if ((threadIdx.x & 63) == 0) wkept[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int tot = wkept[0] + wkept[1] + wkept[2] + wkept[3];
+      if (tot) atomicAdd(reinterpret_cast<unsigned long long*>(a.n_kept), (unsigned long long)tot);
+    }
+  }
+}
+
+__device__ bool gather_one(const GatherArgs& a, int64_t ray, int64_t kpix, uint64_t ctr) {
   const int f = (int)(ray / a.n_per);
   const nslam_frame fr = a.fr[f];
-  const int64_t k = a.pix[ray];
+  // drawn: Lemire's multiply-shift maps 32 uniform bits onto [0, wn) (bias < wn / 2^32)
+  const int64_t k = a.pix ? kpix
+                          : (int64_t)(((mix64(a.draw.seed ^ mix64(ctr * 0x9e3779b97f4a7c15ull + (uint64_t)ray)) >> 32) *
+                                       (uint64_t)a.wn) >> 32);
   // window index -> (row, col); torch.linspace(W0, W1-1, W1-W0) holds exact integers
   const int64_t r = k / a.ww, c = k - r * a.ww;
   const int64_t px = (a.h0 + r) * a.W + (a.w0 + c);
@@ -81,6 +124,7 @@ __global__ __launch_bounds__(256) void k_gather_rays(GatherArgs a) {
   }
   a.gd[ray] = gt;
   if (a.keep) a.keep[ray] = kp ? 1 : 0;
+  return kp;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -139,6 +183,11 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam(AdamArgs a) {
       sg.exp_avg[e] = m;
       sg.exp_avg_sq[e] = v;
       if (a.zero_grad) sg.grad[e] = 0.f;
+      if (sg.mirror) {  // the packed MFMA copy of this parameter (up to two slots)
+        const int i0 = sg.mirror_idx[2 * e], i1 = sg.mirror_idx[2 * e + 1];
+        if (i0 >= 0) sg.mirror[i0] = p;
+        if (i1 >= 0) sg.mirror[i1] = p;
+      }
     }
   } else {
     const int q = sg.row_len / 4;                 // float4 per row
@@ -239,13 +288,14 @@ extern "C" int nslam_gather_rays(const nslam_frame* frames, int32_t n_frames, in
                                  int32_t H, int32_t W, int32_t h0, int32_t h1, int32_t w0, int32_t w1, float fx,
                                  float fy, float cx, float cy, const double* bound_lo, const double* bound_hi,
                                  float* rays_o, float* rays_d, float* gt_depth, float* gt_color, uint8_t* keep,
-                                 void* stream) {
+                                 const nslam_draw* draw, int64_t* n_kept, void* stream) {
   if (!frames || n_frames <= 0 || n_frames > NSLAM_MAX_FRAMES || n_per < 0) return NSLAM_EINVAL;
   if (H <= 0 || W <= 0 || h0 < 0 || w0 < 0 || h1 > H || w1 > W || h1 <= h0 || w1 <= w0) return NSLAM_EINVAL;
   if ((bound_lo == nullptr) != (bound_hi == nullptr)) return NSLAM_EINVAL;
   const int64_t n = (int64_t)n_frames * n_per;
   if (n == 0) return NSLAM_OK;
-  if (!pix || !rays_o || !rays_d || !gt_depth || !gt_color) return NSLAM_EINVAL;
+  if ((!pix && !draw) || !rays_o || !rays_d || !gt_depth || !gt_color) return NSLAM_EINVAL;
+  if (!pix && (!draw->counter || !draw->ticket)) return NSLAM_EINVAL;
   GatherArgs a{};
   for (int f = 0; f < n_frames; ++f) {
     if (!frames[f].depth || !frames[f].color || !frames[f].c2w) return NSLAM_EINVAL;
@@ -272,6 +322,9 @@ extern "C" int nslam_gather_rays(const nslam_frame* frames, int32_t n_frames, in
   a.gd = gt_depth;
   a.gc = gt_color;
   a.keep = keep;
+  if (!pix) a.draw = *draw;
+  a.wn = (int64_t)(h1 - h0) * (w1 - w0);
+  a.n_kept = n_kept;
   hipLaunchKernelGGL(k_gather_rays, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), a);
   return hip_status();

@@ -1178,7 +1178,8 @@ extern "C" int nslam_query_fwd_ws(const nslam_query_cfg* cfg, const double* pts,
     hipLaunchKernelGGL(k_query_fwd_parts<NSLAM_STAGE_FINE>, dim3((unsigned)(groups * 2)), dim3(256), 0, s, a, occ);
   else
     hipLaunchKernelGGL(k_query_fwd_parts<NSLAM_STAGE_COLOR>, dim3((unsigned)(groups * 3)), dim3(256), 0, s, a, occ);
-  hipLaunchKernelGGL(k_occ_combine, dim3((unsigned)((n_pts + 255) / 256)), dim3(256), 0, s, raw, occ, n_pts);
+  if (!cfg->defer_occ)  // else the consumer adds ws on read (nslam_loss_cfg.occ_add)
+    hipLaunchKernelGGL(k_occ_combine, dim3((unsigned)((n_pts + 255) / 256)), dim3(256), 0, s, raw, occ, n_pts);
   return hip_status();
 }
 

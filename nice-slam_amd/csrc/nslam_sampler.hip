@@ -48,8 +48,14 @@ struct SamplerArgs {
   int s1;
   int lindisp;
   double* z;
-  const uint32_t* ws;
+  const uint32_t* ws;    // max_batch(gt) as an order-preserving key (large batches)
+  const float* gmax_ptr; // max_batch(gt) given by the caller (ray-sharded job: all-reduced)
+  int local_max;         // small batch: every workgroup of k_sample_wave reduces gt itself
 };
+
+// Batches up to this many rays reduce max(gt) inside k_sample_wave (each workgroup re-reads the
+// whole gt vector, <= 32 KiB from L2) instead of a memset + k_max_gt launch ahead of it.
+constexpr int64_t kLocalMaxRays = 8192;
 
 __global__ __launch_bounds__(128) void k_sample(SamplerArgs a) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -132,6 +138,15 @@ __global__ __launch_bounds__(128) void k_sample(SamplerArgs a) {
 __global__ __launch_bounds__(256) void k_sample_wave(SamplerArgs a) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + wave_id();
+  __shared__ uint32_t wmax[4];
+  if (a.local_max) {  // workgroup-wide max over the batch (all threads take part before any exit)
+    uint32_t m = 0;
+    for (int64_t i = threadIdx.x; i < a.n; i += 256) m = max(m, fkey(a.gt[i]));
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
+    if (lane == 0) wmax[wave_id()] = m;
+    __syncthreads();
+  }
   if (r >= a.n) return;
   double tmin = 0.0;
 #pragma unroll
@@ -150,7 +165,12 @@ __global__ __launch_bounds__(256) void k_sample_wave(SamplerArgs a) {
   double far = far_bb;
   if (has_gt) {
     g = a.gt[r];
-    gmax = fkey_inv(*a.ws);
+    if (a.gmax_ptr)
+      gmax = *a.gmax_ptr;
+    else if (a.local_max)
+      gmax = fkey_inv(max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3])));
+    else
+      gmax = fkey_inv(*a.ws);
     near_f = g * 0.01f;
     const double hi = (double)(gmax * 1.2f);
     far = far_bb < 0.0 ? 0.0 : far_bb;
@@ -219,14 +239,21 @@ extern "C" int nslam_sample_rays(const float* rays_o, const float* rays_d, const
   a.lindisp = lindisp;
   a.z = z_vals;
   a.ws = reinterpret_cast<const uint32_t*>(ws);
-  if (gt_depth && gt_max) {
+  const bool wave_form = s0 + (gt_depth ? s1 : 0) <= 64;
+  a.gmax_ptr = nullptr;
+  a.local_max = 0;
+  if (gt_depth && gt_max && wave_form) {
+    a.gmax_ptr = gt_max;
+  } else if (gt_depth && wave_form && n_rays <= kLocalMaxRays) {
+    a.local_max = 1;
+  } else if (gt_depth && gt_max) {
     hipLaunchKernelGGL(k_key_of, dim3(1), dim3(1), 0, s, gt_max, reinterpret_cast<uint32_t*>(ws));
   } else if (gt_depth) {
     if (hipMemsetAsync(ws, 0, 4, s) != hipSuccess) return hip_status();
     const int blocks = (int)std::min<int64_t>((n_rays + 255) / 256, 1024);
     hipLaunchKernelGGL(k_max_gt, dim3(blocks), dim3(256), 0, s, gt_depth, n_rays, reinterpret_cast<uint32_t*>(ws));
   }
-  if (s0 + (gt_depth ? s1 : 0) <= 64)
+  if (wave_form)
     hipLaunchKernelGGL(k_sample_wave, dim3((unsigned)((n_rays + 3) / 4)), dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL(k_sample, dim3((unsigned)((n_rays + 127) / 128)), dim3(128), 0, s, a);
@@ -243,4 +270,4 @@ extern "C" const char* nslam_strerror(int code) {
   }
 }
 
-extern "C" int nslam_abi_version(void) { return 6; }
+extern "C" int nslam_abi_version(void) { return 7; }

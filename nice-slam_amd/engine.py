@@ -23,6 +23,7 @@ from __future__ import annotations
 import ctypes
 import math
 
+import numpy as np
 import torch
 
 from . import _lib, ops
@@ -57,6 +58,18 @@ class FlatDecoder:
         self.grad = torch.zeros(n, dtype=torch.float32, device=dev)
         self.packed = torch.empty(self.packer.index.shape[0], dtype=torch.float32, device=dev)
         self.idx = self.packer.device_index(dev)
+        # inverse of the packing gather: the (at most two) packed slots of each parameter, so Adam
+        # can store an updated parameter straight into the packed copy (FusedAdam.set_mirror)
+        idx = self.packer.index
+        slots = np.full((n, 2), -1, dtype=np.int32)
+        pos = np.nonzero(idx >= 0)[0]
+        order = np.argsort(idx[pos], kind="stable")
+        src, dst = idx[pos][order], pos[order]
+        first = np.ones(src.size, dtype=bool)
+        first[1:] = src[1:] != src[:-1]
+        slots[src[first], 0] = dst[first]
+        slots[src[~first], 1] = dst[~first]
+        self.mirror_idx = torch.from_numpy(slots).to(dev)
         self.repack()
 
     def repack(self):
@@ -77,6 +90,8 @@ class MappingEngine:
         self.dec_bounds = {n: ops._bound_list(nice.decoder(n).bound) for n in names}
         self.oob = ops._bound_list(bound)
         self._saved = None  # ReLU masks of the last query_fwd (read by query_bwd)
+        self.occ_add = None  # middle occupancy of the last deferred-combine query_fwd
+        self._draws = None   # (seed, ops.PixelDraws) of in-kernel pixel draws
         self._side = []     # side streams of the concurrent decoder backward
         self.concurrent = True
         self.priority = False  # concurrent: run the weight-gradient branch on a high-priority stream
@@ -102,6 +117,7 @@ class MappingEngine:
         for k, v in c.items():
             sizes[k] = 0 if not self.grid_grads else (self.rows[k].numel() * 32 if k in self.rows else v.numel())
         self.gbuf = torch.zeros(sum(sizes.values()), dtype=torch.float32, device=self.device)
+        self._clean = False  # every gradient the next iteration accumulates into is known zero
         self.ggrad, off = {}, 0
         for k, v in c.items():
             if not self.grid_grads:  # tracking: grids are constants (Tracker.py:138-141)
@@ -134,13 +150,15 @@ class MappingEngine:
         cfg.saved_masks = ptr(self._saved)
         return cfg
 
-    def query_fwd(self, stage, ro, rd, z):
-        """raw [N*S, 4]; also saves the ReLU masks the backward of frozen decoders uses."""
+    def query_fwd(self, stage, ro, rd, z, defer_occ=False):
+        """raw [N*S, 4]; also saves the ReLU masks the backward of frozen decoders uses.
+        defer_occ: raw[...,3] holds the fine occupancy only and self.occ_add the middle one (None
+        when the stage has a single occupancy decoder) — render_loss(occ_add=...) adds it."""
         n = z.numel()
         raw = torch.empty(n, 4, dtype=torch.float32, device=z.device)
         self._saved = torch.empty(lib().nslam_query_saved_size(n), dtype=torch.uint8, device=z.device)
         cfg = self._cfg(stage, ro, rd, z, (), ())
-        ops.query_fwd_launch(cfg, None, n, raw)
+        self.occ_add = ops.query_fwd_launch(cfg, None, n, raw, defer_occ=defer_occ)
         return raw
 
     def query_bwd(self, stage, ro, rd, z, g_raw, grid_grads, dec_grads, concurrent=None, pts_grad=False):
@@ -153,6 +171,7 @@ class MappingEngine:
         decoder writes its share into its own buffer (so the branches stay independent) and the
         shares are summed afterwards."""
         n = z.numel()
+        self._clean = False
         concurrent = self.concurrent if concurrent is None else concurrent
         cfg = self._cfg(stage, ro, rd, z, grid_grads, dec_grads)
         cfg.need_pts_grad = int(bool(pts_grad))
@@ -210,11 +229,13 @@ class MappingEngine:
         return g
 
     def iteration(self, stage, frames, pix, n_per, hw, intrinsics, optimizer, trainable_decoders=("color",),
-                  gt_max=None, allreduce=None, use_gt_in_sampler=True, exchange=None):
+                  gt_max=None, allreduce=None, use_gt_in_sampler=True, exchange=None, n_kept=None, seed=0):
         """One mapping iteration; returns (ray_loss f64 [N], keep uint8 [N]) as device tensors.
 
         frames: [(depth, color, c2w)] of the window; pix: int64 [len(frames)*n_per] randint
-        indices over the full image; hw = (H, W); intrinsics = (fx, fy, cx, cy).
+        indices over the full image, or None: drawn in the gather kernel (ops.PixelDraws keyed by
+        `seed`, advanced on the device — no host RNG work per hipGraph replay); hw = (H, W);
+        intrinsics = (fx, fy, cx, cy); n_kept: optional device int64 [1] += kept rays.
         gt_max: callable(gt_depth) → device scalar for a ray-sharded job (all-reduced max);
         allreduce: callable(list of grads) run before Adam (ray sharding, dense);
         exchange: callable(grid keys, decoder names) run before Adam instead — the frustum-compacted
@@ -222,26 +243,44 @@ class MappingEngine:
         """
         H, W = hw
         fx, fy, cx, cy = intrinsics
-        ro, rd, gd, gc, keep = ops.gather_rays(frames, pix, n_per, H, W, (0, H, 0, W), fx, fy, cx, cy, self.bound)
+        draw = None
+        if pix is None:
+            if self._draws is None or self._draws[0] != seed:
+                self._draws = (seed, ops.PixelDraws(seed, self.device))
+            draw = self._draws[1]
+        ro, rd, gd, gc, keep = ops.gather_rays(frames, pix, n_per, H, W, (0, H, 0, W), fx, fy, cx, cy, self.bound,
+                                               draw=draw, n_kept=n_kept)
         gsamp = gd if (use_gt_in_sampler and stage != "coarse") else None
         gm = gt_max(gd) if (gt_max is not None and gsamp is not None) else None
         z = ops.sample_z(ro, rd, gsamp, self.bound, self.n_strat, self.n_surf, self.lindisp, gt_max=gm)
-        raw = self.query_fwd(stage, ro, rd, z)
+        raw = self.query_fwd(stage, ro, rd, z, defer_occ=True)
         _, _, _, ray_loss, g_raw = ops.render_loss(raw, z, gd, gc, keep, mode="mapper", use_color=stage == "color",
-                                                   w_color=self.w_color)
+                                                   w_color=self.w_color, occ_add=self.occ_add)
         keys, dnames = self.grads_for(stage, trainable_decoders)
-        self.gbuf.zero_()
-        for n in dnames:
-            self.decs[n].grad.zero_()
+        if not self._clean:
+            self.gbuf.zero_()
+            for n in self.decs.values():
+                n.grad.zero_()
         self.query_bwd(stage, ro, rd, z, g_raw, keys, dnames)
         grads = self.adam_grads(stage, trainable_decoders)
         if exchange is not None:  # frustum-compacted all-reduce (distributed.SparseGradExchange)
             exchange(keys, dnames)
         elif allreduce is not None:  # the grid gradients as one flat buffer, plus the decoder gradients
             allreduce([self.gbuf] + [self.decs[n].grad for n in dnames])
-        optimizer.step(grads=grads)
-        for n in dnames:
-            self.decs[n].repack()
+        # Adam resets every gradient entry it reads.  With compact gradients for every grid of the
+        # stage that is every entry the backward wrote, so the next iteration needs no memsets.
+        clean = all(k in self.rows for k in keys)
+        mirror = hasattr(optimizer, "set_mirror")
+        if mirror:  # Adam stores updated decoder parameters straight into their packed copies
+            for n in dnames:
+                d = self.decs[n]
+                if d.param not in optimizer.mirrors:
+                    optimizer.set_mirror(d.param, d.mirror_idx, d.packed)
+        optimizer.step(grads=grads, zero_grad=clean)
+        self._clean = clean
+        if not mirror:
+            for n in dnames:
+                self.decs[n].repack()
         return ray_loss, keep
 
 

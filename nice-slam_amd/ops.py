@@ -343,18 +343,27 @@ class _GridSample(torch.autograd.Function):
 SPLIT_FWD = True  # decoder-parallel forward (nslam_query_fwd_ws); False: one wave runs every decoder
 
 
-def query_fwd_launch(cfg, pts, n, raw, split=None):
-    """nslam_query_fwd_ws (decoder-parallel) or nslam_query_fwd (one fused chain per wave)."""
+def query_fwd_launch(cfg, pts, n, raw, split=None, defer_occ=False):
+    """nslam_query_fwd_ws (decoder-parallel) or nslam_query_fwd (one fused chain per wave).
+
+    defer_occ: leave raw[...,3] = the fine occupancy and return the middle occupancy [n] float
+    (or None when the stage has no split) for render_loss(occ_add=...) to add on read."""
     split = SPLIT_FWD if split is None else split
     wsb = lib().nslam_query_fwd_workspace_size(ctypes.byref(cfg), n) if split else 0
+    occ = None
     with _span("query_fwd"):
         if wsb:
             ws = torch.empty(wsb, dtype=torch.uint8, device=raw.device)
+            cfg.defer_occ = int(bool(defer_occ))
             rc = lib().nslam_query_fwd_ws(ctypes.byref(cfg), ptr(pts), n, ptr(raw), ptr(ws), wsb,
                                           stream_ptr(raw.device))
+            cfg.defer_occ = 0
+            if defer_occ:
+                occ = ws[:n * 4].view(torch.float32)
         else:
             rc = lib().nslam_query_fwd(ctypes.byref(cfg), ptr(pts), n, ptr(raw), stream_ptr(raw.device))
     check(rc, "nslam_query_fwd")
+    return occ
 
 
 def grid_sample_fwd(grid, coords, out):
@@ -387,7 +396,7 @@ def grid_sample(grid, coords):
 # ----------------------------------------------------------------------------------------------
 # fused mapping / tracking iteration (ABI v4): pixel gather, render loss, ray-form query, Adam
 # ----------------------------------------------------------------------------------------------
-def gather_rays(frames, pix, n_per, H, W, window, fx, fy, cx, cy, bound=None):
+def gather_rays(frames, pix, n_per, H, W, window, fx, fy, cx, cy, bound=None, draw=None, n_kept=None):
     """get_samples (src/common.py:92-134) for every frame of a window in one launch, plus the
     inside-mask prefilter (Mapper.py:469-481) when `bound` is given.
 
@@ -395,11 +404,15 @@ def gather_rays(frames, pix, n_per, H, W, window, fx, fy, cx, cy, bound=None):
     pix: int64 [len(frames)*n_per] select_uv randint indices into each frame's window
     (h0, h1, w0, w1).  Returns rays_o, rays_d [N,3] f32, gt_depth [N] f32 (0 for dropped rays),
     gt_color [N,3] f32, keep [N] uint8.
+    pix=None: draw the pixels on the device (`draw`: PixelDraws, ABI v7); n_kept: optional device
+    int64 [1] incremented by the number of kept rays.
     """
     nf = len(frames)
     if nf == 0 or nf > _lib.MAX_FRAMES:
         raise ValueError(f"1..{_lib.MAX_FRAMES} frames, got {nf}")
-    dev = pix.device
+    if pix is None and draw is None:
+        raise ValueError("pix or draw")
+    dev = pix.device if pix is not None else draw.counter.device
     arr = (_lib.NslamFrame * nf)()
     keepalive = []
     for f, (d, c, m) in enumerate(frames):
@@ -410,7 +423,8 @@ def gather_rays(frames, pix, n_per, H, W, window, fx, fy, cx, cy, bound=None):
             raise ValueError("frame tensors must be depth [H,W], color [H,W,3], c2w [3|4,4]")
         keepalive += [d, c, m]
         arr[f].depth, arr[f].color, arr[f].c2w = ptr(d), ptr(c), ptr(m)
-    pix = pix.to(torch.int64).contiguous()
+    if pix is not None:
+        pix = pix.to(torch.int64).contiguous()
     n = nf * n_per
     ro = torch.empty(n, 3, dtype=torch.float32, device=dev)
     rd = torch.empty(n, 3, dtype=torch.float32, device=dev)
@@ -425,13 +439,27 @@ def gather_rays(frames, pix, n_per, H, W, window, fx, fy, cx, cy, bound=None):
         blo = bhi = None
     with _span("gather_rays"):
         rc = lib().nslam_gather_rays(arr, nf, n_per, ptr(pix), H, W, h0, h1, w0, w1, fx, fy, cx, cy, blo, bhi,
-                                     ptr(ro), ptr(rd), ptr(gd), ptr(gc), ptr(keep), stream_ptr(dev))
+                                     ptr(ro), ptr(rd), ptr(gd), ptr(gc), ptr(keep),
+                                     ctypes.byref(draw.struct) if (pix is None) else None,
+                                     ptr(n_kept) if n_kept is not None else None, stream_ptr(dev))
     check(rc, "nslam_gather_rays")
     return ro, rd, gd, gc, keep
 
 
+class PixelDraws:
+    """Device state of in-kernel pixel draws (nslam_draw, ABI v7): a seed and a device draw
+    counter the gather kernel advances itself — no host RNG work per (graph-replayed) call.
+    Uniform over the window like select_uv's torch.randint (common.py:113-134), but a different
+    stream (counter-based splitmix64), so draws do not reproduce torch's sequence."""
+
+    def __init__(self, seed, device):
+        self.counter = torch.zeros(1, dtype=torch.int64, device=device)
+        self.ticket = torch.zeros(1, dtype=torch.int32, device=device)
+        self.struct = _lib.NslamDraw(int(seed) & (2 ** 64 - 1), ptr(self.counter), ptr(self.ticket))
+
+
 def render_loss(raw, z, gt_depth, gt_color, keep=None, mode="mapper", use_color=True, handle_dynamic=False,
-                w_color=0.2, want_grad=True):
+                w_color=0.2, want_grad=True, occ_add=None):
     """Mapper/Tracker rendering loss fused with compositing and its backward (see nslam.h).
 
     raw [N,S,4] (or [N*S,4]) f32, z [N,S] f64.  Returns (depth f64 [N], var f64 [N],
@@ -443,7 +471,7 @@ def render_loss(raw, z, gt_depth, gt_color, keep=None, mode="mapper", use_color=
     dev = z.device
     raw = raw.detach().float().contiguous()
     cfg = _lib.NslamLossCfg(_lib.LOSS_MAPPER if mode == "mapper" else _lib.LOSS_TRACKER, int(bool(use_color)),
-                            int(bool(handle_dynamic)), float(w_color))
+                            int(bool(handle_dynamic)), float(w_color), ptr(occ_add) if occ_add is not None else None)
     depth = torch.empty(n, dtype=torch.float64, device=dev)
     var = torch.empty(n, dtype=torch.float64, device=dev)
     color = torch.empty(n, 3, dtype=torch.float32, device=dev)
@@ -509,6 +537,14 @@ class FusedAdam:
                 dev = p.device
         self.device = dev
         self.ticket = torch.zeros(1, dtype=torch.int32, device=dev) if dev is not None else None
+        self.mirrors = {}
+
+    def set_mirror(self, p, idx, dst):
+        """After each update also store dense parameter p into dst at idx ([p.numel(), 2] int32,
+        -1 = none): keeps a decoder's MFMA-packed copy current inside the Adam launch."""
+        if idx.shape != (p.numel(), 2) or idx.dtype != torch.int32 or not idx.is_contiguous():
+            raise ValueError("mirror index must be int32 [numel, 2]")
+        self.mirrors[p] = (idx, dst)
 
     def _st(self, p, rows):
         st = self.state.get(p)
@@ -550,6 +586,9 @@ class FusedAdam:
                     if not (dense and gr.stride() == p.stride() and st["exp_avg"].stride() == p.stride()):
                         raise ValueError("dense Adam segments need param, grad and state of one dense layout")
                     s.rows, s.n, s.row_len = None, p.numel(), 0
+                    mi = self.mirrors.get(p)
+                    if mi is not None:
+                        s.mirror_idx, s.mirror = ptr(mi[0]), ptr(mi[1])
                 s.lr = float(g["lr"])
                 segs.append((s, p, gr))
         return segs

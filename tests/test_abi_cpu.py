@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_strerror(pkg):
     L = pkg._lib.lib()
-    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 6
+    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 7
     assert L.nslam_strerror(0) == b"ok"
     assert b"invalid" in L.nslam_strerror(-1)
 
@@ -73,7 +73,8 @@ def test_struct_layouts_match_header(pkg, tmp_path):
     mirrors in _lib.py."""
     L = pkg._lib
     structs = {"nslam_grid": L.NslamGrid, "nslam_dec_grad": L.NslamDecGrad, "nslam_query_cfg": L.NslamQueryCfg,
-               "nslam_frame": L.NslamFrame, "nslam_loss_cfg": L.NslamLossCfg, "nslam_adam_seg": L.NslamAdamSeg}
+               "nslam_frame": L.NslamFrame, "nslam_loss_cfg": L.NslamLossCfg, "nslam_adam_seg": L.NslamAdamSeg,
+               "nslam_draw": L.NslamDraw}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "nslam.h"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'  printf("{cname} size %zu\\n", sizeof({cname}));')
@@ -97,9 +98,16 @@ def test_v4_entry_points_validate_without_gpu(pkg):
     lib = pkg._lib
     fr = (lib.NslamFrame * 1)()
     assert L.nslam_gather_rays(fr, 0, 10, None, 10, 10, 0, 10, 0, 10, 1.0, 1.0, 0.0, 0.0, None, None,
-                               None, None, None, None, None, None) == -1
+                               None, None, None, None, None, None, None, None) == -1
     assert L.nslam_gather_rays(fr, 1, 10, None, 10, 10, 0, 11, 0, 10, 1.0, 1.0, 0.0, 0.0, None, None,
-                               None, None, None, None, None, None) == -1
+                               None, None, None, None, None, None, None, None) == -1
+    # ABI v7: neither pix nor draws, and draws without device counter/ticket, are rejected
+    fr[0].depth = fr[0].color = fr[0].c2w = 64
+    assert L.nslam_gather_rays(fr, 1, 10, None, 10, 10, 0, 10, 0, 10, 1.0, 1.0, 0.0, 0.0, None, None,
+                               64, 64, 64, 64, None, None, None, None) == -1
+    draw = lib.NslamDraw(7, None, None)
+    assert L.nslam_gather_rays(fr, 1, 10, None, 10, 10, 0, 10, 0, 10, 1.0, 1.0, 0.0, 0.0, None, None,
+                               64, 64, 64, 64, None, ctypes.byref(draw), None, None) == -1
     cfg = lib.NslamLossCfg(5, 0, 0, 0.2)
     assert L.nslam_render_loss(ctypes.byref(cfg), None, None, 4, 48, None, None, None, None, None, None, None,
                                None, None, 0, None) == -1

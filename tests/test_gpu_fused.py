@@ -234,11 +234,16 @@ def test_engine_compact_gradients_match_dense(tiny):
         eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV, rows=rows if compact else None)
         opt = P.ops.FusedAdam([{"params": [eng.decs["color"].param], "lr": 0.005}] +
                               [{"params": [c[k]], "lr": 0.005, "rows": rows[k]} for k in keys])
-        eng.iteration("color", frames, pix, 150, (96, 128), (sc.fx, sc.fy, sc.cx, sc.cy), opt)
         gr = {}
-        for k in keys:
-            gg = eng.ggrad[k]
-            gr[k] = gg.clone() if compact else gg.permute(0, 2, 3, 4, 1).reshape(-1, 32)[rows[k].long()].clone()
+
+        def snapshot(ks, dn):  # runs where the ray-sharded exchange would: after backward, before Adam
+            for k in keys:
+                gg = eng.ggrad[k]
+                gr[k] = gg.clone() if compact else gg.permute(0, 2, 3, 4, 1).reshape(-1, 32)[rows[k].long()].clone()
+
+        eng.iteration("color", frames, pix, 150, (96, 128), (sc.fx, sc.fy, sc.cx, sc.cy), opt, exchange=snapshot)
+        if compact:  # Adam consumed (zeroed) the compact gradients: the next iteration needs no memset
+            assert float(eng.gbuf.abs().sum()) == 0.0
         out[compact] = (gr, {k: c[k].detach().clone() for k in keys}, eng.decs["color"].param.detach().clone())
         if compact:
             assert eng.gbuf.numel() == sum(r.numel() for r in rows.values()) * 32
@@ -387,3 +392,84 @@ def test_tracker_track_frame_fused_matches_loop(tiny):
         pre[:3, 3] += 0.02
         outs.append(tr.track_frame(1, sc.color.cuda(), sc.depth.cuda(), c2w, pre_c2w=pre))
     assert torch.allclose(outs[0], outs[1], atol=5e-4), (outs[0] - outs[1]).abs().max()
+
+
+def test_sampler_batch_max_paths_agree(tiny):
+    """The sampler's batch-global max(gt_depth) (Renderer.py:107-111,144) three ways — reduced
+    inside the sampling kernel (small batches), by a separate k_max_gt pass (large batches) and
+    given by the caller (ray sharding) — yields bit-identical z_vals."""
+    sc, frames = _frames(tiny)
+    g = torch.Generator(device=DEV).manual_seed(21)
+    for n in (700, 9000):
+        ro = (sc.bound[:, 0] + 0.5 * (sc.bound[:, 1] - sc.bound[:, 0])).float().to(DEV).expand(n, 3).contiguous()
+        rd = torch.randn(n, 3, device=DEV, generator=g)
+        gd = torch.rand(n, device=DEV, generator=g) * 2.0
+        gd[::7] = 0.0
+        z0 = P.ops.sample_z(ro, rd, gd, sc.bound, 32, 16)
+        z1 = P.ops.sample_z(ro, rd, gd, sc.bound, 32, 16, gt_max=gd.max().reshape(1))
+        assert torch.equal(z0, z1), n
+        # a shard given the full batch's max samples exactly as the full batch does
+        zs = P.ops.sample_z(ro[:100], rd[:100], gd[:100], sc.bound, 32, 16, gt_max=gd.max().reshape(1))
+        assert torch.equal(zs, z0[:100]), n
+
+
+def _mix64(x):
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xbf58476d1ce4e5b9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94d049bb133111eb)
+    return x ^ (x >> np.uint64(31))
+
+
+def _drawn_pix(seed, ctr, n, wn):
+    """Host restatement of nslam_gather_rays' in-kernel draws (ABI v7, splitmix64 + Lemire)."""
+    with np.errstate(over="ignore"):
+        r = np.arange(n, dtype=np.uint64)
+        h = _mix64(np.uint64(seed) ^ _mix64(np.uint64(ctr) * np.uint64(0x9e3779b97f4a7c15) + r))
+        return ((h >> np.uint64(32)) * np.uint64(wn)) >> np.uint64(32)
+
+
+@pytest.mark.parametrize("window", [(0, 96, 0, 128), (20, 76, 20, 108)])
+def test_gather_rays_device_draws(tiny, window):
+    """pix=None draws select_uv's indices inside the kernel: the rays equal an explicit-pix gather of
+    the host-restated draws bit for bit, the counter advances once per call, n_kept counts keep."""
+    sc, frames = _frames(tiny)
+    H, W = 96, 128
+    h0, h1, w0, w1 = window
+    wn = (h1 - h0) * (w1 - w0)
+    n_per = 700
+    draw = P.ops.PixelDraws(1234, DEV)
+    kept = torch.zeros(1, dtype=torch.int64, device=DEV)
+    seen = []
+    for call in range(3):
+        out = P.ops.gather_rays(frames, None, n_per, H, W, window, sc.fx, sc.fy, sc.cx, sc.cy, sc.bound,
+                                draw=draw, n_kept=kept)
+        assert int(draw.counter) == call + 1
+        pix = torch.from_numpy(_drawn_pix(1234, call, len(frames) * n_per, wn).astype(np.int64)).to(DEV)
+        ref = P.ops.gather_rays(frames, pix, n_per, H, W, window, sc.fx, sc.fy, sc.cx, sc.cy, sc.bound)
+        for a, b in zip(out, ref):
+            assert torch.equal(a, b)
+        seen.append(pix)
+        assert int(draw.ticket) == 0
+    assert int(kept) == sum(int(P.ops.gather_rays(frames, p, n_per, H, W, window, sc.fx, sc.fy, sc.cx, sc.cy,
+                                                      sc.bound)[4].sum()) for p in seen)
+    allp = torch.cat(seen).cpu().numpy()
+    assert allp.min() >= 0 and allp.max() < wn
+    # uniform over the window: each quarter of the window index range gets 25% +- 3%
+    q = np.bincount(allp * 4 // wn, minlength=4) / allp.size
+    assert np.all(np.abs(q - 0.25) < 0.03), q
+
+
+def test_adam_mirror_keeps_packed_copy_current(tiny):
+    """FusedAdam.set_mirror: the engine's packed decoder copy after Adam equals a fresh repack."""
+    sc, frames = _frames(tiny)
+    nice, c = _nice(sc)
+    eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV)
+    opt = P.ops.FusedAdam([{"params": [eng.decs["color"].param], "lr": 0.005}] +
+                          [{"params": [c[k]], "lr": 0.005} for k in ("grid_middle", "grid_fine", "grid_color")])
+    pix = torch.randint(96 * 128, (3 * 150,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(3))
+    for _ in range(2):
+        eng.iteration("color", frames, pix, 150, (96, 128), (sc.fx, sc.fy, sc.cx, sc.cy), opt)
+    d = eng.decs["color"]
+    assert d.param in opt.mirrors
+    got = d.packed.clone()
+    d.repack()
+    assert torch.equal(got, d.packed)

@@ -6,7 +6,8 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 marks = [i for i, r in enumerate(rows) if "k_gather_rays" in r["Kernel_Name"]]
-i0, i1 = (marks[-3], marks[-2]) if len(marks) >= 3 else (0, len(rows))
+back = int(sys.argv[2]) if len(sys.argv) > 2 else 3   # which iteration, counted from the end
+i0, i1 = (marks[-back], marks[-back + 1]) if len(marks) >= back else (0, len(rows))
 t0 = int(rows[i0]["Start_Timestamp"])
 end = t0
 busy = []
