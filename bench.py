@@ -204,13 +204,16 @@ class Room0Scene:
         if self.path != "fused":
             return self.step_autograd(stage, sharded)
         cfg = self.cfg
-        D = pkg().distributed
         F, H, W = cfg["window"], cfg["H"], cfg["W"]
         n = cfg["pixels"] // F
+        # ray-sharded: one global batch of pixels * world draws (same seed on every rank), each rank
+        # gathering its slice; the gather kernel also yields the global batch's max(gt_depth), so
+        # the only collective of the iteration is the gradient exchange
+        world = int(os.environ.get("WORLD_SIZE", "1")) if sharded else 1
         self.engine.iteration(
             stage, self.frames, None, n, (H, W), (cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"]), self.opt,
-            trainable_decoders=("color",), gt_max=(lambda g: D.global_max(g)) if sharded else None,
-            exchange=self.exchange if sharded else None, n_kept=self.kept, seed=1000 + self.rank)
+            trainable_decoders=("color",), exchange=self.exchange if sharded else None, n_kept=self.kept,
+            seed=1000, world=world, rank=self.rank if sharded else 0)
 
     def step_autograd(self, stage="color", sharded=False):
         """The same iteration through the autograd drop-in path (dense Adam, torch glue ops).

@@ -190,6 +190,17 @@ typedef struct nslam_draw {
   uint64_t seed;
   uint64_t* counter;
   uint32_t* ticket;
+  /* Ray sharding without a collective (world > 1; world = 1, rank = 0: a single rank).  The
+   * global batch holds n_per * world pixels per frame, drawn from ONE stream (every rank passes
+   * the same seed); this call's ray (f, k) is global ray f*n_per*world + rank*n_per + k.
+   * gt_max (device float, may be NULL) receives max(gt_depth) over the kept rays of the whole
+   * global batch (Renderer.py:107-111,144), which every rank evaluates itself — each thread
+   * re-draws its pixel slot for every rank — so the sampler needs no all-reduce.
+   * gt_max_key: device uint32, zero-initialised once, required with gt_max. */
+  int32_t world;
+  int32_t rank;
+  float* gt_max;
+  uint32_t* gt_max_key;
 } nslam_draw;
 
 /* n_kept (ABI v7, device int64, may be NULL) is incremented by the number of kept rays.

@@ -81,7 +81,9 @@ class NslamLossCfg(ctypes.Structure):
 
 
 class NslamDraw(ctypes.Structure):  # ABI v7 in-kernel pixel draws
-    _fields_ = [("seed", ctypes.c_uint64), ("counter", ctypes.c_void_p), ("ticket", ctypes.c_void_p)]
+    _fields_ = [("seed", ctypes.c_uint64), ("counter", ctypes.c_void_p), ("ticket", ctypes.c_void_p),
+                ("world", ctypes.c_int32), ("rank", ctypes.c_int32), ("gt_max", ctypes.c_void_p),
+                ("gt_max_key", ctypes.c_void_p)]
 
 
 class NslamAdamSeg(ctypes.Structure):

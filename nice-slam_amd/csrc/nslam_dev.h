@@ -76,6 +76,14 @@ struct NoXyzPack {  // MLP_no_xyz (decoder.py:206-274), coarse level
 // ------------------------------------------------------------------------------------------
 // MFMA tile helpers
 // ------------------------------------------------------------------------------------------
+// order-preserving float <-> uint (atomicMax over a batch of floats; key 0 is below every float)
+__device__ __forceinline__ uint32_t fkey(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float fkey_inv(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
 // Wave index inside the workgroup as a wave-uniform (SGPR) value: LLVM's divergence analysis
 // treats threadIdx.x >> 6 as divergent, which would push every tile / slab address derived from
 // it into VGPRs (and buffer resources into waterfall loops).

@@ -45,86 +45,121 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
 __device__ __forceinline__ double nanmax(double a, double b) { return (a > b || a != a) ? a : b; }
 __device__ __forceinline__ double nanmin(double a, double b) { return (a < b || a != a) ? a : b; }
 
-__device__ bool gather_one(const GatherArgs& a, int64_t ray, int64_t kpix, uint64_t ctr);
+// One pixel of frame f at window index k: rays_o/rays_d (common.py:74-89), gt depth (0 when the
+// inside mask drops the ray), the pixel offset and the mask.
+struct RayAt {
+  float o[3], d[3], gt;
+  int64_t px;
+  bool kp;
+};
 
-__global__ __launch_bounds__(256) void k_gather_rays(GatherArgs a) {
-  const int64_t ray = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  __shared__ uint64_t ctr;
-  __shared__ int wkept[4];
-  if (a.pix && threadIdx.x == 0) ctr = 0;
-  if (!a.pix) {  // in-kernel draws: every workgroup reads the counter before the last one bumps it
-    if (threadIdx.x == 0) ctr = __hip_atomic_load(a.draw.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      // the read above completed (its value is in LDS); count this workgroup in, last one advances
-      const uint32_t t = __hip_atomic_fetch_add(a.draw.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (t == gridDim.x - 1) {
-        __hip_atomic_store(a.draw.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(a.draw.counter, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
-  bool kp = false;
-  if (ray < a.n) kp = gather_one(a, ray, a.pix ? a.pix[ray] : 0, ctr);
-  if (a.n_kept) {  // kept-ray count: wave ballot, one atomic per workgroup
-    const int cnt = __popcll(__ballot(kp));
-    if ((threadIdx.x & 63) == 0) wkept[threadIdx.x >> 6] = cnt;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const int tot = wkept[0] + wkept[1] + wkept[2] + wkept[3];
-      if (tot) atomicAdd(reinterpret_cast<unsigned long long*>(a.n_kept), (unsigned long long)tot);
-    }
-  }
-}
-
-__device__ bool gather_one(const GatherArgs& a, int64_t ray, int64_t kpix, uint64_t ctr) {
-  const int f = (int)(ray / a.n_per);
-  const nslam_frame fr = a.fr[f];
-  // drawn: Lemire's multiply-shift maps 32 uniform bits onto [0, wn) (bias < wn / 2^32)
-  const int64_t k = a.pix ? kpix
-                          : (int64_t)(((mix64(a.draw.seed ^ mix64(ctr * 0x9e3779b97f4a7c15ull + (uint64_t)ray)) >> 32) *
-                                       (uint64_t)a.wn) >> 32);
+__device__ __forceinline__ RayAt ray_at(const GatherArgs& a, int f, int64_t k) {
+  const nslam_frame& fr = a.fr[f];
+  RayAt r;
   // window index -> (row, col); torch.linspace(W0, W1-1, W1-W0) holds exact integers
-  const int64_t r = k / a.ww, c = k - r * a.ww;
-  const int64_t px = (a.h0 + r) * a.W + (a.w0 + c);
-  const float i = (float)(a.w0 + c), j = (float)(a.h0 + r);
+  const int64_t row = k / a.ww, col = k - row * a.ww;
+  r.px = (a.h0 + row) * a.W + (a.w0 + col);
+  const float i = (float)(a.w0 + col), j = (float)(a.h0 + row);
   // dirs = ((i-cx)/fx, -(j-cy)/fy, -1); rays_d = sum(dirs * c2w[:3,:3], -1) (common.py:80-86).
   // On the GPU torch divides by a CPU scalar as a multiply by its float reciprocal
   // (BinaryDivTrueKernel), which is what the reference runs: do the same.
   const float d0 = (i - a.cx) * (1.f / a.fx);
   const float d1 = -(j - a.cy) * (1.f / a.fy);
   const float d2 = -1.f;
-  float o[3], d[3];
 #pragma unroll
   for (int m = 0; m < 3; ++m) {
-    const float* row = fr.c2w + 4 * m;
+    const float* c2w = fr.c2w + 4 * m;
     // torch's 3-element sum reduces as (p0 + p2) + p1 on this device (tools/probes/rays_order.py)
-    d[m] = (d0 * row[0] + d2 * row[2]) + d1 * row[1];
-    o[m] = row[3];
+    r.d[m] = (d0 * c2w[0] + d2 * c2w[2]) + d1 * c2w[1];
+    r.o[m] = c2w[3];
   }
-  float gt = fr.depth[px];
-  bool kp = true;
+  r.gt = fr.depth[r.px];
+  r.kp = true;
   if (a.use_bound) {  // t = (bound - o) / d (float64); t_exit = min_axis max(t_lo, t_hi) >= gt
     double tex = 0.0;
 #pragma unroll
     for (int m = 0; m < 3; ++m) {
-      const double tl = (a.lo[m] - (double)o[m]) / (double)d[m];
-      const double th = (a.hi[m] - (double)o[m]) / (double)d[m];
+      const double tl = (a.lo[m] - (double)r.o[m]) / (double)r.d[m];
+      const double th = (a.hi[m] - (double)r.o[m]) / (double)r.d[m];
       const double tm = nanmax(tl, th);
       tex = m == 0 ? tm : nanmin(tex, tm);
     }
-    kp = tex >= (double)gt;
+    r.kp = tex >= (double)r.gt;
   }
-  if (!kp) gt = 0.f;
+  if (!r.kp) r.gt = 0.f;
+  return r;
+}
+
+// select_uv's draw for global ray g: Lemire's multiply-shift maps 32 uniform bits onto [0, wn)
+// (bias < wn / 2^32)
+__device__ __forceinline__ int64_t draw_k(const GatherArgs& a, uint64_t ctr, uint64_t g) {
+  return (int64_t)(((mix64(a.draw.seed ^ mix64(ctr * 0x9e3779b97f4a7c15ull + g)) >> 32) * (uint64_t)a.wn) >> 32);
+}
+
+__global__ __launch_bounds__(256) void k_gather_rays(GatherArgs a) {
+  const int64_t ray = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  __shared__ uint64_t ctr;
+  __shared__ uint32_t wred[2][4];
+  const bool drawn = a.pix == nullptr;
+  if (threadIdx.x == 0)  // in-kernel draws: every workgroup reads the counter before the last one bumps it
+    ctr = drawn ? __hip_atomic_load(a.draw.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+  __syncthreads();
+  bool kp = false;
+  uint32_t mkey = 0;  // max over the global batch's kept gt (key 0: below every float)
+  if (ray < a.n) {
+    const int f = (int)(ray / a.n_per);
+    const int64_t kk = ray - (int64_t)f * a.n_per;
+    const uint64_t g0 = (uint64_t)f * (uint64_t)(a.n_per * a.draw.world) + (uint64_t)kk;  // rank 0's slot
+    const int64_t k = drawn ? draw_k(a, ctr, g0 + (uint64_t)a.draw.rank * a.n_per) : a.pix[ray];
+    const RayAt r = ray_at(a, f, k);
 #pragma unroll
-  for (int m = 0; m < 3; ++m) {
-    a.ro[ray * 3 + m] = o[m];
-    a.rd[ray * 3 + m] = d[m];
-    a.gc[ray * 3 + m] = fr.color[px * 3 + m];
+    for (int m = 0; m < 3; ++m) {
+      a.ro[ray * 3 + m] = r.o[m];
+      a.rd[ray * 3 + m] = r.d[m];
+      a.gc[ray * 3 + m] = a.fr[f].color[r.px * 3 + m];
+    }
+    a.gd[ray] = r.gt;
+    if (a.keep) a.keep[ray] = r.kp ? 1 : 0;
+    kp = r.kp;
+    if (a.draw.gt_max) {  // the other ranks' rays of this slot, re-drawn here (no collective)
+      mkey = fkey(r.gt);
+      for (int j = 0; j < a.draw.world; ++j)
+        if (j != a.draw.rank) mkey = max(mkey, fkey(ray_at(a, f, draw_k(a, ctr, g0 + (uint64_t)j * a.n_per)).gt));
+    }
   }
-  a.gd[ray] = gt;
-  if (a.keep) a.keep[ray] = kp ? 1 : 0;
-  return kp;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (a.n_kept) {  // kept-ray count: wave ballot, one atomic per workgroup
+    const int cnt = __popcll(__ballot(kp));
+    if (lane == 0) wred[0][wv] = (uint32_t)cnt;
+  }
+  if (a.draw.gt_max) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) mkey = max(mkey, (uint32_t)__shfl_xor((int)mkey, d, 64));
+    if (lane == 0) wred[1][wv] = mkey;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (a.n_kept) {
+      const uint32_t tot = wred[0][0] + wred[0][1] + wred[0][2] + wred[0][3];
+      if (tot) atomicAdd(reinterpret_cast<unsigned long long*>(a.n_kept), (unsigned long long)tot);
+    }
+    if (a.draw.gt_max)
+      __hip_atomic_fetch_max(a.draw.gt_max_key, max(max(wred[1][0], wred[1][1]), max(wred[1][2], wred[1][3])),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (drawn) {
+      // count this workgroup in (release: its max is in); the last one (acquire: sees every max)
+      // publishes the batch max, re-arms the key and ticket and advances the draw counter
+      const uint32_t t = __hip_atomic_fetch_add(a.draw.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == gridDim.x - 1) {
+        if (a.draw.gt_max) {
+          const uint32_t key = __hip_atomic_exchange(a.draw.gt_max_key, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          *a.draw.gt_max = fkey_inv(key);
+        }
+        __hip_atomic_store(a.draw.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(a.draw.counter, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -296,6 +331,8 @@ extern "C" int nslam_gather_rays(const nslam_frame* frames, int32_t n_frames, in
   if (n == 0) return NSLAM_OK;
   if ((!pix && !draw) || !rays_o || !rays_d || !gt_depth || !gt_color) return NSLAM_EINVAL;
   if (!pix && (!draw->counter || !draw->ticket)) return NSLAM_EINVAL;
+  if (!pix && (draw->world < 1 || draw->rank < 0 || draw->rank >= draw->world)) return NSLAM_EINVAL;
+  if (!pix && draw->gt_max && !draw->gt_max_key) return NSLAM_EINVAL;
   GatherArgs a{};
   for (int f = 0; f < n_frames; ++f) {
     if (!frames[f].depth || !frames[f].color || !frames[f].c2w) return NSLAM_EINVAL;
@@ -322,7 +359,12 @@ extern "C" int nslam_gather_rays(const nslam_frame* frames, int32_t n_frames, in
   a.gd = gt_depth;
   a.gc = gt_color;
   a.keep = keep;
-  if (!pix) a.draw = *draw;
+  if (!pix) {
+    a.draw = *draw;
+  } else {
+    a.draw = nslam_draw{};
+    a.draw.world = 1;
+  }
   a.wn = (int64_t)(h1 - h0) * (w1 - w0);
   a.n_kept = n_kept;
   hipLaunchKernelGGL(k_gather_rays, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,

@@ -16,15 +16,6 @@ namespace {
 
 constexpr int kMaxS0 = 128, kMaxS1 = 64;
 
-// order-preserving float <-> uint (for atomicMax over the batch)
-__device__ __forceinline__ uint32_t fkey(float f) {
-  const uint32_t u = __float_as_uint(f);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-__device__ __forceinline__ float fkey_inv(uint32_t k) {
-  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
-}
-
 __global__ void k_key_of(const float* __restrict__ gmax, uint32_t* __restrict__ ws) { *ws = fkey(*gmax); }
 
 __global__ __launch_bounds__(256) void k_max_gt(const float* __restrict__ gt, int64_t n, uint32_t* __restrict__ ws) {

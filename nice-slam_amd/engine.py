@@ -229,12 +229,16 @@ class MappingEngine:
         return g
 
     def iteration(self, stage, frames, pix, n_per, hw, intrinsics, optimizer, trainable_decoders=("color",),
-                  gt_max=None, allreduce=None, use_gt_in_sampler=True, exchange=None, n_kept=None, seed=0):
+                  gt_max=None, allreduce=None, use_gt_in_sampler=True, exchange=None, n_kept=None, seed=0,
+                  world=1, rank=0):
         """One mapping iteration; returns (ray_loss f64 [N], keep uint8 [N]) as device tensors.
 
         frames: [(depth, color, c2w)] of the window; pix: int64 [len(frames)*n_per] randint
         indices over the full image, or None: drawn in the gather kernel (ops.PixelDraws keyed by
-        `seed`, advanced on the device — no host RNG work per hipGraph replay); hw = (H, W);
+        `seed`, advanced on the device — no host RNG work per hipGraph replay; with world > 1 every
+        rank passes the same seed, gathers its slice of a global batch of n_per*world pixels per
+        frame and gets the global batch's max(gt_depth) from the gather kernel — no collective
+        before the sampler); hw = (H, W);
         intrinsics = (fx, fy, cx, cy); n_kept: optional device int64 [1] += kept rays.
         gt_max: callable(gt_depth) → device scalar for a ray-sharded job (all-reduced max);
         allreduce: callable(list of grads) run before Adam (ray sharding, dense);
@@ -245,13 +249,19 @@ class MappingEngine:
         fx, fy, cx, cy = intrinsics
         draw = None
         if pix is None:
-            if self._draws is None or self._draws[0] != seed:
-                self._draws = (seed, ops.PixelDraws(seed, self.device))
+            key = (seed, world, rank)
+            if self._draws is None or self._draws[0] != key:
+                self._draws = (key, ops.PixelDraws(seed, self.device, world, rank, with_max=world > 1))
             draw = self._draws[1]
         ro, rd, gd, gc, keep = ops.gather_rays(frames, pix, n_per, H, W, (0, H, 0, W), fx, fy, cx, cy, self.bound,
                                                draw=draw, n_kept=n_kept)
         gsamp = gd if (use_gt_in_sampler and stage != "coarse") else None
-        gm = gt_max(gd) if (gt_max is not None and gsamp is not None) else None
+        if gsamp is None:
+            gm = None
+        elif draw is not None and draw.gt_max is not None:  # global batch max from the gather kernel
+            gm = draw.gt_max
+        else:
+            gm = gt_max(gd) if gt_max is not None else None
         z = ops.sample_z(ro, rd, gsamp, self.bound, self.n_strat, self.n_surf, self.lindisp, gt_max=gm)
         raw = self.query_fwd(stage, ro, rd, z, defer_occ=True)
         _, _, _, ray_loss, g_raw = ops.render_loss(raw, z, gd, gc, keep, mode="mapper", use_color=stage == "color",

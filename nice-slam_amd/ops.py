@@ -450,12 +450,24 @@ class PixelDraws:
     """Device state of in-kernel pixel draws (nslam_draw, ABI v7): a seed and a device draw
     counter the gather kernel advances itself — no host RNG work per (graph-replayed) call.
     Uniform over the window like select_uv's torch.randint (common.py:113-134), but a different
-    stream (counter-based splitmix64), so draws do not reproduce torch's sequence."""
+    stream (counter-based splitmix64), so draws do not reproduce torch's sequence.
 
-    def __init__(self, seed, device):
+    Ray sharding (world > 1): every rank passes the same seed; the global batch holds
+    n_per * world pixels per frame and this rank gathers slots [rank*n_per, (rank+1)*n_per) of
+    each frame.  with_max: the kernel also leaves max(gt_depth) over the kept rays of the WHOLE
+    global batch in self.gt_max (each rank re-draws the other ranks' slots) — the sampler's
+    batch-global scalar (Renderer.py:107-111,144) without an all-reduce."""
+
+    def __init__(self, seed, device, world=1, rank=0, with_max=False):
+        if not (world >= 1 and 0 <= rank < world):
+            raise ValueError(f"rank {rank} of world {world}")
         self.counter = torch.zeros(1, dtype=torch.int64, device=device)
         self.ticket = torch.zeros(1, dtype=torch.int32, device=device)
-        self.struct = _lib.NslamDraw(int(seed) & (2 ** 64 - 1), ptr(self.counter), ptr(self.ticket))
+        self.world, self.rank = int(world), int(rank)
+        self.gt_max = torch.zeros(1, dtype=torch.float32, device=device) if with_max else None
+        self.key = torch.zeros(1, dtype=torch.int32, device=device) if with_max else None
+        self.struct = _lib.NslamDraw(int(seed) & (2 ** 64 - 1), ptr(self.counter), ptr(self.ticket), self.world,
+                                     self.rank, ptr(self.gt_max), ptr(self.key))
 
 
 def render_loss(raw, z, gt_depth, gt_color, keep=None, mode="mapper", use_color=True, handle_dynamic=False,

@@ -473,3 +473,28 @@ def test_adam_mirror_keeps_packed_copy_current(tiny):
     got = d.packed.clone()
     d.repack()
     assert torch.equal(got, d.packed)
+
+
+def test_sharded_draws_slice_the_global_batch(tiny):
+    """Ray sharding without a collective: rank r of `world` (same seed) gathers exactly its slice of
+    the global batch (n_per*world pixels per frame), its gather kernel reports the global batch's
+    max(gt_depth) over kept rays, and its z-values equal the global batch's (Renderer.py:107-111,144)."""
+    sc, frames = _frames(tiny)
+    H, W, n_per, world = 96, 128, 300, 3
+    args = (H, W, (0, H, 0, W), sc.fx, sc.fy, sc.cx, sc.cy, sc.bound)
+    full = P.ops.gather_rays(frames, None, n_per * world, *args, draw=P.ops.PixelDraws(77, DEV))
+    z_full = P.ops.sample_z(full[0], full[1], full[2], sc.bound, 32, 16)
+    nf = len(frames)
+    for rank in range(world):
+        dr = P.ops.PixelDraws(77, DEV, world, rank, with_max=True)
+        for it in range(2):  # the key re-arms itself: a second call reports the same max
+            out = P.ops.gather_rays(frames, None, n_per, *args, draw=dr)
+            dr.counter.zero_()
+            assert float(dr.gt_max) == float(full[2].max()), (rank, it)
+            assert int(dr.key) == 0 and int(dr.ticket) == 0
+        sl = torch.cat([torch.arange(f * n_per * world + rank * n_per, f * n_per * world + (rank + 1) * n_per)
+                        for f in range(nf)]).to(DEV)
+        for a, b in zip(out, full):
+            assert torch.equal(a, b[sl])
+        z = P.ops.sample_z(out[0], out[1], out[2], sc.bound, 32, 16, gt_max=dr.gt_max)
+        assert torch.equal(z, z_full[sl])
