@@ -34,6 +34,7 @@ ROOM0 = {
     "lr": {"decoders": 0.005, "middle": 0.005, "fine": 0.005, "color": 0.005},
 }
 FLOP_FWD_PER_SAMPLE = 2 * (15479 + 20599 + 15575)   # SURVEY §8(a10) MACs, colour stage
+FLOP_FINE_STAGE_PER_POINT = 2 * (15479 + 20599)          # fine stage: middle + fine decoders
 BYTES_FWD_PER_SAMPLE = 3 * 1024                      # 3 trilinear lookups × 8 corners × 128 B
 F32_PEAK_TFLOPS = 157.3                              # MI355X dense fp32 (MFMA = VALU rate)
 HBM_PEAK_GBS = 8000.0
@@ -318,6 +319,53 @@ def stress_grid_query(dev, side=512, rays=65536, samples=64, reps=10):
                         "samples, random rays through the cube"}
 
 
+def bulk_queries(scene, res=256, reps=2):
+    """Forward-only bulk queries through the drop-in API on the same kernels:
+    Mesher.get_mesh's grid evaluation (Mesher.py:281-319,382-433: res³ points over the bound in
+    Renderer.points_batch_size = 500k chunks, fine stage for occupancy and colour stage for the
+    vertex colours) and Renderer.render_img at room0 size (Renderer.py:200-255: H×W rays × 48
+    samples in 100k-ray batches, with the frame's depth as gt).  Timed with events on the stream."""
+    dev = scene.dev
+    nice, grids, r = scene.nice, scene.grids, scene.renderer
+    b = scene.bound
+    ax = [torch.linspace(float(b[k, 0]), float(b[k, 1]), res, dtype=torch.float64, device=dev) for k in range(3)]
+    pts = torch.stack(torch.meshgrid(*ax, indexing="ij"), -1).reshape(-1, 3)
+    out = {}
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    with torch.no_grad():
+        for stage, fl in (("fine", FLOP_FINE_STAGE_PER_POINT), ("color", FLOP_FWD_PER_SAMPLE)):
+            def mesh():
+                for i in range(0, pts.shape[0], r.points_batch_size):
+                    r.eval_points(pts[i:i + r.points_batch_size], nice, grids, stage, dev)
+            ms = timed(mesh)
+            n = pts.shape[0]
+            tf = n * fl / (ms * 1e-3) / 1e12
+            out["mesh_eval_" + stage] = {
+                "points": n, "ms": ms, "points_per_s": n / (ms * 1e-3), "flop_per_point": fl,
+                "achieved_tflops": tf, "frac_mfma_peak": tf / F32_PEAK_TFLOPS,
+                "workload": f"{res}^3 grid points over the room0 bound, eval_points in 500k-point chunks"}
+        c2w = scene.c2w[0]
+        ms = timed(lambda: r.render_img(grids, nice, c2w, dev, "color", gt_depth=scene.depth[0]))
+        n = scene.cfg["H"] * scene.cfg["W"] * (scene.cfg["n_strat"] + scene.cfg["n_surf"])
+        out["render_img"] = {"ms_per_image": ms, "ray_samples_per_s": n / (ms * 1e-3),
+                             "workload": f"{scene.cfg['H']}x{scene.cfg['W']} rays x 48 samples, colour stage, "
+                                         "100k-ray batches, gt depth"}
+    del pts
+    torch.cuda.empty_cache()
+    return out
+
+
 def reference_gpu_baseline(scene, budget_s=4.0):
     """The reference's PyTorch path ON THE GPU, for the ≥10x target of BASELINE.json: the oracle's
     restatement of Renderer.render_batch_ray + Mapper loss (the same torch ops the reference issues:
@@ -441,6 +489,7 @@ def main():
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture")
     ap.add_argument("--no-stress", action="store_true", help="skip the 512^3 grid-query HBM measurement")
     ap.add_argument("--no-frames", action="store_true", help="skip the room0 frames/s (tracking + mapping stages)")
+    ap.add_argument("--no-bulk", action="store_true", help="skip the forward-only mesher / render_img queries")
     ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                     help="process-group backend for N>1 (gloo: rehearse the sharded path on one GPU, eager)")
     ap.add_argument("--pixels", type=int, default=None,
@@ -552,6 +601,8 @@ def main():
             out["room0"] = room0_frame_rate(scene)
         if world == 1 and not args.no_stress:
             out["grid_query_stress"] = stress_grid_query(dev)
+        if world == 1 and not args.no_bulk:
+            out["bulk_forward"] = bulk_queries(scene)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(scene)
             ref = reference_gpu_baseline(scene)

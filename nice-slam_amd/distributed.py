@@ -112,14 +112,21 @@ class SparseGradExchange:
                 g = self.engine.decs[n].grad
                 tails.append((g, off))
                 off += g.numel()
-            self._plan[k] = (rows, tails, torch.empty(off, dtype=torch.float32, device=dev))
+            span = None
+            if not rows.numel() and tails:  # compact pieces back to back in one buffer: exchange in place
+                pieces = sorted(((t.data_ptr(), t.numel(), t) for t, _ in tails), key=lambda q: q[0])
+                if all(a[0] + a[1] * 4 == b[0] for a, b in zip(pieces, pieces[1:])):
+                    base = pieces[0][2]
+                    span = base.as_strided((sum(p[1] for p in pieces),), (1,))
+            buf = span if span is not None else torch.empty(off, dtype=torch.float32, device=dev)
+            self._plan[k] = (rows, tails if span is None else [], buf)
         return self._plan[k]
 
     def payload_bytes(self, keys, dnames):
         return self.plan(keys, dnames)[2].numel() * 4
 
     def __call__(self, keys, dnames):
-        rows, tails, buf = self.plan(keys, dnames)
+        rows, tails, buf = self.plan(keys, dnames)  # no rows, no tails: buf is the gradients themselves
         gbuf = self.engine.gbuf
         if rows.numel():
             self.pack(gbuf, rows, None, buf)

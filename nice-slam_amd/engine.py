@@ -116,7 +116,19 @@ class MappingEngine:
         sizes = {}
         for k, v in c.items():
             sizes[k] = 0 if not self.grid_grads else (self.rows[k].numel() * 32 if k in self.rows else v.numel())
-        self.gbuf = torch.zeros(sum(sizes.values()), dtype=torch.float32, device=self.device)
+        # one flat gradient buffer: the grids (c order), then the decoders' gradients (colour first, so
+        # the colour stage's whole exchange payload — middle/fine/colour rows + colour decoder — is
+        # one contiguous span of it: all-reduced in place, distributed.SparseGradExchange)
+        dorder = [n for n in ("color", "fine", "middle", "coarse") if n in self.decs]
+        gsum = sum(sizes.values())
+        self.gall = torch.zeros(gsum + sum(self.decs[n].param.numel() for n in dorder), dtype=torch.float32,
+                                device=self.device)
+        self.gbuf = self.gall[:gsum]
+        off = gsum
+        for n in dorder:
+            k = self.decs[n].param.numel()
+            self.decs[n].grad = self.gall[off:off + k]
+            off += k
         self._clean = False  # every gradient the next iteration accumulates into is known zero
         self.ggrad, off = {}, 0
         for k, v in c.items():
@@ -268,9 +280,7 @@ class MappingEngine:
                                                    w_color=self.w_color, occ_add=self.occ_add)
         keys, dnames = self.grads_for(stage, trainable_decoders)
         if not self._clean:
-            self.gbuf.zero_()
-            for n in self.decs.values():
-                n.grad.zero_()
+            self.gall.zero_()  # grid and decoder gradients: one memset
         self.query_bwd(stage, ro, rd, z, g_raw, keys, dnames)
         grads = self.adam_grads(stage, trainable_decoders)
         if exchange is not None:  # frustum-compacted all-reduce (distributed.SparseGradExchange)

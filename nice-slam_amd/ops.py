@@ -195,7 +195,7 @@ class _Query(torch.autograd.Function):
         raw = torch.empty(pts.shape[0], 4, dtype=torch.float32, device=pts.device)
         cfg = _fill_cfg(meta, [(g, None) if g is not None else (None, None) for g in grids], packed, {}, False)
         saved = None
-        if torch.is_grad_enabled() and any(ctx.needs_input_grad):  # ReLU masks for the backward
+        if any(ctx.needs_input_grad):  # ReLU masks for the backward (grad mode is off inside forward)
             saved = torch.empty(lib().nslam_query_saved_size(pts.shape[0]), dtype=torch.uint8, device=pts.device)
             cfg.saved_masks = saved.data_ptr()
         query_fwd_launch(cfg, pts, pts.shape[0], raw)

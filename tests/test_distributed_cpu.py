@@ -169,7 +169,7 @@ def test_sparse_exchange_sums_frustum_rows_only(tmp_path):
         assert torch.equal(r[k]["after_d"], r[0]["before_d"] + r[1]["before_d"])
 
 
-def _compact_exchange_worker(rank, world, port, out_path):
+def _compact_exchange_worker(rank, world, port, out_path, inplace=False):
     """Engine with frustum-compacted gradients (engine.rows set): the compact [n_rows, 32] grid
     gradients and the decoder gradients are summed over ranks as they are."""
     import sys
@@ -183,14 +183,21 @@ def _compact_exchange_worker(rank, world, port, out_path):
     g = torch.Generator().manual_seed(200 + rank)
     rows = {"grid_middle": torch.tensor([0, 7, 59], dtype=torch.int32),
             "grid_fine": torch.tensor([1, 2, 3, 100, 209], dtype=torch.int32)}
-    gbuf = torch.randn(8 * 32, generator=g)
+    gall = torch.randn(8 * 32 + 11, generator=g)
+    gbuf = gall[:256]
+    # inplace: the decoder gradient follows the grid rows in one buffer (MappingEngine.gall layout)
+    dgrad = gall[256:] if inplace else gall[256:].clone()
     eng = SimpleNamespace(c={"grid_middle": None, "grid_fine": None}, gbuf=gbuf, rows=rows,
                           ggrad={"grid_middle": gbuf[:96].view(-1, 32), "grid_fine": gbuf[96:].view(-1, 32)},
-                          decs={"color": SimpleNamespace(grad=torch.randn(11, generator=g))})
+                          decs={"color": SimpleNamespace(grad=dgrad)})
     before_g, before_d = gbuf.clone(), eng.decs["color"].grad.clone()
     ex = D.SparseGradExchange.__new__(D.SparseGradExchange)
     ex.engine, ex.group, ex.rows, ex._plan = eng, None, {}, {}
     ex.pack, ex.unpack = _torch_rows_pack, _torch_rows_unpack
+    if inplace:  # one contiguous span: all-reduced where it lies, no pack/unpack copies
+        def _no_copy(*a):
+            raise AssertionError("in-place exchange must not pack/unpack")
+        ex.pack = ex.unpack = _no_copy
     keys = ("grid_middle", "grid_fine")
     ex(keys, ("color",))
     torch.save({"before_g": before_g, "before_d": before_d, "after_g": gbuf, "after_d": eng.decs["color"].grad,
@@ -199,9 +206,10 @@ def _compact_exchange_worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-def test_compact_exchange_sums_compact_rows(tmp_path):
+@pytest.mark.parametrize("inplace", [False, True])
+def test_compact_exchange_sums_compact_rows(tmp_path, inplace):
     out = str(tmp_path / "cx")
-    mp.spawn(_compact_exchange_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    mp.spawn(_compact_exchange_worker, args=(2, _free_port(), out, inplace), nprocs=2, join=True)
     r = [torch.load(f"{out}.{k}") for k in range(2)]
     assert r[0]["bytes"] == (8 * 32 + 11) * 4
     for k in range(2):

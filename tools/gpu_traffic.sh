@@ -5,7 +5,7 @@ TAG=${1:?tag}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-CMD="python bench.py --steps 8 --warmup 3 --eager --no-cpu-baseline --no-stress --no-frames"
+CMD="python bench.py --steps 8 --warmup 3 --eager --no-cpu-baseline --no-stress --no-frames --no-bulk"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/fetch -o run -- $CMD > $OUT/fetch.log 2>&1 || { tail -5 $OUT/fetch.log; echo "STOP fetch"; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/write -o run -- $CMD > $OUT/write.log 2>&1 || { tail -5 $OUT/write.log; echo "STOP write"; exit 1; }
 python tools/traffic.py $OUT/fetch $OUT/write "rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE --kernel-trace -- $CMD" > $OUT/traffic.json && python -c "
