@@ -891,9 +891,9 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd_parts(QueryKArgs a, float*
   const Pt q = load_point(a, idx);
   uint32_t m[5];
   Corners cr;
-  grid_corners(cr, a.c.grid[NSLAM_DEC_MIDDLE], q);
-  const f32x16 cm = gather_tile(a.c.grid[NSLAM_DEC_MIDDLE].data, cr, lane);
   if (part == 0) {
+    grid_corners(cr, a.c.grid[NSLAM_DEC_MIDDLE], q);
+    const f32x16 cm = gather_tile(a.c.grid[NSLAM_DEC_MIDDLE].data, cr, lane);
     const float* pk = a.c.packed[NSLAM_DEC_MIDDLE];
     const XyzPack L{1};
     const f32x16 cms[1] = {cm};
@@ -902,9 +902,12 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd_parts(QueryKArgs a, float*
     float o = out_row(pk + L.Wo(), pk + L.Bo(), 0, h4, lane);
     if (!q.inside) o = 100.f;
     if (h == 0 && q.valid) occ_mid[idx] = o;
-  } else if (part == 1) {
+  } else if (part == 1) {  // the fine decoder also reads the middle feature (decoder.py:184-187)
+    Corners cm;
+    grid_corners(cm, a.c.grid[NSLAM_DEC_MIDDLE], q);
     grid_corners(cr, a.c.grid[NSLAM_DEC_FINE], q);
-    const f32x16 cf[2] = {gather_tile(a.c.grid[NSLAM_DEC_FINE].data, cr, lane), cm};
+    const f32x16 cf[2] = {gather_tile(a.c.grid[NSLAM_DEC_FINE].data, cr, lane),
+                          gather_tile(a.c.grid[NSLAM_DEC_MIDDLE].data, cm, lane)};
     const float* pk = a.c.packed[NSLAM_DEC_FINE];
     const XyzPack L{2};
     const f32x16 h4 = xyz_forward<2, false>(pk, cf, q.x, lane, m, nullptr);
