@@ -175,3 +175,78 @@ def test_mapper_optimize_map_schedule(tiny, monkeypatch):
         delta = slam.shared_c[k].detach().cpu() - sc.grids[k]
         rdelta = grids[k].detach() - sc.grids[k]
         assert rel_l2(delta.numpy(), rdelta.numpy()) < 5e-2, k
+
+
+def _nudged(c2w, ang, t):
+    """c2w rotated by `ang` rad about z and shifted by t: a distinct keyframe pose."""
+    ca, sa = float(np.cos(ang)), float(np.sin(ang))
+    R = torch.tensor([[ca, -sa, 0.0], [sa, ca, 0.0], [0.0, 0.0, 1.0]], dtype=torch.float32)
+    out = c2w.clone()
+    out[:3, :3] = R @ c2w[:3, :3]
+    out[:3, 3] += torch.tensor(t, dtype=torch.float32)
+    return out
+
+
+def test_mapper_bundle_adjustment(tiny, monkeypatch):
+    """BA on (the ScanNet config, BASELINE configs[2]): the camera 7-vectors of every window frame
+    but the oldest get gradients through the rays (Mapper.py:346-363, 441-448) and an Adam step at
+    BA_cam_lr in the colour stage (Mapper.py:420-421); optimize_map returns the updated current pose
+    and writes the keyframes' est_c2w back (Mapper.py:520-540)."""
+    sc = Scene(tiny)
+    cfg = base_cfg()
+    fp = FixedPixels(seed=9)
+    monkeypatch.setattr(P.common, "select_uv", fp)
+    slam = sc.slam(cfg)
+    mp_ = P.Mapper(cfg, None, slam)
+    mp_.BA = True
+    mp_.loss_history = []
+    monkeypatch.setattr(mp_, "keyframe_selection_overlap", lambda *a, **k: [0])
+    est = [sc.c2w.clone(), _nudged(sc.c2w, 0.01, (0.01, -0.005, 0.0))]
+    cur = _nudged(sc.c2w, -0.008, (0.0, 0.006, 0.004))
+    kf = [{"gt_c2w": sc.c2w, "idx": i, "color": sc.color, "depth": sc.depth, "est_c2w": est[i].clone()}
+          for i in range(2)]
+    n = 5
+    out = mp_.optimize_map(n, 1.0, 2, sc.color, sc.depth, sc.c2w, kf, [0, 1], cur.clone())
+    assert out is not None and tuple(out.shape) == (4, 4)
+    losses = [float(x) for x in mp_.loss_history]
+
+    # oracle replica: window [0, 1, -1]; the oldest frame (0) stays fixed, frames 1 and -1 are optimised
+    sd = {k: v.clone() for k, v in sc.sd.items() if not k.startswith("coarse")}
+    for k in sd:
+        if k.startswith("color_decoder."):
+            sd[k].requires_grad_(True)
+    grids = {k: v.clone().requires_grad_(True) for k, v in sc.grids.items()}
+    cams = [P.common.get_tensor_from_camera(est[1]).cpu().float().requires_grad_(True),
+            P.common.get_tensor_from_camera(cur).cpu().float().requires_grad_(True)]
+    st = cfg["mapping"]["stage"]
+    groups = [[v for k, v in sd.items() if k.startswith("color_decoder.")], [], [grids["grid_middle"]],
+              [grids["grid_fine"]], [grids["grid_color"]], cams]
+    opt = torch.optim.Adam([{"params": g, "lr": 0} for g in groups])
+    ref = []
+    for it in range(n):
+        stage = "middle" if it <= int(n * 0.4) else ("fine" if it <= int(n * 0.6) else "color")
+        for gi, name in enumerate(("decoders", "coarse", "middle", "fine", "color")):
+            opt.param_groups[gi]["lr"] = st[stage][name + "_lr"]
+        if stage == "color":
+            opt.param_groups[5]["lr"] = cfg["mapping"]["BA_cam_lr"]
+        opt.zero_grad()
+        poses = [est[0], orc.camera_from_tensor(cams[0]), orc.camera_from_tensor(cams[1])]
+        parts = [oracle_samples(sc, fp.log[3 * it + f], 0, sc.H, 0, sc.W, poses[f], sc.depth, sc.color)
+                 for f in range(3)]
+        ro, rd, gd, gc = (torch.cat([p[q] for p in parts]) for q in range(4))
+        keep = orc.inside_mask(ro, rd, gd, sc.bound)
+        ro, rd, gd, gc = ro[keep], rd[keep], gd[keep], gc[keep]
+        d, v, c = orc.render_batch_ray(sd, grids, rd, ro, stage, sc.bound, gd)
+        loss = orc.mapper_loss(d, c, gd, gc, stage)
+        loss.backward()
+        opt.step()
+        ref.append(float(loss))
+    np.testing.assert_allclose(losses, ref, rtol=2e-3)
+    # compare poses (q and -q are the same rotation): the update each camera received
+    for got, cam, start in ((kf[1]["est_c2w"], cams[0], est[1]), (out, cams[1], cur)):
+        ref_pose = orc.camera_from_tensor(cam.detach())
+        d_got = got[:3].detach().cpu() - start[:3]
+        d_ref = ref_pose - start[:3]
+        assert float(d_ref.abs().max()) > 1e-5  # the colour-stage step moved the camera
+        assert rel_l2(d_got.numpy(), d_ref.numpy()) < 5e-2
+    assert torch.equal(kf[0]["est_c2w"], est[0])  # the oldest frame is not optimised
