@@ -366,6 +366,48 @@ def bulk_queries(scene, res=256, reps=2):
     return out
 
 
+def frame_io(dev, n=6):
+    """Frame source: Replica-format frames at room0 size (680×1200 JPEG colour,
+    16-bit PNG depth, traj.txt) written to a temp folder, then read through datasets.Replica onto
+    the device — decode + H2D per frame, float64 colour (the reference's, datasets.py:91) vs the
+    float32 colour the engine keeps resident."""
+    import tempfile
+
+    import numpy as np
+    from PIL import Image
+    P = pkg()
+    H, W = ROOM0["H"], ROOM0["W"]
+    rng = np.random.default_rng(0)
+    out = {}
+    with tempfile.TemporaryDirectory() as d:
+        os.makedirs(os.path.join(d, "results"))
+        yy, xx = np.mgrid[0:H, 0:W]
+        for i in range(n):  # smooth synthetic content (JPEG cost like a real frame, not noise)
+            img = np.stack([(xx * 255 // W + 20 * i) % 256, yy * 255 // H, (xx + yy) % 256], -1).astype(np.uint8)
+            Image.fromarray(img).save(os.path.join(d, f"results/frame{i:06d}.jpg"), quality=95)
+            Image.fromarray(rng.integers(5000, 30000, (H, W)).astype(np.uint16)).save(
+                os.path.join(d, f"results/depth{i:06d}.png"))
+        with open(os.path.join(d, "traj.txt"), "w") as f:
+            for _ in range(n):
+                f.write(" ".join(str(v) for v in np.eye(4).ravel()) + "\n")
+        cfg = {"dataset": "replica", "data": {"input_folder": d},
+               "cam": {"H": H, "W": W, "fx": 600.0, "fy": 600.0, "cx": 599.5, "cy": 339.5,
+                       "png_depth_scale": 6553.5, "crop_edge": 0}}
+        for name, cd in (("f64", torch.float64), ("f32", torch.float32)):
+            ds = P.get_dataset(cfg, None, 1.0, device=dev, color_dtype=cd)
+            ds[0]
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(n):
+                ds[i]
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / n
+            out["color_" + name] = {"ms_per_frame": dt * 1e3, "frames_per_s": 1.0 / dt,
+                                    "device_bytes_per_frame": H * W * (3 * (8 if cd == torch.float64 else 4) + 4)}
+    out["workload"] = f"{n} Replica-format frames {H}x{W} (JPEG q95 colour, 16-bit PNG depth), Pillow decode + H2D"
+    return out
+
+
 def reference_gpu_baseline(scene, budget_s=4.0):
     """The reference's PyTorch path ON THE GPU, for the ≥10x target of BASELINE.json: the oracle's
     restatement of Renderer.render_batch_ray + Mapper loss (the same torch ops the reference issues:
@@ -603,6 +645,8 @@ def main():
             out["grid_query_stress"] = stress_grid_query(dev)
         if world == 1 and not args.no_bulk:
             out["bulk_forward"] = bulk_queries(scene)
+        if world == 1 and not args.no_bulk:
+            out["frame_io"] = frame_io(dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(scene)
             ref = reference_gpu_baseline(scene)
