@@ -403,7 +403,8 @@ def frame_io(dev, n=6):
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / n
             out["color_" + name] = {"ms_per_frame": dt * 1e3, "frames_per_s": 1.0 / dt,
-                                    "device_bytes_per_frame": H * W * (3 * (8 if cd == torch.float64 else 4) + 4)}
+                                    "device_bytes_per_frame": H * W * (3 * (8 if cd == torch.float64 else 4) + 4),
+                                    "h2d_bytes_per_frame": H * W * (3 + 4)}
     out["workload"] = f"{n} Replica-format frames {H}x{W} (JPEG q95 colour, 16-bit PNG depth), Pillow decode + H2D"
     return out
 

@@ -67,8 +67,13 @@ class BaseDataset(torch.utils.data.Dataset):
         return self.n_img
 
     def __getitem__(self, index):
-        color = torch.from_numpy(_read_color(self.color_paths[index]).astype(np.float64) / 255.0)
-        depth = torch.from_numpy(_read_depth(self.depth_paths[index]).astype(np.float32) / self.png_depth_scale)
+        # Only the decoded bytes cross PCIe (uint8 colour: 1/8 of the reference's float64 copy); the
+        # /255 (float64, datasets.py:91), /png_depth_scale (float32, :92), resize and crops run on
+        # the device with the same IEEE operations, so the values are the reference's.
+        color = torch.from_numpy(np.ascontiguousarray(_read_color(self.color_paths[index]))).to(self.device)
+        color = color.to(torch.float64) / 255.0
+        depth = torch.from_numpy(_read_depth(self.depth_paths[index]).astype(np.float32)).to(self.device)
+        depth = depth / self.png_depth_scale
         H, W = depth.shape
         if color.shape[:2] != (H, W):  # cv2.resize(color, (W, H)) INTER_LINEAR (datasets.py:94)
             color = F.interpolate(color.permute(2, 0, 1)[None], (H, W), mode="bilinear",
@@ -84,8 +89,7 @@ class BaseDataset(torch.utils.data.Dataset):
             depth = depth[e:-e, e:-e]
         pose = self.poses[index]
         pose[:3, 3] *= self.scale  # in place, as datasets.py:112
-        return (index, color.to(self.device, self.color_dtype).contiguous(), depth.to(self.device).contiguous(),
-                pose.to(self.device))
+        return index, color.to(self.color_dtype).contiguous(), depth.contiguous(), pose.to(self.device)
 
 
 class Replica(BaseDataset):

@@ -149,3 +149,17 @@ def test_checkpoint_roundtrip(tmp_path):
     assert list(ck["decoder_state_dict"]) == list(sd)
     assert all(torch.equal(ck["decoder_state_dict"][k], sd[k]) for k in sd)
     assert torch.equal(ck["estimate_c2w_list"], est) and ck["keyframe_list"] == [0, 2] and ck["idx"] == 3
+
+
+@pytest.mark.gpu
+def test_device_frames_equal_host_frames(tmp_path):
+    """On the device the /255, /png_depth_scale, resize and crops run after the uint8/float32 upload:
+    the frame must equal the host computation bit for bit."""
+    test_scannet_folder_resize_sort_and_crop(tmp_path)  # writes the folder
+    cfg = _cfg("scannet", str(tmp_path), 24, 32, 1000.0, crop_edge=2)
+    host = P.get_dataset(cfg, None, 1.0, device="cpu")
+    dev = P.get_dataset(cfg, None, 1.0, device="cuda:0")
+    for k in range(len(host)):
+        _, c0, d0, p0 = host[k]
+        _, c1, d1, p1 = dev[k]
+        assert c1.is_cuda and torch.equal(c1.cpu(), c0) and torch.equal(d1.cpu(), d0) and torch.equal(p1.cpu(), p0)
