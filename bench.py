@@ -460,6 +460,9 @@ def kernel_roofline(name, avg_ms, pts):
     return {"kernel": name, "bound": "mfma" if mfma else "hbm", "achieved": achieved, "peak": peak, "unit": unit,
             "frac": achieved / peak, "traffic": pmc_traffic(name), "avg_launch_ms": avg_ms,
             "ray_samples_per_launch": pts, "flop_per_sample": fl, "bytes_per_sample": by,
+            # the HIP-event span brackets these rocprofv3 kernels back to back: compare its average
+            # with the SUM of their average durations in profiles/r01_room0_kernels_*.md
+            "rocprof_kernels": list(SPAN_KERNELS.get(name, ())),
             "traffic_note": "HBM bytes per launch: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, "
                             "profiles/r01_traffic.json"}
 
