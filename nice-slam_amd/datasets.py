@@ -66,14 +66,22 @@ class BaseDataset(torch.utils.data.Dataset):
     def __len__(self):
         return self.n_img
 
+    def _lut(self, device):
+        lut = getattr(self, "_u8_lut", None)
+        if lut is None or lut.device != device:
+            lut = self._u8_lut = (torch.arange(256, dtype=torch.float64) / 255.0).to(device)
+        return lut
+
     def __getitem__(self, index):
-        # Only the decoded bytes cross PCIe (uint8 colour: 1/8 of the reference's float64 copy); the
-        # /255 (float64, datasets.py:91), /png_depth_scale (float32, :92), resize and crops run on
-        # the device with the same IEEE operations, so the values are the reference's.
-        color = torch.from_numpy(np.ascontiguousarray(_read_color(self.color_paths[index]))).to(self.device)
-        color = color.to(torch.float64) / 255.0
-        depth = torch.from_numpy(_read_depth(self.depth_paths[index]).astype(np.float32)).to(self.device)
-        depth = depth / self.png_depth_scale
+        # Only the decoded bytes cross PCIe for colour (uint8: 1/8 of the reference's float64 copy).
+        # /255 (float64, datasets.py:91) is a 256-entry table divided on the host and gathered on
+        # the device — torch's device kernels turn a scalar division into a reciprocal multiply,
+        # which is not the reference's correctly-rounded quotient.  Depth is divided on the host
+        # (float32, :92) for the same reason.  Resize and crops then run on the device.
+        u8 = torch.from_numpy(np.ascontiguousarray(_read_color(self.color_paths[index]))).to(self.device)
+        color = self._lut(u8.device)[u8.long()]
+        depth = torch.from_numpy(_read_depth(self.depth_paths[index]).astype(np.float32) / np.float32(self.png_depth_scale))
+        depth = depth.to(self.device)
         H, W = depth.shape
         if color.shape[:2] != (H, W):  # cv2.resize(color, (W, H)) INTER_LINEAR (datasets.py:94)
             color = F.interpolate(color.permute(2, 0, 1)[None], (H, W), mode="bilinear",
