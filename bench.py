@@ -526,6 +526,38 @@ def room0_frame_rate(scene, reps=20):
                     "tracker and mapper overlapped as the reference's processes (max of the two)"}
 
 
+def leg_main(leg):
+    """One auxiliary measurement in this (child) process on cuda:0; prints one JSON object."""
+    dev = torch.device("cuda", 0)
+    if leg == "stress":
+        res = stress_grid_query(dev)
+    elif leg == "frame_io":
+        res = frame_io(dev)
+    else:
+        scene = Room0Scene(dev, 0, cfg=dict(ROOM0), path="fused")
+        for _ in range(3):
+            scene.step()
+        torch.cuda.synchronize()
+        res = room0_frame_rate(scene) if leg == "frames" else bulk_queries(scene)
+    print(json.dumps(res))
+
+
+def run_leg(leg, timeout=300):
+    """Spawn `bench.py --leg <leg>` as a child process (not an exec of this GPU process) and return
+    its JSON, or an error record if it failed."""
+    import subprocess
+    try:
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--leg", leg], capture_output=True, text=True,
+                           timeout=timeout)
+    except subprocess.TimeoutExpired:
+        return {"error": f"leg {leg} timed out after {timeout} s"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        print(r.stderr[-2000:], file=sys.stderr)
+        return {"error": f"leg {leg} exited with {r.returncode}"}
+    return json.loads(lines[-1])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -542,7 +574,11 @@ def main():
                     help="override mapping pixels per iteration (scaling studies; the metric uses room0's 1000)")
     ap.add_argument("--path", choices=("fused", "autograd"), default="fused",
                     help="fused engine (default) or the autograd drop-in path")
+    ap.add_argument("--leg", choices=("frames", "stress", "bulk", "frame_io"), default=None,
+                    help="run one auxiliary measurement and print its JSON (bench.py spawns these itself)")
     args = ap.parse_args()
+    if args.leg:
+        return leg_main(args.leg)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -643,14 +679,15 @@ def main():
             keys, dn = scene.engine.grads_for("color", ("color",))
             out["exchange_bytes_per_step"] = scene.exchange.payload_bytes(keys, dn)
             out["dense_grad_bytes_per_step"] = sum(v.numel() for v in scene.grids.values()) * 4
+        # the auxiliary measurements run as child processes: a failure there (one run on a fresh
+        # box ended in a host heap abort inside a later leg) cannot take the headline line with it
         if world == 1 and not args.no_frames and args.path == "fused":
-            out["room0"] = room0_frame_rate(scene)
+            out["room0"] = run_leg("frames")
         if world == 1 and not args.no_stress:
-            out["grid_query_stress"] = stress_grid_query(dev)
+            out["grid_query_stress"] = run_leg("stress")
         if world == 1 and not args.no_bulk:
-            out["bulk_forward"] = bulk_queries(scene)
-        if world == 1 and not args.no_bulk:
-            out["frame_io"] = frame_io(dev)
+            out["bulk_forward"] = run_leg("bulk")
+            out["frame_io"] = run_leg("frame_io")
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(scene)
             ref = reference_gpu_baseline(scene)
