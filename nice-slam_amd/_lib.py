@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NSLAM_LIB") or os.path.join(_HERE, "libnslam.so")  # NSLAM_LIB: instrumented builds
 
 NSLAM_OK = 0
-ABI_VERSION = 7
+ABI_VERSION = 8
 STAGES = {"coarse": 0, "middle": 1, "fine": 2, "color": 3}
 DEC_COARSE, DEC_MIDDLE, DEC_FINE, DEC_COLOR = 0, 1, 2, 3
 
@@ -111,7 +111,7 @@ EXPORTS = (
     "nslam_composite_fwd", "nslam_composite_bwd", "nslam_grid_sample_fwd", "nslam_grid_sample_bwd",
     "nslam_workspace_size", "nslam_strerror", "nslam_abi_version", "nslam_gather_rays", "nslam_render_loss",
     "nslam_render_loss_workspace_size", "nslam_adam_step", "nslam_rows_pack", "nslam_rows_unpack",
-    "nslam_query_fwd_ws", "nslam_query_fwd_workspace_size",
+    "nslam_query_fwd_ws", "nslam_query_fwd_workspace_size", "nslam_cam_grad",
 )
 
 _lib = None
@@ -160,6 +160,7 @@ def lib():
         L.nslam_adam_step.argtypes = [ctypes.POINTER(NslamAdamSeg), i32, f32, f32, f32, i32, vp, vp]
         L.nslam_rows_pack.argtypes = [vp, vp, i64, i32, vp, i64, vp, vp]
         L.nslam_rows_unpack.argtypes = [vp, vp, i64, i32, vp, vp, i64, vp]
+        L.nslam_cam_grad.argtypes = [vp, vp, vp, vp, vp, i64, i32, vp, vp]
         if L.nslam_abi_version() != ABI_VERSION:
             raise RuntimeError(f"libnslam.so ABI {L.nslam_abi_version()} != {ABI_VERSION}: rebuild it")
         _lib = L

@@ -406,3 +406,108 @@ extern "C" int nslam_adam_step(const nslam_adam_seg* segs, int32_t n_segs, float
   hipLaunchKernelGGL(k_adam_steps, dim3(1), dim3(64), 0, s, a);
   return hip_status();
 }
+
+// ------------------------------------------------------------------------------------------
+// Camera gradient of a tracking iteration (ABI v8, include/nslam.h nslam_cam_grad)
+// ------------------------------------------------------------------------------------------
+namespace {
+
+constexpr int kCamThreads = 256;
+
+struct CamArgs {
+  const float* cam;
+  const float* c2w;
+  const double* g_pts;
+  const double* z;
+  const float* rd;
+  int64_t n;
+  int32_t S;
+  float* g_cam;
+};
+
+__global__ __launch_bounds__(kCamThreads) void k_cam_grad(CamArgs a) {
+  // per-thread partials over its rays: g_t (3) and A = Σ_r g_d,r d_rᵀ (9), in double
+  double acc[12];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) acc[k] = 0.0;
+  for (int64_t r = threadIdx.x; r < a.n; r += kCamThreads) {
+    double gt[3] = {0.0, 0.0, 0.0}, gd[3] = {0.0, 0.0, 0.0};
+    const double* gp = a.g_pts + r * a.S * 3;
+    const double* zr = a.z + r * a.S;
+    for (int s = 0; s < a.S; ++s) {
+      const double zs = zr[s];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const double g = gp[s * 3 + k];
+        gt[k] += g;
+        gd[k] += zs * g;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) acc[k] += gt[k];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const double gdi = (double)(float)gd[i];  // the ray-direction gradient is f32 (rays_d is f32)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) acc[3 + 3 * i + j] += gdi * (double)a.rd[r * 3 + j];
+    }
+  }
+  __shared__ double red[12][kCamThreads];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) red[k][threadIdx.x] = acc[k];
+  __syncthreads();
+  for (int w = kCamThreads / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+#pragma unroll
+      for (int k = 0; k < 12; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  double A[9], R[9], gR[9];
+  for (int k = 0; k < 9; ++k) A[k] = red[3 + k][0];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) R[3 * i + j] = a.c2w[4 * i + j];
+  for (int i = 0; i < 3; ++i)  // g_R = A · R
+    for (int j = 0; j < 3; ++j) gR[3 * i + j] = A[3 * i + 0] * R[j] + A[3 * i + 1] * R[3 + j] + A[3 * i + 2] * R[6 + j];
+  // quad2rotation (common.py:150-159): R = I + s P(q), q = (w, x, y, z) = indices 0..3.
+  // G[a][b] = Σ_ij gR_ij M_ij,ab with the ±1 terms of each entry of P.
+  double G[4][4] = {};
+  const double* g = gR;
+  G[2][2] -= g[0]; G[3][3] -= g[0];
+  G[1][2] += g[1]; G[3][0] -= g[1];
+  G[1][3] += g[2]; G[2][0] += g[2];
+  G[1][2] += g[3]; G[3][0] += g[3];
+  G[1][1] -= g[4]; G[3][3] -= g[4];
+  G[2][3] += g[5]; G[1][0] -= g[5];
+  G[1][3] += g[6]; G[2][0] -= g[6];
+  G[2][3] += g[7]; G[1][0] += g[7];
+  G[1][1] -= g[8]; G[2][2] -= g[8];
+  double q[4], qq = 0.0;
+  for (int k = 0; k < 4; ++k) {
+    q[k] = a.cam[k];
+    qq += q[k] * q[k];
+  }
+  const double s = 2.0 / qq;
+  double Hq[4], qHq = 0.0;
+  for (int i = 0; i < 4; ++i) {
+    double h = 0.0;
+    for (int j = 0; j < 4; ++j) h += (G[i][j] + G[j][i]) * q[j];
+    Hq[i] = h;
+    qHq += q[i] * h;
+  }
+  for (int i = 0; i < 4; ++i) a.g_cam[i] = (float)(s * Hq[i] - 0.5 * s * s * qHq * q[i]);
+  for (int k = 0; k < 3; ++k) a.g_cam[4 + k] = (float)red[k][0];
+}
+
+}  // namespace
+
+extern "C" int nslam_cam_grad(const float* cam, const float* c2w, const double* g_pts, const double* z_vals,
+                              const float* rays_d, int64_t n_rays, int32_t n_samples, float* g_cam, void* stream) {
+  if (!cam || !c2w || !g_cam || n_rays < 0 || n_samples <= 0) return NSLAM_EINVAL;
+  if (n_rays > 0 && (!g_pts || !z_vals || !rays_d)) return NSLAM_EINVAL;
+  CamArgs a{cam, c2w, g_pts, z_vals, rays_d, n_rays, n_samples, g_cam};
+  hipLaunchKernelGGL(k_cam_grad, dim3(1), dim3(kCamThreads), 0, reinterpret_cast<hipStream_t>(stream), a);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? NSLAM_OK : NSLAM_EHIP - (int)e;
+}

@@ -261,4 +261,4 @@ extern "C" const char* nslam_strerror(int code) {
   }
 }
 
-extern "C" int nslam_abi_version(void) { return 7; }
+extern "C" int nslam_abi_version(void) { return 8; }

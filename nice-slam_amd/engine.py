@@ -379,7 +379,7 @@ class TrackingEngine:
         sampler, decoders (ray form, ReLU masks saved) nslam_sample_rays, nslam_query_fwd_ws
         compositing + tracker loss + their backward    nslam_render_loss (mode TRACKER, median)
         d loss / d pts, frozen decoders                nslam_query_bwd_decoder (mask-only, 3 branches)
-        pts → rays → c2w → cam                         closed-form chain (QuatChain): ~15 launches
+        pts → rays → c2w → cam                         nslam_cam_grad (QuatChain's closed form)
         Adam on the camera                             ops.FusedAdam (device step count)
 
     so `iters` iterations can be captured in one hipGraph.  Grids and decoders are constants
@@ -420,12 +420,10 @@ class TrackingEngine:
         _, _, _, ray_loss, g_raw = ops.render_loss(raw, z, gd, gc, keep, mode="tracker", use_color=self.use_color,
                                                    handle_dynamic=self.handle_dynamic, w_color=self.w_color)
         g_pts = self.eng.query_bwd("color", ro, rd, z, g_raw, (), (), pts_grad=True)
-        with torch.no_grad():
-            g_cam = self._chain.backward(cam.detach(), s, c2w, g_pts, z, rd)
         if cam.grad is None:
-            cam.grad = g_cam
-        else:
-            cam.grad.copy_(g_cam)
+            cam.grad = torch.empty_like(cam)
+        # the whole pts → rays → c2w → 7-vector chain in one launch (QuatChain.backward's algebra)
+        ops.cam_grad(cam.detach(), c2w, g_pts, z, rd, cam.grad)
         optimizer.step()
         return ray_loss.sum()
 

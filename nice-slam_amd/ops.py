@@ -470,6 +470,21 @@ class PixelDraws:
                                      self.rank, ptr(self.gt_max), ptr(self.key))
 
 
+def cam_grad(cam, c2w, g_pts, z, rd, out):
+    """nslam_cam_grad (ABI v8): out [7] f32 = d loss / d cam through pts = t + (R·dir)·z and
+    get_camera_from_tensor (Renderer.py:172-174, common.py:137-176), from g_pts [N*S,3] f64,
+    z [N,S] f64, rays_d [N,3] f32 and the c2w [3,4] f32 the rays were built with."""
+    n, S = z.shape
+    for t, dt, shp in ((cam, torch.float32, (7,)), (c2w, torch.float32, (3, 4)), (g_pts, torch.float64, (n * S, 3)),
+                       (z, torch.float64, (n, S)), (rd, torch.float32, (n, 3)), (out, torch.float32, (7,))):
+        if t.dtype != dt or tuple(t.shape) != shp or not t.is_contiguous():
+            raise ValueError(f"cam_grad: expected contiguous {dt} {shp}, got {t.dtype} {tuple(t.shape)}")
+    with _span("cam_grad"):
+        rc = lib().nslam_cam_grad(ptr(cam), ptr(c2w), ptr(g_pts), ptr(z), ptr(rd), n, S, ptr(out), stream_ptr(cam.device))
+    check(rc, "nslam_cam_grad")
+    return out
+
+
 def render_loss(raw, z, gt_depth, gt_color, keep=None, mode="mapper", use_color=True, handle_dynamic=False,
                 w_color=0.2, want_grad=True, occ_add=None):
     """Mapper/Tracker rendering loss fused with compositing and its backward (see nslam.h).

@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_strerror(pkg):
     L = pkg._lib.lib()
-    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 7
+    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 8
     assert L.nslam_strerror(0) == b"ok"
     assert b"invalid" in L.nslam_strerror(-1)
 
@@ -122,3 +122,11 @@ def test_v4_entry_points_validate_without_gpu(pkg):
     for f in ("param", "grad", "exp_avg", "exp_avg_sq", "step"):
         setattr(seg[0], f, 64)
     assert L.nslam_adam_step(seg, 1, 0.9, 0.999, 1e-8, 1, 64, None) == -1
+
+
+def test_v8_cam_grad_validates_without_gpu(pkg):
+    L = pkg._lib.lib()
+    assert L.nslam_cam_grad(None, 64, 64, 64, 64, 10, 48, 64, None) == -1   # no cam
+    assert L.nslam_cam_grad(64, 64, 64, 64, 64, -1, 48, 64, None) == -1     # negative ray count
+    assert L.nslam_cam_grad(64, 64, None, 64, 64, 10, 48, 64, None) == -1   # rays without g_pts
+    assert L.nslam_cam_grad(64, 64, 64, 64, 64, 10, 0, 64, None) == -1      # no samples

@@ -498,3 +498,25 @@ def test_sharded_draws_slice_the_global_batch(tiny):
             assert torch.equal(a, b[sl])
         z = P.ops.sample_z(out[0], out[1], out[2], sc.bound, 32, 16, gt_max=dr.gt_max)
         assert torch.equal(z, z_full[sl])
+
+
+def test_cam_grad_kernel_matches_autograd():
+    """nslam_cam_grad (ABI v8) vs autograd through get_camera_from_tensor and pts = t + (R·dir)·z."""
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(4)
+    for n in (1, 200, 777):
+        cam = torch.randn(7, generator=g)
+        S = 48
+        z = torch.rand(n, S, generator=g, dtype=torch.float64) * 3
+        dirs = torch.randn(n, 3, generator=g)
+        camg = cam.clone().requires_grad_(True)
+        R = P.common.get_camera_from_tensor(camg)
+        rd = (dirs[:, None, :] * R[:3, :3]).sum(-1)
+        pts = R[:3, 3][None, None, :].double() + rd[:, None, :].double() * z[..., None]
+        gpts = torch.randn(n * S, 3, generator=g, dtype=torch.float64)
+        (ref,) = torch.autograd.grad(pts.reshape(-1, 3), camg, gpts)
+        ch = P.engine.QuatChain(dev)
+        c2w, _ = ch.forward(cam.to(dev))
+        out = torch.empty(7, device=dev)
+        P.ops.cam_grad(cam.to(dev), c2w.contiguous(), gpts.to(dev), z.to(dev), rd.detach().to(dev).contiguous(), out)
+        assert float((out.cpu() - ref).norm() / ref.norm()) < 1e-5, n
