@@ -412,7 +412,7 @@ extern "C" int nslam_adam_step(const nslam_adam_seg* segs, int32_t n_segs, float
 // ------------------------------------------------------------------------------------------
 namespace {
 
-constexpr int kCamThreads = 256;
+constexpr int kCamThreads = 1024;
 
 struct CamArgs {
   const float* cam;
@@ -426,43 +426,46 @@ struct CamArgs {
 };
 
 __global__ __launch_bounds__(kCamThreads) void k_cam_grad(CamArgs a) {
-  // per-thread partials over its rays: g_t (3) and A = Σ_r g_d,r d_rᵀ (9), in double
+  // One point per thread per step (coalesced g_pts rows): g_t = Σ g and A = Σ_r g_d,r d_rᵀ, which
+  // is linear in the points, = Σ_p (z_p g_p) d_r(p)ᵀ; double partials, wave shuffles, then LDS.
   double acc[12];
 #pragma unroll
   for (int k = 0; k < 12; ++k) acc[k] = 0.0;
-  for (int64_t r = threadIdx.x; r < a.n; r += kCamThreads) {
-    double gt[3] = {0.0, 0.0, 0.0}, gd[3] = {0.0, 0.0, 0.0};
-    const double* gp = a.g_pts + r * a.S * 3;
-    const double* zr = a.z + r * a.S;
-    for (int s = 0; s < a.S; ++s) {
-      const double zs = zr[s];
+  const int np = (int)(a.n * a.S);  // < 2^31 (checked by nslam_cam_grad): 32-bit index math
+  for (int p = threadIdx.x; p < np; p += kCamThreads) {
+    const int r = p / a.S;
+    const double zs = a.z[p];
+    double g[3];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const double g = gp[s * 3 + k];
-        gt[k] += g;
-        gd[k] += zs * g;
-      }
+    for (int k = 0; k < 3; ++k) {
+      g[k] = a.g_pts[p * 3 + k];
+      acc[k] += g[k];
     }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) acc[k] += gt[k];
+    const double d0 = a.rd[r * 3], d1 = a.rd[r * 3 + 1], d2 = a.rd[r * 3 + 2];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      const double gdi = (double)(float)gd[i];  // the ray-direction gradient is f32 (rays_d is f32)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) acc[3 + 3 * i + j] += gdi * (double)a.rd[r * 3 + j];
+      const double gz = zs * g[i];
+      acc[3 + 3 * i] += gz * d0;
+      acc[4 + 3 * i] += gz * d1;
+      acc[5 + 3 * i] += gz * d2;
     }
   }
-  __shared__ double red[12][kCamThreads];
 #pragma unroll
-  for (int k = 0; k < 12; ++k) red[k][threadIdx.x] = acc[k];
+  for (int k = 0; k < 12; ++k)
+    for (int off = 32; off > 0; off >>= 1) acc[k] += __shfl_xor(acc[k], off, 64);
+  __shared__ double red[12][kCamThreads / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 12; ++k) red[k][wave] = acc[k];
+  }
   __syncthreads();
-  for (int w = kCamThreads / 2; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) {
-#pragma unroll
-      for (int k = 0; k < 12; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + w];
-    }
-    __syncthreads();
+  if (threadIdx.x < 12) {  // fixed-order sum over the waves: deterministic
+    double t = 0.0;
+    for (int w = 0; w < kCamThreads / 64; ++w) t += red[threadIdx.x][w];
+    red[threadIdx.x][0] = t;
   }
+  __syncthreads();
   if (threadIdx.x != 0) return;
   double A[9], R[9], gR[9];
   for (int k = 0; k < 9; ++k) A[k] = red[3 + k][0];
@@ -506,6 +509,7 @@ extern "C" int nslam_cam_grad(const float* cam, const float* c2w, const double* 
                               const float* rays_d, int64_t n_rays, int32_t n_samples, float* g_cam, void* stream) {
   if (!cam || !c2w || !g_cam || n_rays < 0 || n_samples <= 0) return NSLAM_EINVAL;
   if (n_rays > 0 && (!g_pts || !z_vals || !rays_d)) return NSLAM_EINVAL;
+  if (n_rays * (int64_t)n_samples >= (int64_t(1) << 31)) return NSLAM_EUNSUPPORTED;
   CamArgs a{cam, c2w, g_pts, z_vals, rays_d, n_rays, n_samples, g_cam};
   hipLaunchKernelGGL(k_cam_grad, dim3(1), dim3(kCamThreads), 0, reinterpret_cast<hipStream_t>(stream), a);
   const hipError_t e = hipGetLastError();
