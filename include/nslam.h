@@ -298,6 +298,10 @@ int nslam_rows_unpack(const float* in, const int32_t* rows, int64_t n_rows, int3
 int nslam_cam_grad(const float* cam, const float* c2w, const double* g_pts, const double* z_vals, const float* rays_d,
                    int64_t n_rays, int32_t n_samples, float* g_cam, void* stream);
 
+/* ABI v8.  c2w [3,4] f32 = get_camera_from_tensor(cam [7]) (common.py:137-176, quad2rotation's
+ * formula and operation order; |q|² summed ((w²+x²)+y²)+z²), one thread. */
+int nslam_cam_pose(const float* cam, float* c2w, void* stream);
+
 enum { NSLAM_WS_SAMPLER = 0 };
 size_t nslam_workspace_size(int which, int64_t n);
 

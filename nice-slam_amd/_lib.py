@@ -111,7 +111,7 @@ EXPORTS = (
     "nslam_composite_fwd", "nslam_composite_bwd", "nslam_grid_sample_fwd", "nslam_grid_sample_bwd",
     "nslam_workspace_size", "nslam_strerror", "nslam_abi_version", "nslam_gather_rays", "nslam_render_loss",
     "nslam_render_loss_workspace_size", "nslam_adam_step", "nslam_rows_pack", "nslam_rows_unpack",
-    "nslam_query_fwd_ws", "nslam_query_fwd_workspace_size", "nslam_cam_grad",
+    "nslam_query_fwd_ws", "nslam_query_fwd_workspace_size", "nslam_cam_grad", "nslam_cam_pose",
 )
 
 _lib = None
@@ -161,6 +161,7 @@ def lib():
         L.nslam_rows_pack.argtypes = [vp, vp, i64, i32, vp, i64, vp, vp]
         L.nslam_rows_unpack.argtypes = [vp, vp, i64, i32, vp, vp, i64, vp]
         L.nslam_cam_grad.argtypes = [vp, vp, vp, vp, vp, i64, i32, vp, vp]
+        L.nslam_cam_pose.argtypes = [vp, vp, vp]
         if L.nslam_abi_version() != ABI_VERSION:
             raise RuntimeError(f"libnslam.so ABI {L.nslam_abi_version()} != {ABI_VERSION}: rebuild it")
         _lib = L

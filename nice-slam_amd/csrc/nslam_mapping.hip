@@ -515,3 +515,27 @@ extern "C" int nslam_cam_grad(const float* cam, const float* c2w, const double* 
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? NSLAM_OK : NSLAM_EHIP - (int)e;
 }
+
+namespace {
+
+__global__ __launch_bounds__(64) void k_cam_pose(const float* __restrict__ cam, float* __restrict__ c2w) {
+  if (threadIdx.x != 0) return;
+  const float qr = cam[0], qi = cam[1], qj = cam[2], qk = cam[3];
+  const float two_s = 2.0f / (((qr * qr + qi * qi) + qj * qj) + qk * qk);
+  const float R[9] = {1.0f - two_s * (qj * qj + qk * qk), two_s * (qi * qj - qk * qr), two_s * (qi * qk + qj * qr),
+                      two_s * (qi * qj + qk * qr), 1.0f - two_s * (qi * qi + qk * qk), two_s * (qj * qk - qi * qr),
+                      two_s * (qi * qk - qj * qr), two_s * (qj * qk + qi * qr), 1.0f - two_s * (qi * qi + qj * qj)};
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) c2w[4 * i + j] = R[3 * i + j];
+    c2w[4 * i + 3] = cam[4 + i];
+  }
+}
+
+}  // namespace
+
+extern "C" int nslam_cam_pose(const float* cam, float* c2w, void* stream) {
+  if (!cam || !c2w) return NSLAM_EINVAL;
+  hipLaunchKernelGGL(k_cam_pose, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), cam, c2w);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? NSLAM_OK : NSLAM_EHIP - (int)e;
+}

@@ -397,7 +397,7 @@ class TrackingEngine:
         self.window = (he, self.H - he, we, self.W - we)
         self.w_color, self.handle_dynamic, self.use_color = w_color, handle_dynamic, use_color
         self.device = torch.device(device)
-        self._chain = None
+        self._c2w = None
 
     def n_window(self):
         h0, h1, w0, w1 = self.window
@@ -409,10 +409,9 @@ class TrackingEngine:
         .grad the optimizer reads.  Returns the loss (device f64 scalar) of the pose BEFORE the step."""
         fx, fy, cx, cy = self.intr
         n = pix.numel()
-        if self._chain is None:
-            self._chain = QuatChain(cam.device)
-        with torch.no_grad():
-            c2w, s = self._chain.forward(cam.detach())
+        if self._c2w is None:
+            self._c2w = torch.empty(3, 4, dtype=torch.float32, device=cam.device)
+        c2w = ops.cam_pose(cam.detach(), self._c2w)  # get_camera_from_tensor in one launch
         ro, rd, gd, gc, keep = ops.gather_rays([(depth, color, c2w)], pix, n, self.H, self.W, self.window,
                                                fx, fy, cx, cy, self.bound)
         z = ops.sample_z(ro, rd, gd, self.bound, self.n_strat, self.n_surf)

@@ -470,6 +470,16 @@ class PixelDraws:
                                      self.rank, ptr(self.gt_max), ptr(self.key))
 
 
+def cam_pose(cam, out):
+    """nslam_cam_pose (ABI v8): out [3,4] f32 = get_camera_from_tensor(cam [7]) in one launch."""
+    if cam.dtype != torch.float32 or tuple(cam.shape) != (7,) or not cam.is_contiguous():
+        raise ValueError("cam_pose: cam must be a contiguous float32 [7]")
+    if out.dtype != torch.float32 or tuple(out.shape) != (3, 4) or not out.is_contiguous():
+        raise ValueError("cam_pose: out must be a contiguous float32 [3, 4]")
+    check(lib().nslam_cam_pose(ptr(cam), ptr(out), stream_ptr(cam.device)), "nslam_cam_pose")
+    return out
+
+
 def cam_grad(cam, c2w, g_pts, z, rd, out):
     """nslam_cam_grad (ABI v8): out [7] f32 = d loss / d cam through pts = t + (R·dir)·z and
     get_camera_from_tensor (Renderer.py:172-174, common.py:137-176), from g_pts [N*S,3] f64,

@@ -130,3 +130,9 @@ def test_v8_cam_grad_validates_without_gpu(pkg):
     assert L.nslam_cam_grad(64, 64, 64, 64, 64, -1, 48, 64, None) == -1     # negative ray count
     assert L.nslam_cam_grad(64, 64, None, 64, 64, 10, 48, 64, None) == -1   # rays without g_pts
     assert L.nslam_cam_grad(64, 64, 64, 64, 64, 10, 0, 64, None) == -1      # no samples
+
+
+def test_v8_cam_pose_validates_without_gpu(pkg):
+    L = pkg._lib.lib()
+    assert L.nslam_cam_pose(None, 64, None) == -1
+    assert L.nslam_cam_pose(64, None, None) == -1

@@ -520,3 +520,21 @@ def test_cam_grad_kernel_matches_autograd():
         out = torch.empty(7, device=dev)
         P.ops.cam_grad(cam.to(dev), c2w.contiguous(), gpts.to(dev), z.to(dev), rd.detach().to(dev).contiguous(), out)
         assert float((out.cpu() - ref).norm() / ref.norm()) < 1e-5, n
+
+
+def test_cam_pose_kernel_matches_get_camera_from_tensor():
+    """nslam_cam_pose (ABI v8) vs the torch restatement of get_camera_from_tensor on the device.
+    Same products and differences; |q|² may be summed in a different order than torch's reduce,
+    so the pose is checked to 2 ulp-scale (rel 1e-6), and the exact-match fraction is reported."""
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(6)
+    exact, worst = 0, 0.0
+    out = torch.empty(3, 4, device=dev)
+    for _ in range(200):
+        cam = torch.randn(7, generator=g).to(dev)
+        ref = P.common.get_camera_from_tensor(cam)
+        P.ops.cam_pose(cam, out)
+        exact += bool(torch.equal(out, ref))
+        worst = max(worst, float((out - ref).abs().max() / ref.abs().max()))
+    print(f"cam_pose: {exact}/200 bit-identical, worst rel {worst:.2e}")
+    assert worst < 1e-6
