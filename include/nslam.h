@@ -288,18 +288,21 @@ int nslam_rows_pack(const float* grid, const int32_t* rows, int64_t n_rows, int3
 int nslam_rows_unpack(const float* in, const int32_t* rows, int64_t n_rows, int32_t row_len, float* grid,
                       float* tail, int64_t n_tail, void* stream);
 
-/* ABI v8.  Camera gradient of a tracking iteration (Tracker.py:110-126): the 7-vector gradient of
+/* ABI v9.  Camera gradient of a tracking iteration (Tracker.py:110-126): the 7-vector gradient of
  * the loss through pts = t + (R·dir)·z (Renderer.py:172-174, common.py:80-89) and
  * get_camera_from_tensor (common.py:137-176), in one single-workgroup launch:
  *   g_t = Σ g_pts;  g_R = (Σ_r g_d,r d_rᵀ)·R with g_d,r = Σ_s z_rs g_pts,rs (dir = Rᵀ d);
  *   g_q = s (G + Gᵀ) q − s² (qᵀ G q) q,  s = 2/|q|²,  G = Σ_ij g_R,ij M_ij  (R = I + s·P(q)).
  * cam [7] (w,x,y,z,tx,ty,tz), c2w [3,4] the pose rendered with, g_pts [n_rays*n_samples,3] f64,
- * z_vals [n_rays,n_samples] f64, rays_d [n_rays,3] f32; writes g_cam [7] f32. */
+ * z_vals [n_rays,n_samples] f64, rays_d [n_rays,3] f32; writes g_cam [7] f32.
+ * NSLAM_EUNSUPPORTED when 3*n_rays*n_samples >= 2^31 (32-bit g_pts offsets). */
 int nslam_cam_grad(const float* cam, const float* c2w, const double* g_pts, const double* z_vals, const float* rays_d,
                    int64_t n_rays, int32_t n_samples, float* g_cam, void* stream);
 
-/* ABI v8.  c2w [3,4] f32 = get_camera_from_tensor(cam [7]) (common.py:137-176, quad2rotation's
- * formula and operation order; |q|² summed ((w²+x²)+y²)+z²), one thread. */
+/* ABI v9.  c2w [3,4] f32 = get_camera_from_tensor(cam [7]) (common.py:137-176, quad2rotation's
+ * products and differences, no FMA contraction), one thread.  |q|² is summed ((w²+x²)+y²)+z²;
+ * the order of torch's (quad*quad).sum(-1) reduction is not pinned, so the pose matches the
+ * reference to within ~1 ulp per entry (bit-identical for most poses), not bit-for-bit. */
 int nslam_cam_pose(const float* cam, float* c2w, void* stream);
 
 enum { NSLAM_WS_SAMPLER = 0 };

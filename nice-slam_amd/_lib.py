@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NSLAM_LIB") or os.path.join(_HERE, "libnslam.so")  # NSLAM_LIB: instrumented builds
 
 NSLAM_OK = 0
-ABI_VERSION = 8
+ABI_VERSION = 9
 STAGES = {"coarse": 0, "middle": 1, "fine": 2, "color": 3}
 DEC_COARSE, DEC_MIDDLE, DEC_FINE, DEC_COLOR = 0, 1, 2, 3
 
@@ -125,6 +125,12 @@ def lib():
             raise RuntimeError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
                                "(make -C nice-slam_amd/csrc); there is no CPU fallback")
         L = ctypes.CDLL(LIB_PATH)
+        # a stale build (older ABI, or one that lacks an export) gets the rebuild message, not an
+        # AttributeError from the first missing symbol
+        missing = [n for n in EXPORTS if not hasattr(L, n)]
+        if missing:
+            raise RuntimeError(f"{LIB_PATH} does not export {', '.join(missing)}: rebuild it "
+                               "(make -C nice-slam_amd/csrc)")
         vp, i32, i64, sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
         dp = ctypes.POINTER(ctypes.c_double)
         L.nslam_pack_layout.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int32), ctypes.c_int]

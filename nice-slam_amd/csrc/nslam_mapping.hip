@@ -431,7 +431,7 @@ __global__ __launch_bounds__(kCamThreads) void k_cam_grad(CamArgs a) {
   double acc[12];
 #pragma unroll
   for (int k = 0; k < 12; ++k) acc[k] = 0.0;
-  const int np = (int)(a.n * a.S);  // < 2^31 (checked by nslam_cam_grad): 32-bit index math
+  const int np = (int)(a.n * a.S);  // 3*np < 2^31 (checked by nslam_cam_grad): 32-bit g_pts offsets
   for (int p = threadIdx.x; p < np; p += kCamThreads) {
     const int r = p / a.S;
     const double zs = a.z[p];
@@ -509,7 +509,8 @@ extern "C" int nslam_cam_grad(const float* cam, const float* c2w, const double* 
                               const float* rays_d, int64_t n_rays, int32_t n_samples, float* g_cam, void* stream) {
   if (!cam || !c2w || !g_cam || n_rays < 0 || n_samples <= 0) return NSLAM_EINVAL;
   if (n_rays > 0 && (!g_pts || !z_vals || !rays_d)) return NSLAM_EINVAL;
-  if (n_rays * (int64_t)n_samples >= (int64_t(1) << 31)) return NSLAM_EUNSUPPORTED;
+  // the kernel indexes g_pts rows as 32-bit p*3+k: the point count must satisfy 3*points < 2^31
+  if (n_rays * (int64_t)n_samples * 3 >= (int64_t(1) << 31)) return NSLAM_EUNSUPPORTED;
   CamArgs a{cam, c2w, g_pts, z_vals, rays_d, n_rays, n_samples, g_cam};
   hipLaunchKernelGGL(k_cam_grad, dim3(1), dim3(kCamThreads), 0, reinterpret_cast<hipStream_t>(stream), a);
   const hipError_t e = hipGetLastError();

@@ -328,48 +328,6 @@ def c2w_grads(g_pts, z, dirs):
     return torch.cat([g_R, g_ro.sum(1)[..., None]], 2)
 
 
-class QuatChain:
-    """get_camera_from_tensor (src/common.py:137-176) and its vector-Jacobian product in closed form,
-    as a handful of vectorised launches instead of the ~100 scalar autograd kernels of
-    quad2rotation's graph (they were 80 % of a 0.59 ms tracking iteration).
-
-    With q = (w, x, y, z) and s = 2/|q|², quad2rotation is R = I + s·P(q), P_ij = Σ_ab M_ij,ab q_a q_b
-    for a constant ±1 tensor M (common.py:150-159, same products, sums and rounding: two non-zero
-    terms per entry).  For an upstream gradient g_R, with G = Σ_ij g_R,ij M_ij (4×4):
-        d/dq (g_R · R) = s (G + Gᵀ) q − s² (qᵀ G q) q.
-    Through the rays: pts = o + d·z with o = t, d = R·dir (common.py:80-89, Renderer.py:172-174), so
-    g_t = Σ g_pts and g_R = Σ_r g_d,r dir_rᵀ = (Σ_r g_d,r d_rᵀ) R, g_d,r = Σ_s z g_pts (dir = Rᵀ d)."""
-
-    _TERMS = (((-1, 2, 2), (-1, 3, 3)), ((1, 1, 2), (-1, 3, 0)), ((1, 1, 3), (1, 2, 0)),
-              ((1, 1, 2), (1, 3, 0)), ((-1, 1, 1), (-1, 3, 3)), ((1, 2, 3), (-1, 1, 0)),
-              ((1, 1, 3), (-1, 2, 0)), ((1, 2, 3), (1, 1, 0)), ((-1, 1, 1), (-1, 2, 2)))
-
-    def __init__(self, device):
-        M = torch.zeros(9, 4, 4, dtype=torch.float32)
-        for r, terms in enumerate(self._TERMS):
-            for sgn, a, b in terms:
-                M[r, a, b] = sgn
-        self.M = M.view(9, 16).to(device)
-        self.eye = torch.eye(3, dtype=torch.float32, device=device)
-
-    def forward(self, cam):
-        q = cam[:4]
-        s = 2.0 / (q * q).sum()
-        P = (self.M * (q[:, None] * q[None, :]).view(1, 16)).sum(1).view(3, 3)
-        return torch.cat([self.eye + s * P, cam[4:, None]], 1), s
-
-    def backward(self, cam, s, c2w, g_pts, z, rd):
-        q = cam[:4]
-        gp = g_pts.view(z.shape[0], z.shape[1], 3)
-        g_t = gp.sum((0, 1)).float()
-        g_d = (gp * z[..., None]).sum(1).float()
-        g_R = (g_d.t() @ rd) @ c2w[:, :3]
-        G = (self.M * g_R.reshape(9, 1)).sum(0).view(4, 4)
-        Hq = (G + G.t()) @ q
-        g_q = s * Hq - (0.5 * s * s * torch.dot(q, Hq)) * q
-        return torch.cat([g_q, g_t])
-
-
 class TrackingEngine:
     """Tracker.optimize_cam_in_batch (src/Tracker.py:71-128) on the HIP kernels, without host
     synchronisation: one camera iteration is
@@ -379,7 +337,7 @@ class TrackingEngine:
         sampler, decoders (ray form, ReLU masks saved) nslam_sample_rays, nslam_query_fwd_ws
         compositing + tracker loss + their backward    nslam_render_loss (mode TRACKER, median)
         d loss / d pts, frozen decoders                nslam_query_bwd_decoder (mask-only, 3 branches)
-        pts → rays → c2w → cam                         nslam_cam_grad (QuatChain's closed form)
+        pts → rays → c2w → cam                         nslam_cam_grad (closed form, include/nslam.h)
         Adam on the camera                             ops.FusedAdam (device step count)
 
     so `iters` iterations can be captured in one hipGraph.  Grids and decoders are constants
@@ -421,7 +379,7 @@ class TrackingEngine:
         g_pts = self.eng.query_bwd("color", ro, rd, z, g_raw, (), (), pts_grad=True)
         if cam.grad is None:
             cam.grad = torch.empty_like(cam)
-        # the whole pts → rays → c2w → 7-vector chain in one launch (QuatChain.backward's algebra)
+        # the whole pts → rays → c2w → 7-vector chain in one launch
         ops.cam_grad(cam.detach(), c2w, g_pts, z, rd, cam.grad)
         optimizer.step()
         return ray_loss.sum()

@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_strerror(pkg):
     L = pkg._lib.lib()
-    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 8
+    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 9
     assert L.nslam_strerror(0) == b"ok"
     assert b"invalid" in L.nslam_strerror(-1)
 
@@ -130,6 +130,8 @@ def test_v8_cam_grad_validates_without_gpu(pkg):
     assert L.nslam_cam_grad(64, 64, 64, 64, 64, -1, 48, 64, None) == -1     # negative ray count
     assert L.nslam_cam_grad(64, 64, None, 64, 64, 10, 48, 64, None) == -1   # rays without g_pts
     assert L.nslam_cam_grad(64, 64, 64, 64, 64, 10, 0, 64, None) == -1      # no samples
+    # g_pts rows are indexed p*3+k in 32 bits: 3 * rays * samples must stay below 2^31
+    assert L.nslam_cam_grad(64, 64, 64, 64, 64, (1 << 31) // 3 // 48 + 1, 48, 64, None) == -2
 
 
 def test_v8_cam_pose_validates_without_gpu(pkg):

@@ -501,7 +501,8 @@ def test_sharded_draws_slice_the_global_batch(tiny):
 
 
 def test_cam_grad_kernel_matches_autograd():
-    """nslam_cam_grad (ABI v8) vs autograd through get_camera_from_tensor and pts = t + (R·dir)·z."""
+    """nslam_cam_grad (ABI v9) vs autograd through get_camera_from_tensor and pts = t + (R·dir)·z;
+    the pose handed to the kernel is get_camera_from_tensor's own (common.py:163-176)."""
     dev = torch.device("cuda:0")
     g = torch.Generator().manual_seed(4)
     for n in (1, 200, 777):
@@ -515,15 +516,14 @@ def test_cam_grad_kernel_matches_autograd():
         pts = R[:3, 3][None, None, :].double() + rd[:, None, :].double() * z[..., None]
         gpts = torch.randn(n * S, 3, generator=g, dtype=torch.float64)
         (ref,) = torch.autograd.grad(pts.reshape(-1, 3), camg, gpts)
-        ch = P.engine.QuatChain(dev)
-        c2w, _ = ch.forward(cam.to(dev))
+        c2w = P.common.get_camera_from_tensor(cam.to(dev))
         out = torch.empty(7, device=dev)
         P.ops.cam_grad(cam.to(dev), c2w.contiguous(), gpts.to(dev), z.to(dev), rd.detach().to(dev).contiguous(), out)
         assert float((out.cpu() - ref).norm() / ref.norm()) < 1e-5, n
 
 
 def test_cam_pose_kernel_matches_get_camera_from_tensor():
-    """nslam_cam_pose (ABI v8) vs the torch restatement of get_camera_from_tensor on the device.
+    """nslam_cam_pose (ABI v9) vs the torch restatement of get_camera_from_tensor on the device.
     Same products and differences; |q|² may be summed in a different order than torch's reduce,
     so the pose is checked to 2 ulp-scale (rel 1e-6), and the exact-match fraction is reported."""
     dev = torch.device("cuda:0")
