@@ -99,6 +99,11 @@ typedef struct nslam_query_cfg {
    * adds it on read (nslam_loss_cfg.occ_add = ws), saving a launch per query. */
   int32_t defer_occ;
   int32_t pad2_;
+  /* ABI v9: activation tape of the colour decoder (NULL = none).  nslam_query_fwd[_ws] writes the
+   * post-ReLU hidden tiles h0..h4 of every 32-point tile ([tile][layer][4][64] float4,
+   * nslam_query_tape_size(M) bytes); with it and saved_masks the colour decoder's weight-gradient
+   * backward reads them instead of recomputing its forward (Mapper.py:503). */
+  float* act_tape;
 } nslam_query_cfg;
 
 /* ---- packing ------------------------------------------------------------------------------
@@ -151,6 +156,7 @@ int nslam_query_bwd_decoder(const nslam_query_cfg* cfg, int32_t dec, int32_t acc
                             void* stream);
 size_t nslam_query_bwd_decoder_workspace_size(const nslam_query_cfg* cfg, int32_t dec, int64_t n_pts);
 size_t nslam_query_saved_size(int64_t n_pts);
+size_t nslam_query_tape_size(int64_t n_pts); /* ABI v9 */
 
 /* ---- compositing: raw2outputs_nerf_color, src/common.py:204-245 (occupancy mode) ------------ */
 int nslam_composite_fwd(const float* raw, const double* z_vals, int64_t n_rays, int32_t n_samples,

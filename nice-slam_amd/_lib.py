@@ -63,6 +63,7 @@ class NslamQueryCfg(ctypes.Structure):
         ("saved_masks", ctypes.c_void_p),
         ("defer_occ", ctypes.c_int32),  # ABI v7
         ("pad2_", ctypes.c_int32),
+        ("act_tape", ctypes.c_void_p),  # ABI v9: colour-decoder activation tape (NULL = none)
     ]
 
 
@@ -112,6 +113,7 @@ EXPORTS = (
     "nslam_workspace_size", "nslam_strerror", "nslam_abi_version", "nslam_gather_rays", "nslam_render_loss",
     "nslam_render_loss_workspace_size", "nslam_adam_step", "nslam_rows_pack", "nslam_rows_unpack",
     "nslam_query_fwd_ws", "nslam_query_fwd_workspace_size", "nslam_cam_grad", "nslam_cam_pose",
+    "nslam_query_tape_size",
 )
 
 _lib = None
@@ -147,6 +149,8 @@ def lib():
         L.nslam_query_bwd_decoder_workspace_size.restype = sz
         L.nslam_query_saved_size.argtypes = [i64]
         L.nslam_query_saved_size.restype = sz
+        L.nslam_query_tape_size.argtypes = [i64]
+        L.nslam_query_tape_size.restype = sz
         L.nslam_composite_fwd.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp]
         L.nslam_composite_bwd.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, vp]
         L.nslam_grid_sample_fwd.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), vp, i64, vp, vp]

@@ -179,6 +179,7 @@ struct Corners {
   float f0[3], f1[3];  // (lo-side, hi-side) linear factors per axis x,y,z
   float gmul[3];   // d(unnormalised)/d(normalised) incl. the clip gate: 0 or (n-1)/2
   uint32_t ok;     // bit k: corner k is inside the grid (torch's within_bounds_3d)
+  int32_t cell;    // lower-corner voxel coordinates ix | iy << 10 | iz << 20 (dims <= 1024)
 };
 
 // normalised coordinate of axis a (decoder.py:169 → common.py:269-284), float64 then .float()
@@ -215,6 +216,7 @@ __device__ __forceinline__ void make_corners(Corners& c, const float nc3[3], con
     c.f0[a] = (float)(i0[a] + 1) - u;      // (ix_bse - ix)
     hi_ok[a] = (i0[a] + 1) <= n[a] - 1;
   }
+  c.cell = i0[0] | (i0[1] << 10) | (i0[2] << 20);
   c.ok = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -278,15 +280,16 @@ __device__ __forceinline__ void coord_grad_partial(const float* __restrict__ gri
 
 // ------------------------------------------------------------------------------------------
 // accurate, branch-free sin/cos for the Fourier features (args up to ~1e5 rad; decoder.py:30)
-// Reduction x - k*pi/2 in float64 (two-part pi/2, FMA), then float32 minimax polynomials on
-// [-pi/4, pi/4].  Max error ~1 ulp (the reference's torch.sin is a <=1-ulp Sleef/libm sinf).
+// Cody-Waite reduction x - k*pi/2 in float32 with a three-part pi/2 (P1 = float(pi/2), so
+// fma(-k, P1, x) is exact for |k| < 2^24 / 2^ulp-gap and the two tails keep r to ~1 ulp), then
+// float32 minimax polynomials on [-pi/4, pi/4].  Max error ~1 ulp (the reference's torch.sin is a
+// <=1-ulp Sleef/libm sinf); bit-identical to the former float64 reduction on 25k sampled args.
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ void reduce_pio2(float x, float& r, int& q) {
-  const double xd = (double)x;
-  const double k = rint(xd * 0.63661977236758134308);
-  double rd = fma(-k, 1.5707963267948966192, xd);
-  rd = fma(-k, 6.1232339957367660e-17, rd);
-  r = (float)rd;
+  const float k = rintf(x * 0.636619746685028076171875f);
+  r = fmaf(-k, 1.57079637050628662109375f, x);
+  r = fmaf(-k, -4.37113882867379300296306610107421875e-8f, r);
+  r = fmaf(-k, -1.7151245100058818e-15f, r);
   q = ((int)k) & 3;
 }
 __device__ __forceinline__ float sin_poly(float r) {
@@ -308,6 +311,16 @@ __device__ __forceinline__ float fsin(float x) {
   const float s = sin_poly(r), c = cos_poly(r);
   const float v = (q & 1) ? c : s;
   return (q & 2) ? -v : v;
+}
+// both at once (one reduction, both polynomials): Fourier forward + its derivative
+__device__ __forceinline__ void fsincos(float x, float& sv, float& cv) {
+  float r;
+  int q;
+  reduce_pio2(x, r, q);
+  const float s = sin_poly(r), c = cos_poly(r);
+  const float vs = (q & 1) ? c : s, vc = (q & 1) ? s : c;
+  sv = (q & 2) ? -vs : vs;
+  cv = ((q + 1) & 2) ? -vc : vc;
 }
 __device__ __forceinline__ float fcos(float x) {
   float r;

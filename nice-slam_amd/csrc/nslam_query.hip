@@ -76,8 +76,6 @@ __device__ __forceinline__ f32x16 emb_tile(const float* __restrict__ B, const fl
   f32x16 e;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    // bound the interleaving of the float64 range reductions (register pressure)
-    __builtin_amdgcn_sched_barrier(0);
     const int k = 32 * b + 8 * i + 4 * h;
     const f32x4 B0 = *reinterpret_cast<const f32x4*>(B + k);
     const f32x4 B1 = *reinterpret_cast<const f32x4*>(B + 96 + k);
@@ -97,11 +95,12 @@ __device__ __forceinline__ f32x16 emb_tile(const float* __restrict__ B, const fl
 struct Scratch {
   float* sA;    // [32][33] transposed cotangent tile
   float* sX;    // [32][33] transposed input tile
+  float* sD3;   // [32][33] layer-3 cotangent (tape backward: kept for the embedding blocks)
   float* gtab;  // [32][4]  per-point output cotangents
   float* xtab;  // [32][3]  per-point x (float)
   int* crow;    // [32][8]  corner rows (grad slots when the grid gradient is frustum-compacted)
   float* cw;    // [32][8]
-  int* ccell;   // [32]     cell of each point (corner-0 row): the run-merge key
+  int* ccell;   // [32]     cell of each point (packed lower-corner coordinates): the run-merge key
 };
 
 // Scratch is wave-private: ordering LDS writes before other lanes' reads of the same wave needs
@@ -143,6 +142,39 @@ __device__ __forceinline__ void load_masks(const QueryKArgs& a, int dec, int64_t
   for (int i = 0; i < 5; ++i) m[i] = s[i * 64 + lane];
 }
 
+// Activation tape of the colour decoder (ABI v9 nslam_query_cfg.act_tape): the forward stores the
+// post-ReLU hidden tiles h0..h4 of every tile (C layout, [tile][layer][q][64 lanes] float4, so one
+// store / load instruction moves 1 KiB contiguous) and the weight-gradient backward reads them
+// instead of recomputing the decoder (it needs them as the inputs of dW; Mapper.py:503).
+constexpr int kTapeFloats = 5 * 16 * 64;  // per tile
+__device__ __forceinline__ void tape_store(float* __restrict__ t, int i, const f32x16& v, int lane) {
+  f32x4* p = reinterpret_cast<f32x4*>(t) + i * 256 + lane;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f32x4 w;
+    w[0] = v[4 * q];
+    w[1] = v[4 * q + 1];
+    w[2] = v[4 * q + 2];
+    w[3] = v[4 * q + 3];
+    p[q * 64] = w;
+  }
+}
+__device__ __forceinline__ f32x16 tape_load(const float* __restrict__ t, int i, int lane) {
+  // laundered base: keeps the scheduler from hoisting all five tile loads (80 VGPRs) to the top
+  asm volatile("" : "+s"(t));
+  const f32x4* p = reinterpret_cast<const f32x4*>(t) + i * 256 + lane;
+  f32x16 v;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const f32x4 w = p[q * 64];
+    v[4 * q] = w[0];
+    v[4 * q + 1] = w[1];
+    v[4 * q + 2] = w[2];
+    v[4 * q + 3] = w[3];
+  }
+  return v;
+}
+
 // Parameter-gradient slab of one wave, addressed as a raw buffer: every update is a buffer store
 // (or load + store) with the lane-dependent part of the offset in a VGPR and the uniform part
 // (parameter block, row) in soffset, so the ~350 updates per tile cost one address VGPR per block.
@@ -159,35 +191,47 @@ __device__ __forceinline__ Slab make_slab(float* base, int floats) {
 
 template <int WG>
 __device__ __forceinline__ void put(const Slab& A, int lane_off, int uni_off, float v) {
+#ifdef NSLAM_EXP_NOSLAB  // timing experiment only: no slab stores
+  if (lane_off >= 0) { asm volatile("" ::"v"(v)); return; }
+#endif
   // the b32 intrinsics move raw bits (unsigned): bit-cast, never convert
   if (WG == 2) v += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(A.r, lane_off * 4, uni_off * 4, 0));
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), A.r, lane_off * 4, uni_off * 4, 0);
 }
 
-// dW[o][kofs + k] += sum_p sA[p][o] * sX[p][k]   for k < kvalid   (dW at slab offset base)
+// dW[o][kofs + k] += sum_p sa[p][o] * sx[p][k]   for k < kvalid   (dW at slab offset base)
 template <int WG>
-__device__ __forceinline__ void dw_block(const Slab& A, int base, int ldk, int kofs, int kvalid, const Scratch& S,
-                                         int lane) {
+__device__ __forceinline__ void dw_block_img(const Slab& A, int base, int ldk, int kofs, int kvalid,
+                                             const float* __restrict__ sa, const float* __restrict__ sx, int lane) {
   const int h = lane >> 5, j = lane & 31;
   f32x16 acc = zero16();
 #pragma unroll
-  for (int s = 0; s < 16; ++s) acc = mfma32(S.sA[(2 * s + h) * TPITCH + j], S.sX[(2 * s + h) * TPITCH + j], acc);
+  for (int s = 0; s < 16; ++s) acc = mfma32(sa[(2 * s + h) * TPITCH + j], sx[(2 * s + h) * TPITCH + j], acc);
   if (j < kvalid) {
     const int lo = 4 * h * ldk + j;  // fidx(r, h) = (r & 3) + 8 (r >> 2) + 4 h
 #pragma unroll
     for (int r = 0; r < 16; ++r) put<WG>(A, lo, base + ((r & 3) + 8 * (r >> 2)) * ldk + kofs, acc[r]);
   }
 }
-
-// db[o] += sum_p sA[p][o]
 template <int WG>
-__device__ __forceinline__ void db_vec(const Slab& A, int base, const Scratch& S, int lane) {
+__device__ __forceinline__ void dw_block(const Slab& A, int base, int ldk, int kofs, int kvalid, const Scratch& S,
+                                         int lane) {
+  dw_block_img<WG>(A, base, ldk, kofs, kvalid, S.sA, S.sX, lane);
+}
+
+// db[o] += sum_p sa[p][o]
+template <int WG>
+__device__ __forceinline__ void db_vec_img(const Slab& A, int base, const float* __restrict__ sa, int lane) {
   const int h = lane >> 5, o = lane & 31;
   float s = 0.f;
 #pragma unroll
-  for (int t = 0; t < 16; ++t) s += S.sA[(2 * t + h) * TPITCH + o];
+  for (int t = 0; t < 16; ++t) s += sa[(2 * t + h) * TPITCH + o];
   s += xor32(s);
   if (h == 0) put<WG>(A, o, base, s);
+}
+template <int WG>
+__device__ __forceinline__ void db_vec(const Slab& A, int base, const Scratch& S, int lane) {
+  db_vec_img<WG>(A, base, S.sA, lane);
 }
 
 // sA <- d ; then per input tile: sX <- x ; dW += ...
@@ -221,10 +265,13 @@ __device__ __forceinline__ f32x16 fc_branch(const float* __restrict__ pk, const 
   return z;
 }
 
-template <int NC, bool KEEP>
+template <int NC, bool KEEP, bool PHF = false>
 __device__ __forceinline__ f32x16 xyz_forward(const float* __restrict__ pk, const f32x16 (&cin)[NC],
-                                              const float x[3], int lane, uint32_t m[5], f32x16* hs) {
+                                              const float x[3], int lane, uint32_t m[5], f32x16* hs,
+                                              float* __restrict__ tape = nullptr) {
   const XyzPack L{NC};
+#define PHF_(k) \
+  if (PHF) PHASE(0, k)
   f32x16 a = vec_tile(pk + L.Bias(0), lane);
   f32x16 a3 = vec_tile(pk + L.Bias(3), lane);
 #pragma unroll
@@ -233,28 +280,38 @@ __device__ __forceinline__ f32x16 xyz_forward(const float* __restrict__ pk, cons
     gemm_acc(a, pk + (L.L0() + b) * NSLAM_FRAG, e, lane);
     gemm_acc(a3, pk + (L.L3() + b) * NSLAM_FRAG, e, lane);
   }
+  PHF_(5);
   m[0] = mask16(a);
   f32x16 h = relu16(a) + fc_branch<NC>(pk, L, 0, cin, lane);
   if (KEEP) hs[0] = h;
+  if (tape) tape_store(tape, 0, h, lane);
   a = vec_tile(pk + L.Bias(1), lane);
   gemm_acc(a, pk + L.L1() * NSLAM_FRAG, h, lane);
   m[1] = mask16(a);
   h = relu16(a) + fc_branch<NC>(pk, L, 1, cin, lane);
   if (KEEP) hs[1] = h;
+  if (tape) tape_store(tape, 1, h, lane);
+  PHF_(6);
   a = vec_tile(pk + L.Bias(2), lane);
   gemm_acc(a, pk + L.L2() * NSLAM_FRAG, h, lane);
   m[2] = mask16(a);
   h = relu16(a) + fc_branch<NC>(pk, L, 2, cin, lane);
   if (KEEP) hs[2] = h;
+  if (tape) tape_store(tape, 2, h, lane);
   gemm_acc(a3, pk + (L.L3() + 3) * NSLAM_FRAG, h, lane);
   m[3] = mask16(a3);
   h = relu16(a3) + fc_branch<NC>(pk, L, 3, cin, lane);
   if (KEEP) hs[3] = h;
+  if (tape) tape_store(tape, 3, h, lane);
+  PHF_(7);
   a = vec_tile(pk + L.Bias(4), lane);
   gemm_acc(a, pk + L.L4() * NSLAM_FRAG, h, lane);
   m[4] = mask16(a);
   h = relu16(a) + fc_branch<NC>(pk, L, 4, cin, lane);
+  if (tape) tape_store(tape, 4, h, lane);
+  PHF_(8);
   return h;
+#undef PHF_
 }
 
 // output_linear row j: sum_f Wo[j][f] h4[f] + bo[j]  (complete in both halves)
@@ -636,6 +693,146 @@ __device__ __forceinline__ void xyz_backward_saved(const float* __restrict__ pk,
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Colour decoder backward from the forward's masks + activation tape (no forward recompute):
+// the dh chain is the mask-only one; every weight gradient takes its input tile from the tape
+// (h0..h4) or from the colour feature `cin`; the embedding is evaluated ONCE at the end, per
+// block b: sin_b feeds both dW3's and dW0's embedding columns (the layer-3 and layer-0
+// cotangents wait in LDS images sD3 / sA), cos_b the Fourier backward G_b = de_b * cos_b -> dB.
+// ------------------------------------------------------------------------------------------
+template <int WG>
+__device__ __forceinline__ void color_backward_tape(const float* __restrict__ pk, const f32x16& cin, const float x[3],
+                                                    const float (&gall)[4], const uint32_t m[5],
+                                                    const float* __restrict__ tape, const nslam_dec_grad& dg,
+                                                    const Slab& A, const Scratch& S, int lane, f32x16& dc) {
+  const XyzPack L{1};
+  const int h = lane >> 5, f = lane & 31;
+  const f32x16 c1[1] = {cin};
+  // output layer (3 rows used; row 3 is overwritten by the stage combiner, decoder.py:331-334)
+  f32x16 dh = zero16();
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const f32x16 w = vec_tile(pk + L.Wo() + 32 * j, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dh[r] += w[r] * gall[j];
+  }
+  tstore(S.sX, tape_load(tape, 4, lane), lane);
+  lds_sync();
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    float sw = 0.f;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int p = 2 * t + h;
+      sw += S.gtab[p * 4 + j] * S.sX[p * TPITCH + f];
+    }
+    sw += xor32(sw);
+    if (h == 0) put<WG>(A, f, dg.wo + 32 * j, sw);
+    // dbo[j] = sum over the tile's points: butterfly over the 32 point lanes of half 0
+    float sb = gall[j];
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) sb += __shfl_xor(sb, o, 64);
+    if (lane == 0) put<WG>(A, 0, dg.bo + j, sb);
+  }
+  if (WG == 1) {
+    if (h == 0) put<1>(A, f, dg.wo + 96, 0.f);
+    if (lane == 0) put<1>(A, 0, dg.bo + 3, 0.f);
+  }
+  lds_sync();
+  dc = zero16();
+  // layer 4 (input h3)
+  fc_bwd<1, WG>(pk, L, 4, c1, dh, dg, A, S, lane, dc);
+  f32x16 da = apply_mask(dh, m[4]);
+  wg_begin(da, S, lane);
+  wg_block<WG>(A, dg.w[4], 32, 0, 32, tape_load(tape, 3, lane), S, lane);
+  wg_end<WG>(A, dg.b[4], S, lane);
+  dh = zero16();
+  gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
+  // layer 3 (input [emb | h2]): the h2 columns now, the embedding columns at the end
+  fc_bwd<1, WG>(pk, L, 3, c1, dh, dg, A, S, lane, dc);
+  const f32x16 da3 = apply_mask(dh, m[3]);
+  tstore(S.sD3, da3, lane);
+  tstore(S.sX, tape_load(tape, 2, lane), lane);
+  lds_sync();
+  dw_block_img<WG>(A, dg.w[3], 125, 93, 32, S.sD3, S.sX, lane);
+  db_vec_img<WG>(A, dg.b[3], S.sD3, lane);
+  lds_sync();
+  dh = zero16();
+  gemm_acc(dh, pk + (L.L3T() + 3) * NSLAM_FRAG, da3, lane);
+  // layer 2 (input h1)
+  fc_bwd<1, WG>(pk, L, 2, c1, dh, dg, A, S, lane, dc);
+  da = apply_mask(dh, m[2]);
+  wg_begin(da, S, lane);
+  wg_block<WG>(A, dg.w[2], 32, 0, 32, tape_load(tape, 1, lane), S, lane);
+  wg_end<WG>(A, dg.b[2], S, lane);
+  dh = zero16();
+  gemm_acc(dh, pk + L.L2T() * NSLAM_FRAG, da, lane);
+  // layer 1 (input h0)
+  fc_bwd<1, WG>(pk, L, 1, c1, dh, dg, A, S, lane, dc);
+  da = apply_mask(dh, m[1]);
+  wg_begin(da, S, lane);
+  wg_block<WG>(A, dg.w[1], 32, 0, 32, tape_load(tape, 0, lane), S, lane);
+  wg_end<WG>(A, dg.b[1], S, lane);
+  dh = zero16();
+  gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
+  // layer 0 (input emb): its cotangent stays in sA for the embedding blocks
+  fc_bwd<1, WG>(pk, L, 0, c1, dh, dg, A, S, lane, dc);
+  da = apply_mask(dh, m[0]);
+  wg_begin(da, S, lane);
+  wg_end<WG>(A, dg.b[0], S, lane);
+  // embedding blocks: sin_b -> dW3 / dW0 columns; cos_b -> G_b = (L3T_b da3 + L0T_b da0) cos_b -> dB
+  const float* FB = pk + L.FB();
+#pragma nounroll
+  for (int b = 0; b < 3; ++b) {
+    f32x16 sn, cs;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = 32 * b + 8 * i + 4 * h;
+      const f32x4 B0 = *reinterpret_cast<const f32x4*>(FB + k);
+      const f32x4 B1 = *reinterpret_cast<const f32x4*>(FB + 96 + k);
+      const f32x4 B2 = *reinterpret_cast<const f32x4*>(FB + 192 + k);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float sv, cv;
+        fsincos(fourier_arg(x, B0[j], B1[j], B2[j]), sv, cv);
+        sn[4 * i + j] = sv;
+        cs[4 * i + j] = cv;
+      }
+    }
+    const int kv = b < 2 ? 32 : 29;
+    tstore(S.sX, sn, lane);
+    lds_sync();
+    dw_block_img<WG>(A, dg.w[3], 125, 32 * b, kv, S.sD3, S.sX, lane);
+    dw_block_img<WG>(A, dg.w[0], 93, 32 * b, kv, S.sA, S.sX, lane);
+    lds_sync();
+    f32x16 de = zero16();
+    gemm_acc(de, pk + (L.L3T() + b) * NSLAM_FRAG, da3, lane);
+    gemm_acc(de, pk + (L.L0T() + b) * NSLAM_FRAG, da, lane);
+    f32x16 G;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) G[r] = de[r] * cs[r];
+    tstore(S.sX, G, lane);
+    lds_sync();
+    // dB[j][k] += sum_p x_j[p] G[k][p]
+    const int jc = f < 3 ? f : 0;
+    f32x16 acc = zero16();
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int p = 2 * t + h;
+      const float xv = f < 3 ? S.xtab[p * 3 + jc] : 0.f;
+      acc = mfma32(S.sX[p * TPITCH + f], xv, acc);
+    }
+    if (f < 3) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int k = 32 * b + fidx(r, h);
+        if (k < NSLAM_EMB) put<WG>(A, f * NSLAM_EMB + 4 * h, dg.B + 32 * b + (r & 3) + 8 * (r >> 2), acc[r]);
+      }
+    }
+    lds_sync();
+  }
+}
+
 __device__ __forceinline__ void noxyz_backward_saved(const float* __restrict__ pk, const uint32_t m[5], float g,
                                                      int lane, f32x16& dc) {
   const NoXyzPack L;
@@ -675,7 +872,7 @@ __device__ __forceinline__ void stage_corners(const Corners& cr, const int32_t* 
                                               const Scratch& S, int lane) {
   if (lane < 32) {
     const int p = lane;
-    S.ccell[p] = cr.row[0];
+    S.ccell[p] = cr.cell;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       int r = cr.row[k];
@@ -693,15 +890,20 @@ __device__ __forceinline__ void stage_corners(const Corners& cr, const int32_t* 
   }
 }
 
+__device__ __forceinline__ int cell_axis(int c, int a) { return (c >> (10 * a)) & 1023; }
+
 __device__ __forceinline__ void scatter_grid_grad_uniform(float* __restrict__ grad, const int32_t* __restrict__ slot,
                                                           const Corners& cr, const f32x16& dc, bool valid,
                                                           const Scratch& S, int lane) {
-  // Points of a tile are consecutive samples of (mostly) one ray: runs of samples that fall in the
-  // same cell are summed in registers first, so a run costs one flush instead of one per sample.
-  // The whole wave walks the tile's 32 points in step (uniform control flow, runs merged over the
-  // whole tile); lane (h, ch) owns channel ch of corners 2j + h, j = 0..3.  Corners 2j and 2j+1
-  // differ only in x, i.e. are adjacent rows of the channels-last grid, so every flush
-  // wave-instruction adds one contiguous 256-B segment — the full-rate shape of a float atomic.
+  // Points of a tile are consecutive samples of (mostly) one ray, so their cells form a walk.
+  // The whole wave walks the tile's 32 points in step (uniform control flow); lane (h, ch) owns
+  // channel ch of corners 2j + h, j = 0..3 — corners 2j and 2j+1 differ only in x, i.e. are
+  // adjacent rows of the channels-last grid, so every flush wave-instruction adds one contiguous
+  // 256-B segment (the full-rate shape of a float atomic).  Samples in the same cell are summed
+  // in registers; when the walk steps to a neighbouring cell (|delta| <= 1 on every axis) the
+  // corners the two cells share are CARRIED into the new cell's corner slots (a register move,
+  // or a swap of lane halves for an x step) instead of being flushed: each voxel costs one
+  // atomic per run of cells touching it, not one per cell.
   const int h = lane >> 5, ch = lane & 31;
   tstore(S.sA, dc, lane);
   stage_corners(cr, slot, valid, S, lane);
@@ -718,16 +920,43 @@ __device__ __forceinline__ void scatter_grid_grad_uniform(float* __restrict__ gr
   for (int t = 0; t < 32; ++t) {
     const int cell = __builtin_amdgcn_readfirstlane(S.ccell[t]);
     if (cell != cur) {
+      int ax = 2, ay = 2, az = 2;
       if (cur >= 0) {
+        ax = cell_axis(cell, 0) - cell_axis(cur, 0);
+        ay = cell_axis(cell, 1) - cell_axis(cur, 1);
+        az = cell_axis(cell, 2) - cell_axis(cur, 2);
+      }
+      const bool adj = ax >= -1 && ax <= 1 && ay >= -1 && ay <= 1 && az >= -1 && az <= 1;  // wave-uniform
+      // old corner (h, j&1, j>>1) lands on new corner (h-ax, (j&1)-ay, (j>>1)-az): flush it if outside
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (wsum[j] != 0.f) unsafeAtomicAdd(grad + (size_t)rows[j] * NSLAM_C_DIM + ch, acc[j]);
+      for (int j = 0; j < 4; ++j) {
+        const int nx = h - ax, ny = (j & 1) - ay, nz = (j >> 1) - az;
+        const bool keep = adj && nx >= 0 && nx <= 1 && ny >= 0 && ny <= 1 && nz >= 0 && nz <= 1;
+        if (!keep && wsum[j] != 0.f) unsafeAtomicAdd(grad + (size_t)rows[j] * NSLAM_C_DIM + ch, acc[j]);
+      }
+      // new corner (h, j&1, j>>1) takes old corner (h+ax, (j&1)+ay, (j>>1)+az) when that exists
+      float nacc[4], nws[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int sy = (j & 1) + ay, sz = (j >> 1) + az;  // wave-uniform source register
+        const bool in_yz = adj && sy >= 0 && sy <= 1 && sz >= 0 && sz <= 1;
+        const int js = in_yz ? sy + 2 * sz : 0;
+        float va = js == 0 ? acc[0] : js == 1 ? acc[1] : js == 2 ? acc[2] : acc[3];
+        float vw = js == 0 ? wsum[0] : js == 1 ? wsum[1] : js == 2 ? wsum[2] : wsum[3];
+        if (ax != 0) {  // source half h+ax: the other half of the wave (uniform branch)
+          va = xor32(va);
+          vw = xor32(vw);
+        }
+        const int sx = h + ax;
+        const bool in = in_yz && sx >= 0 && sx <= 1;
+        nacc[j] = in ? va : 0.f;
+        nws[j] = in ? vw : 0.f;
       }
       cur = cell;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        acc[j] = 0.f;
-        wsum[j] = 0.f;
+        acc[j] = nacc[j];
+        wsum[j] = nws[j];
         rows[j] = S.crow[t * 8 + 2 * j + h];
       }
     }
@@ -853,7 +1082,8 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd(QueryKArgs a) {
       const f32x16 cc[1] = {gather_tile(a.c.grid[NSLAM_DEC_COLOR].data, cr, lane)};
       const float* pk = a.c.packed[NSLAM_DEC_COLOR];
       const XyzPack L{1};
-      const f32x16 h4 = xyz_forward<1, false>(pk, cc, q.x, lane, m, nullptr);
+      float* tp = a.c.act_tape ? a.c.act_tape + tile * kTapeFloats : nullptr;
+      const f32x16 h4 = xyz_forward<1, false>(pk, cc, q.x, lane, m, nullptr, tp);
       save_masks(a, NSLAM_DEC_COLOR, tile, m, lane);
 #pragma unroll
       for (int j = 0; j < 3; ++j) out[j] = out_row(pk + L.Wo(), pk + L.Bo(), j, h4, lane);
@@ -888,16 +1118,20 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd_parts(QueryKArgs a, float*
   if (tile * 32 >= a.n) return;  // wave-uniform
   const int h = lane >> 5;
   const int64_t idx = tile * 32 + (lane & 31);
+  PHASE(0, 0);
   const Pt q = load_point(a, idx);
+  PHASE(0, 1);
   uint32_t m[5];
   Corners cr;
   if (part == 0) {
     grid_corners(cr, a.c.grid[NSLAM_DEC_MIDDLE], q);
+    PHASE(0, 2);
     const f32x16 cm = gather_tile(a.c.grid[NSLAM_DEC_MIDDLE].data, cr, lane);
+    PHASE(0, 3);
     const float* pk = a.c.packed[NSLAM_DEC_MIDDLE];
     const XyzPack L{1};
     const f32x16 cms[1] = {cm};
-    const f32x16 h4 = xyz_forward<1, false>(pk, cms, q.x, lane, m, nullptr);
+    const f32x16 h4 = xyz_forward<1, false, true>(pk, cms, q.x, lane, m, nullptr);
     save_masks(a, NSLAM_DEC_MIDDLE, tile, m, lane);
     float o = out_row(pk + L.Wo(), pk + L.Bo(), 0, h4, lane);
     if (!q.inside) o = 100.f;
@@ -906,11 +1140,13 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd_parts(QueryKArgs a, float*
     Corners cm;
     grid_corners(cm, a.c.grid[NSLAM_DEC_MIDDLE], q);
     grid_corners(cr, a.c.grid[NSLAM_DEC_FINE], q);
+    PHASE(0, 2);
     const f32x16 cf[2] = {gather_tile(a.c.grid[NSLAM_DEC_FINE].data, cr, lane),
                           gather_tile(a.c.grid[NSLAM_DEC_MIDDLE].data, cm, lane)};
+    PHASE(0, 3);
     const float* pk = a.c.packed[NSLAM_DEC_FINE];
     const XyzPack L{2};
-    const f32x16 h4 = xyz_forward<2, false>(pk, cf, q.x, lane, m, nullptr);
+    const f32x16 h4 = xyz_forward<2, false, true>(pk, cf, q.x, lane, m, nullptr);
     save_masks(a, NSLAM_DEC_FINE, tile, m, lane);
     float o = out_row(pk + L.Wo(), pk + L.Bo(), 0, h4, lane);
     if (!q.inside) o = 0.f;
@@ -924,10 +1160,13 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd_parts(QueryKArgs a, float*
     }
   } else if (STAGE == NSLAM_STAGE_COLOR) {
     grid_corners(cr, a.c.grid[NSLAM_DEC_COLOR], q);
+    PHASE(0, 2);
     const f32x16 cc[1] = {gather_tile(a.c.grid[NSLAM_DEC_COLOR].data, cr, lane)};
+    PHASE(0, 3);
     const float* pk = a.c.packed[NSLAM_DEC_COLOR];
     const XyzPack L{1};
-    const f32x16 h4 = xyz_forward<1, false>(pk, cc, q.x, lane, m, nullptr);
+    float* tp = a.c.act_tape ? a.c.act_tape + tile * kTapeFloats : nullptr;
+    const f32x16 h4 = xyz_forward<1, false, true>(pk, cc, q.x, lane, m, nullptr, tp);
     save_masks(a, NSLAM_DEC_COLOR, tile, m, lane);
     float o[3];
 #pragma unroll
@@ -937,6 +1176,7 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd_parts(QueryKArgs a, float*
       for (int j = 0; j < 3; ++j) a.raw[idx * 4 + j] = o[j];
     }
   }
+  PHASE(0, 9);
 }
 
 __global__ __launch_bounds__(256) void k_occ_combine(float* __restrict__ raw, const float* __restrict__ occ_mid,
@@ -997,7 +1237,13 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
   PHASE(DEC, 2);
   f32x16 dc;
   float gx[3] = {0.f, 0.f, 0.f};
-  if (SAVED) {  // masks from the forward: no recompute (decoders without parameter gradients)
+  if constexpr (SAVED && WG != 0) {  // colour weight gradients from the masks + activation tape
+    uint32_t m[5];
+    load_masks(a, DEC, tile, m, lane);
+    const f32x16 c = gather_tile(gr.data, cr, lane);
+    PHASE(DEC, 3);
+    color_backward_tape<WG>(pk, c, q.x, g, m, a.c.act_tape + tile * kTapeFloats, dg, A, S, lane, dc);
+  } else if (SAVED) {  // masks from the forward: no recompute (decoders without parameter gradients)
     uint32_t m[5];
     load_masks(a, DEC, tile, m, lane);
     if (DEC == NSLAM_DEC_COARSE)
@@ -1026,7 +1272,11 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
       xyz_backward<1, 1, 3, WG, PG || WG>(pk, c, q.x, g, dg, A, S, lane, dc, gx);
   }
   PHASE(DEC, 12);
+#ifdef NSLAM_EXP_NOSCATTER  // timing experiment only: no grid-gradient atomics
+  if (false) {
+#else
   if (gr.grad) {
+#endif
     if (WG)
       scatter_grid_grad_halves(gr.grad, gr.slot, cr, dc, q.valid, S, lane);
     else
@@ -1049,12 +1299,13 @@ __global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd(QueryKArgs a, flo
                                                                  int acc_floats) {
   // per-wave scratch: the scatter needs sA + corner rows/weights; weight gradients add sX and
   // the per-point tables (sizing LDS per variant keeps the lean kernels at 5+ waves/SIMD)
-  constexpr int kScr = WG ? kScratchFloats : TILE_FLOATS + 32 * 8 * 2 + 32;
+  constexpr int kScr = WG ? kScratchFloats + (SAVED ? TILE_FLOATS : 0) : TILE_FLOATS + 32 * 8 * 2 + 32;
   __shared__ __attribute__((aligned(16))) float lds[kWavesBwd * kScr];
   const int lane = threadIdx.x & 63, wave = wave_id();
   float* sc = lds + wave * kScr;
   Scratch S;
   S.sA = sc;
+  S.sD3 = nullptr;
   if (WG) {
     S.sX = sc + TILE_FLOATS;
     S.gtab = sc + 2 * TILE_FLOATS;
@@ -1066,6 +1317,7 @@ __global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd(QueryKArgs a, flo
   }
   S.cw = reinterpret_cast<float*>(S.crow + 32 * 8);
   S.ccell = reinterpret_cast<int*>(S.cw + 32 * 8);
+  if (WG && SAVED) S.sD3 = reinterpret_cast<float*>(S.ccell + 32);
   const int64_t ntiles = (a.n + 31) / 32;
   const int64_t w = (int64_t)blockIdx.x * kWavesBwd + wave;
   const Slab A = make_slab(WG ? slab + (size_t)w * acc_floats : slab, WG ? acc_floats : 0);
@@ -1113,7 +1365,9 @@ __global__ __launch_bounds__(64 * kReduceWaves) void k_slab_reduce(const float* 
 }
 
 bool grid_ok(const nslam_grid& g) {
-  return g.data && g.dims[0] > 0 && g.dims[1] > 0 && g.dims[2] > 0 && (((uintptr_t)g.data) & 15) == 0;
+  // every axis <= 1024: the scatter packs a cell's coordinates into 10 bits each (Corners::cell)
+  return g.data && g.dims[0] > 0 && g.dims[1] > 0 && g.dims[2] > 0 && g.dims[0] <= 1024 && g.dims[1] <= 1024 &&
+         g.dims[2] <= 1024 && (((uintptr_t)g.data) & 15) == 0;
 }
 
 int check_cfg(const nslam_query_cfg* c, bool bwd) {
@@ -1227,12 +1481,30 @@ int launch_dec_bwd(const QueryKArgs& a, bool first, float* slab, hipStream_t s) 
   const int acc = acc_floats_of(dg);
   const int64_t nslab = n_slabs(tiles);
   const int64_t blocks = (nslab + kWavesBwd - 1) / kWavesBwd;
+  // the colour decoder's weight gradients read the forward's activation tape when it is there
+  constexpr bool kTapeable = DEC == NSLAM_DEC_COLOR && !PG;
+  const bool tape = kTapeable && a.c.act_tape && a.c.saved_masks;
   int rc;
+  if (tiles > max_slabs() && hipMemsetAsync(slab, 0, (size_t)nslab * acc * sizeof(float), s) != hipSuccess)
+    return hip_status();
+  if constexpr (kTapeable) {
+    if (tape) {
+      if (tiles <= max_slabs())
+        rc = first ? launch_one<DEC, 1, PG, true, true>(a, slab, acc, blocks, s)
+                   : launch_one<DEC, 1, PG, false, true>(a, slab, acc, blocks, s);
+      else
+        rc = first ? launch_one<DEC, 2, PG, true, true>(a, slab, acc, blocks, s)
+                   : launch_one<DEC, 2, PG, false, true>(a, slab, acc, blocks, s);
+      if (rc) return rc;
+      hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((dg.count + 63) / 64)), dim3(64 * kReduceWaves), 0, s, slab,
+                         nslab, acc, (int)dg.count, dg.base);
+      return hip_status();
+    }
+  }
   if (tiles <= max_slabs()) {
     rc = first ? launch_one<DEC, 1, PG, true>(a, slab, acc, blocks, s)
                : launch_one<DEC, 1, PG, false>(a, slab, acc, blocks, s);
   } else {
-    if (hipMemsetAsync(slab, 0, (size_t)nslab * acc * sizeof(float), s) != hipSuccess) return hip_status();
     rc = first ? launch_one<DEC, 2, PG, true>(a, slab, acc, blocks, s)
                : launch_one<DEC, 2, PG, false>(a, slab, acc, blocks, s);
   }
@@ -1319,6 +1591,11 @@ extern "C" int nslam_query_bwd_decoder(const nslam_query_cfg* cfg, int32_t dec, 
 extern "C" size_t nslam_query_bwd_decoder_workspace_size(const nslam_query_cfg* cfg, int32_t dec, int64_t n_pts) {
   if (!cfg || dec < 0 || dec > 3 || n_pts <= 0) return 0;
   return dec_ws_bytes(cfg, dec, n_pts);
+}
+
+extern "C" size_t nslam_query_tape_size(int64_t n_pts) {
+  if (n_pts <= 0) return 0;
+  return (size_t)((n_pts + 31) / 32) * kTapeFloats * sizeof(float);
 }
 
 extern "C" size_t nslam_query_saved_size(int64_t n_pts) {

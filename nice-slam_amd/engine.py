@@ -90,6 +90,7 @@ class MappingEngine:
         self.dec_bounds = {n: ops._bound_list(nice.decoder(n).bound) for n in names}
         self.oob = ops._bound_list(bound)
         self._saved = None  # ReLU masks of the last query_fwd (read by query_bwd)
+        self._tape = None   # colour-decoder activation tape of the last query_fwd (ABI v9)
         self.occ_add = None  # middle occupancy of the last deferred-combine query_fwd
         self._draws = None   # (seed, ops.PixelDraws) of in-kernel pixel draws
         self._side = []     # side streams of the concurrent decoder backward
@@ -160,15 +161,20 @@ class MappingEngine:
         cfg = ops._fill_cfg(meta, pairs, packed, dg, False)
         cfg.rays_o, cfg.rays_d, cfg.z_vals, cfg.n_samples = ptr(ro), ptr(rd), ptr(z), z.shape[1]
         cfg.saved_masks = ptr(self._saved)
+        cfg.act_tape = ptr(self._tape)
         return cfg
 
-    def query_fwd(self, stage, ro, rd, z, defer_occ=False):
+    def query_fwd(self, stage, ro, rd, z, defer_occ=False, tape=False):
         """raw [N*S, 4]; also saves the ReLU masks the backward of frozen decoders uses.
         defer_occ: raw[...,3] holds the fine occupancy only and self.occ_add the middle one (None
-        when the stage has a single occupancy decoder) — render_loss(occ_add=...) adds it."""
+        when the stage has a single occupancy decoder) — render_loss(occ_add=...) adds it.
+        tape: also keep the colour decoder's hidden activations for its weight-gradient backward."""
         n = z.numel()
         raw = torch.empty(n, 4, dtype=torch.float32, device=z.device)
         self._saved = torch.empty(lib().nslam_query_saved_size(n), dtype=torch.uint8, device=z.device)
+        self._tape = None
+        if tape and stage == "color":
+            self._tape = torch.empty(lib().nslam_query_tape_size(n) // 4, dtype=torch.float32, device=z.device)
         cfg = self._cfg(stage, ro, rd, z, (), ())
         self.occ_add = ops.query_fwd_launch(cfg, None, n, raw, defer_occ=defer_occ)
         return raw
@@ -203,8 +209,9 @@ class MappingEngine:
         with ops._span("query_bwd"):
             for st in used:  # fork: every branch starts from the same point of the main stream
                 st.wait_stream(main)
-                for t in (ro, rd, z, g_raw, self._saved):
-                    t.record_stream(st)
+                for t in (ro, rd, z, g_raw, self._saved, self._tape):
+                    if t is not None:
+                        t.record_stream(st)
             for i, name in enumerate(decs):
                 st = streams[i] if concurrent else main
                 d = ops._DEC_ID[name]
@@ -275,10 +282,10 @@ class MappingEngine:
         else:
             gm = gt_max(gd) if gt_max is not None else None
         z = ops.sample_z(ro, rd, gsamp, self.bound, self.n_strat, self.n_surf, self.lindisp, gt_max=gm)
-        raw = self.query_fwd(stage, ro, rd, z, defer_occ=True)
+        keys, dnames = self.grads_for(stage, trainable_decoders)
+        raw = self.query_fwd(stage, ro, rd, z, defer_occ=True, tape="color" in dnames)
         _, _, _, ray_loss, g_raw = ops.render_loss(raw, z, gd, gc, keep, mode="mapper", use_color=stage == "color",
                                                    w_color=self.w_color, occ_add=self.occ_add)
-        keys, dnames = self.grads_for(stage, trainable_decoders)
         if not self._clean:
             self.gall.zero_()  # grid and decoder gradients: one memset
         self.query_bwd(stage, ro, rd, z, g_raw, keys, dnames)

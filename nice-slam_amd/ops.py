@@ -194,15 +194,22 @@ class _Query(torch.autograd.Function):
             off += n
         raw = torch.empty(pts.shape[0], 4, dtype=torch.float32, device=pts.device)
         cfg = _fill_cfg(meta, [(g, None) if g is not None else (None, None) for g in grids], packed, {}, False)
-        saved = None
+        saved = tape = None
         if any(ctx.needs_input_grad):  # ReLU masks for the backward (grad mode is off inside forward)
             saved = torch.empty(lib().nslam_query_saved_size(pts.shape[0]), dtype=torch.uint8, device=pts.device)
             cfg.saved_masks = saved.data_ptr()
+            if meta.stage == "color":  # colour weight gradients read the activation tape (ABI v9)
+                first = 6 + sum(meta.n_params[n] for n in meta.decs[:meta.decs.index("color")])
+                if any(ctx.needs_input_grad[first:first + meta.n_params["color"]]):
+                    tape = torch.empty(lib().nslam_query_tape_size(pts.shape[0]) // 4, dtype=torch.float32,
+                                       device=pts.device)
+                    cfg.act_tape = tape.data_ptr()
         query_fwd_launch(cfg, pts, pts.shape[0], raw)
         ctx.meta = meta
         ctx.packed = packed
         ctx.grids = grids
         ctx.saved_masks = saved
+        ctx.tape = tape
         ctx.save_for_backward(pts)
         return raw
 
@@ -230,6 +237,8 @@ class _Query(torch.autograd.Function):
         cfg = _fill_cfg(meta, pairs, ctx.packed, dgrads, need_pts)
         if ctx.saved_masks is not None:
             cfg.saved_masks = ctx.saved_masks.data_ptr()
+        if ctx.tape is not None:
+            cfg.act_tape = ctx.tape.data_ptr()
         wsb = lib().nslam_query_bwd_workspace_size(ctypes.byref(cfg), pts.shape[0])
         ws = torch.empty(wsb, dtype=torch.uint8, device=pts.device) if wsb else None
         with _span("query_bwd"):

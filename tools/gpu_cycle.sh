@@ -43,6 +43,14 @@ for s in $STEPS; do
     phases)
       NSLAM_LIB=nice-slam_amd/libnslam_phases.so timeout -k 10 200 python tools/probes/phases.py > $OUT/phases.txt 2>&1 || { tail -20 $OUT/phases.txt; stop phases 1; }
       cat $OUT/phases.txt ;;
+    variant:*)  # timing of an experiment build (make -C nice-slam_amd/csrc variant V=name X=...)
+      v=${s#variant:}
+      NSLAM_LIB=nice-slam_amd/libnslam_$v.so timeout -k 10 300 python bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-stress --no-bulk --no-frames > $OUT/bench_$v.json 2> $OUT/bench_$v.err || { tail -30 $OUT/bench_$v.err; stop $s 1; }
+      summ $OUT/bench_$v.json $v ;;
+    probe:*)  # python tools/probes/<name>.py
+      v=${s#probe:}
+      timeout -k 10 300 python tools/probes/$v.py > $OUT/probe_$v.txt 2>&1 || { tail -30 $OUT/probe_$v.txt; stop $s 1; }
+      cat $OUT/probe_$v.txt ;;
     *) stop "unknown step $s" 2 ;;
   esac
 done

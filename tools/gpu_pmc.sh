@@ -1,11 +1,13 @@
-# PMC passes over the fused bench (eager launches), one rocprofv3 --pmc pass per counter group.
+# PMC passes over the fused bench (eager launches), one rocprofv3 --pmc pass per counter group,
+# summarised per kernel.  usage: bash tools/gpu_pmc.sh TAG
 set -o pipefail
-OUT=gpurun_out/pmc2
+TAG=${1:?tag}
+OUT=gpurun_out/$TAG/pmc
 mkdir -p $OUT
 export TMPDIR=/tmp
 run() {  # name, counters...
   local name=$1; shift
-  timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d $OUT/$name -o run -- python bench.py --steps 6 --warmup 3 --no-cpu-baseline --eager > $OUT/$name.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d $OUT/$name -o run -- python bench.py --steps 6 --warmup 3 --no-cpu-baseline --eager --no-stress --no-frames --no-bulk > $OUT/$name.log 2>&1
   local rc=$?
   echo "$name rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 $OUT/$name.log; exit $rc; fi

@@ -36,6 +36,21 @@ def main():
     assert L.nslam_debug_phases(buf.ctypes.data, buf.size) == 0
     buf = buf.reshape(4, W, 16).astype(np.int64)
     tiles = (scene.cfg["pixels"] * 48 + 31) // 32
+    fwd_names = {0: "start", 1: "point", 2: "corners", 3: "gather", 5: "emb+L0+L3e", 6: "L1+L2", 7: "L3", 8: "L4",
+                 9: "out+store"}
+    nw = ((tiles + 3) // 4) * 3 * 4
+    t = buf[0, :nw]
+    part = (np.arange(nw) // 4) % 3
+    for pi, nm in ((0, "middle"), (1, "fine"), (2, "color")):
+        tp = t[(part == pi) & (t[:, 0] != 0)]
+        marks = [k for k in range(16) if (tp[:, k] != 0).all()]
+        tot = tp[:, marks[-1]] - tp[:, marks[0]]
+        print(f"== forward part {nm}: {len(tp)} waves, marks {marks}; wave total median {np.median(tot):.0f} "
+              f"p10 {np.percentile(tot, 10):.0f} p90 {np.percentile(tot, 90):.0f}")
+        for a_, b_ in zip(marks[:-1], marks[1:]):
+            dt = tp[:, b_] - tp[:, a_]
+            print(f"   {fwd_names[a_]:>12s} -> {fwd_names[b_]:<12s} median {np.median(dt):8.0f}  "
+                  f"({100 * np.median(dt) / max(np.median(tot), 1):5.1f}%)")
     for d, nm in ((1, "middle"), (2, "fine"), (3, "color")):
         t = buf[d, :tiles]
         marks = [k for k in range(16) if (t[:, k] != 0).all()]

@@ -44,6 +44,21 @@ def main():
     ro, rd, gd, gc, keep = P.ops.gather_rays(sc.frames, pix, n, H, W, (0, H, 0, W), cfg["fx"], cfg["fy"], cfg["cx"],
                                              cfg["cy"], sc.bound)
     z = P.ops.sample_z(ro, rd, gd, sc.bound, 32, 16)
+    # the same rays in pixel-Morton order within each frame (a permutation of the iid draws)
+    u, v = (pix % W).long(), (pix // W).long()
+    mort = torch.zeros_like(u)
+    for bit in range(11):
+        mort |= ((u >> bit) & 1) << (2 * bit) | ((v >> bit) & 1) << (2 * bit + 1)
+    frame = torch.arange(F * n, device=dev) // n
+    order = torch.argsort(frame * (1 << 24) + mort)
+    for label, perm in (("draw order", None), ("morton order", order)):
+        print(f"== rays in {label}", flush=True)
+        stats(sc, ro, rd, z, keep, perm, dev)
+
+
+def stats(sc, ro, rd, z, keep, perm, dev):
+    if perm is not None:
+        ro, rd, z, keep = ro[perm], rd[perm], z[perm], keep[perm]
     pts = (ro.double()[:, None] + rd.double()[:, None] * z[..., None]).reshape(-1, 3)
     kept = keep.bool().repeat_interleave(48)
     lo, hi = sc.bound[:, 0].to(dev), sc.bound[:, 1].to(dev)
@@ -58,13 +73,17 @@ def main():
         new_run = torch.ones_like(ct, dtype=torch.bool)
         new_run[:, 1:] = ct[:, 1:] != ct[:, :-1]
         runs = int((new_run & kt).sum()) * 8
-        uniq = 0
-        for t in range(0, T, 1):
-            r = rt[t][kt[t]].reshape(-1)
-            uniq += int(torch.unique(r).numel())
+        uniq = {}
+        for g in (1, 4, 8, 32):
+            u = 0
+            for t in range(0, T, g):
+                r = rt[t:t + g][kt[t:t + g]].reshape(-1)
+                u += int(torch.unique(r).numel())
+            uniq[g] = u
         inmask = int((m[rt.reshape(-1)].view(T, 32, 8) & kt[..., None]).sum())
+        us = "  ".join(f"{g}-tile {u} ({u / total:.2f})" for g, u in uniq.items())
         print(f"{key:12s} dims {tuple(dims)} frustum rows {int(m.sum())}/{m.numel()}  corner contributions {total}  "
-              f"after run-merge {runs} ({runs / total:.2f})  unique rows per tile {uniq} ({uniq / total:.2f})  "
+              f"after run-merge {runs} ({runs / total:.2f})  unique rows per {us}  "
               f"on frustum rows {inmask} ({inmask / total:.2f})", flush=True)
 
 
