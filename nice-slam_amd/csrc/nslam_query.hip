@@ -1,1397 +1,9 @@
-// nslam_query.hip — fused point query for gfx950: normalise → trilinear gather (channels-last
-// grids) → Fourier embedding → tiny MLP decoders on MFMA (v_mfma_f32_32x32x2_f32) → stage
-// combiner → OOB logit, and its recompute-backward.
-//
-// Replaces, per point: Renderer.eval_points (src/utils/Renderer.py:23-61), NICE.forward
-// (src/conv_onet/models/decoder.py:312-342), MLP / MLP_no_xyz forward (decoder.py:177-203,
-// 262-274), sample_grid_feature (decoder.py:168-175, F.grid_sample) and the autograd backward of
-// all of them (Tracker.py:125, Mapper.py:503).
-//
-// Work decomposition: one wave = one tile of 32 points.  Each lane pair (l, l+32) owns one point;
-// the half h = l>>5 gathers/holds the 16 feature channels F(r,h) of that point (nslam_dev.h).
-#include "nslam_dev.h"
+// nslam_query.hip — C-ABI entry points of the fused point query (include/nslam.h): forward
+// launches, backward dispatch (the per-decoder backward launchers are compiled in
+// nslam_query_dec.hip), workspace / tape / mask sizes and the pack layout.
+#include "nslam_query_impl.h"
 
-namespace {
-
-struct QueryKArgs {
-  nslam_query_cfg c;
-  const double* pts;
-  int64_t n;
-  float* raw;          // fwd output [n][4]
-  const float* g_raw;  // bwd input  [n][4]
-  double* g_pts;       // bwd output [n][3]
-};
-
-// ------------------------------------------------------------------------------------------
-// per-point context
-// ------------------------------------------------------------------------------------------
-struct Pt {
-  double p[3];
-  float x[3];  // p.float() (decoder.py:189)
-  bool valid;
-  bool inside;
-};
-
-__device__ __forceinline__ Pt load_point(const QueryKArgs& a, int64_t idx) {
-  Pt q;
-  q.valid = idx < a.n;
-  const int64_t i = q.valid ? idx : 0;  // invalid tail lanes compute on a real point, write nothing
-  if (a.c.rays_o) {  // pts = rays_o + rays_d * z (float64, Renderer.py:172-174); host checks n < 2^31
-    const uint32_t r = (uint32_t)i / (uint32_t)a.c.n_samples;
-    const double z = a.c.z_vals[i];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) q.p[k] = (double)a.c.rays_o[r * 3 + k] + (double)a.c.rays_d[r * 3 + k] * z;
-  } else {
-    q.p[0] = a.pts[i * 3 + 0];
-    q.p[1] = a.pts[i * 3 + 1];
-    q.p[2] = a.pts[i * 3 + 2];
-  }
-  bool in = true;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    q.x[k] = (float)q.p[k];
-    in = in && (q.p[k] < a.c.bound_hi[k]) && (q.p[k] > a.c.bound_lo[k]);  // Renderer.py:43-46
-  }
-  q.inside = in;
-  return q;
-}
-
-__device__ __forceinline__ void grid_corners(Corners& cr, const nslam_grid& g, const Pt& q) {
-  float nc3[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) nc3[k] = norm_coord(q.p[k], g.lo[k], g.hi[k]);
-  make_corners(cr, nc3, g.dims);
-}
-
-// ------------------------------------------------------------------------------------------
-// Fourier embedding (decoder.py:26-30): block b, reg r of lane (h,p) is dim k = 32b + F(r,h)
-// ------------------------------------------------------------------------------------------
-__device__ __forceinline__ float fourier_arg(const float x[3], float b0, float b1, float b2) {
-  return fmaf(x[2], b2, fmaf(x[1], b1, x[0] * b0));
-}
-
-template <bool COS>
-__device__ __forceinline__ f32x16 emb_tile(const float* __restrict__ B, const float x[3], int b, int lane) {
-  const int h = lane >> 5;
-  f32x16 e;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int k = 32 * b + 8 * i + 4 * h;
-    const f32x4 B0 = *reinterpret_cast<const f32x4*>(B + k);
-    const f32x4 B1 = *reinterpret_cast<const f32x4*>(B + 96 + k);
-    const f32x4 B2 = *reinterpret_cast<const f32x4*>(B + 192 + k);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float t = fourier_arg(x, B0[j], B1[j], B2[j]);
-      e[4 * i + j] = COS ? fcos(t) : fsin(t);
-    }
-  }
-  return e;
-}
-
-// ------------------------------------------------------------------------------------------
-// LDS helpers for weight gradients (wave-private scratch, WG = 1 wave in the backward kernel)
-// ------------------------------------------------------------------------------------------
-struct Scratch {
-  float* sA;    // [32][33] transposed cotangent tile
-  float* sX;    // [32][33] transposed input tile
-  float* sD3;   // [32][33] layer-3 cotangent (tape backward: kept for the embedding blocks)
-  float* gtab;  // [32][4]  per-point output cotangents
-  float* xtab;  // [32][3]  per-point x (float)
-  int* crow;    // [32][8]  corner rows (grad slots when the grid gradient is frustum-compacted)
-  float* cw;    // [32][8]
-  int* ccell;   // [32]     cell of each point (packed lower-corner coordinates): the run-merge key
-};
-
-// Scratch is wave-private: ordering LDS writes before other lanes' reads of the same wave needs
-// only the wave's own LDS counter drained (and a compiler memory barrier), not a workgroup barrier.
-__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-
-// Phase timing (debug build only, make phases): lane 0 of each backward wave records s_memtime
-// at marks 0..15 of its tile into g_phase[decoder][wave][16].
-#ifdef NSLAM_PHASES
-constexpr int kPhaseWaves = 1 << 15;
-__device__ unsigned long long g_phase[4 * kPhaseWaves * 16];
-#define PHASE(dec, k)                                                                                     \
-  do {                                                                                                    \
-    const int64_t w_ = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);                     \
-    if ((threadIdx.x & 63) == 0 && w_ < kPhaseWaves)                                                      \
-      g_phase[((size_t)(dec) * kPhaseWaves + w_) * 16 + (k)] = __builtin_amdgcn_s_memtime();              \
-  } while (0)
-#else
-#define PHASE(dec, k) \
-  do {                \
-  } while (0)
-#endif
-
-// ReLU masks saved by the forward: [decoder][tile][layer][64 lanes] uint16 (one 128-B row per layer)
-__device__ __forceinline__ uint16_t* mask_slot(const QueryKArgs& a, int dec, int64_t tile) {
-  const int64_t ntiles = (a.n + 31) / 32;
-  return a.c.saved_masks + ((size_t)dec * ntiles + tile) * 5 * 64;
-}
-__device__ __forceinline__ void save_masks(const QueryKArgs& a, int dec, int64_t tile, const uint32_t m[5],
-                                           int lane) {
-  if (!a.c.saved_masks) return;
-  uint16_t* s = mask_slot(a, dec, tile);
-#pragma unroll
-  for (int i = 0; i < 5; ++i) s[i * 64 + lane] = (uint16_t)m[i];
-}
-__device__ __forceinline__ void load_masks(const QueryKArgs& a, int dec, int64_t tile, uint32_t m[5], int lane) {
-  const uint16_t* s = mask_slot(a, dec, tile);
-#pragma unroll
-  for (int i = 0; i < 5; ++i) m[i] = s[i * 64 + lane];
-}
-
-// Activation tape of the colour decoder (ABI v9 nslam_query_cfg.act_tape): the forward stores the
-// post-ReLU hidden tiles h0..h4 of every tile (C layout, [tile][layer][q][64 lanes] float4, so one
-// store / load instruction moves 1 KiB contiguous) and the weight-gradient backward reads them
-// instead of recomputing the decoder (it needs them as the inputs of dW; Mapper.py:503).
-constexpr int kTapeFloats = 5 * 16 * 64;  // per tile
-__device__ __forceinline__ void tape_store(float* __restrict__ t, int i, const f32x16& v, int lane) {
-  f32x4* p = reinterpret_cast<f32x4*>(t) + i * 256 + lane;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    f32x4 w;
-    w[0] = v[4 * q];
-    w[1] = v[4 * q + 1];
-    w[2] = v[4 * q + 2];
-    w[3] = v[4 * q + 3];
-    p[q * 64] = w;
-  }
-}
-__device__ __forceinline__ f32x16 tape_load(const float* __restrict__ t, int i, int lane) {
-  // laundered base: keeps the scheduler from hoisting all five tile loads (80 VGPRs) to the top
-  asm volatile("" : "+s"(t));
-  const f32x4* p = reinterpret_cast<const f32x4*>(t) + i * 256 + lane;
-  f32x16 v;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const f32x4 w = p[q * 64];
-    v[4 * q] = w[0];
-    v[4 * q + 1] = w[1];
-    v[4 * q + 2] = w[2];
-    v[4 * q + 3] = w[3];
-  }
-  return v;
-}
-
-// Parameter-gradient slab of one wave, addressed as a raw buffer: every update is a buffer store
-// (or load + store) with the lane-dependent part of the offset in a VGPR and the uniform part
-// (parameter block, row) in soffset, so the ~350 updates per tile cost one address VGPR per block.
-// A slab address is owned by one lane of one wave, so no atomics: WG == 1 (a wave's only tile)
-// stores, WG == 2 (waves walking several tiles over a zeroed slab) read-modify-writes; both are
-// per-lane program-ordered.
-struct Slab {
-  __amdgpu_buffer_rsrc_t r;
-};
-
-__device__ __forceinline__ Slab make_slab(float* base, int floats) {
-  return Slab{__builtin_amdgcn_make_buffer_rsrc(base, 0, floats * 4, 0x00020000)};
-}
-
-template <int WG>
-__device__ __forceinline__ void put(const Slab& A, int lane_off, int uni_off, float v) {
-#ifdef NSLAM_EXP_NOSLAB  // timing experiment only: no slab stores
-  if (lane_off >= 0) { asm volatile("" ::"v"(v)); return; }
-#endif
-  // the b32 intrinsics move raw bits (unsigned): bit-cast, never convert
-  if (WG == 2) v += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(A.r, lane_off * 4, uni_off * 4, 0));
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), A.r, lane_off * 4, uni_off * 4, 0);
-}
-
-// dW[o][kofs + k] += sum_p sa[p][o] * sx[p][k]   for k < kvalid   (dW at slab offset base)
-template <int WG>
-__device__ __forceinline__ void dw_block_img(const Slab& A, int base, int ldk, int kofs, int kvalid,
-                                             const float* __restrict__ sa, const float* __restrict__ sx, int lane) {
-  const int h = lane >> 5, j = lane & 31;
-  f32x16 acc = zero16();
-#pragma unroll
-  for (int s = 0; s < 16; ++s) acc = mfma32(sa[(2 * s + h) * TPITCH + j], sx[(2 * s + h) * TPITCH + j], acc);
-  if (j < kvalid) {
-    const int lo = 4 * h * ldk + j;  // fidx(r, h) = (r & 3) + 8 (r >> 2) + 4 h
-#pragma unroll
-    for (int r = 0; r < 16; ++r) put<WG>(A, lo, base + ((r & 3) + 8 * (r >> 2)) * ldk + kofs, acc[r]);
-  }
-}
-template <int WG>
-__device__ __forceinline__ void dw_block(const Slab& A, int base, int ldk, int kofs, int kvalid, const Scratch& S,
-                                         int lane) {
-  dw_block_img<WG>(A, base, ldk, kofs, kvalid, S.sA, S.sX, lane);
-}
-
-// db[o] += sum_p sa[p][o]
-template <int WG>
-__device__ __forceinline__ void db_vec_img(const Slab& A, int base, const float* __restrict__ sa, int lane) {
-  const int h = lane >> 5, o = lane & 31;
-  float s = 0.f;
-#pragma unroll
-  for (int t = 0; t < 16; ++t) s += sa[(2 * t + h) * TPITCH + o];
-  s += xor32(s);
-  if (h == 0) put<WG>(A, o, base, s);
-}
-template <int WG>
-__device__ __forceinline__ void db_vec(const Slab& A, int base, const Scratch& S, int lane) {
-  db_vec_img<WG>(A, base, S.sA, lane);
-}
-
-// sA <- d ; then per input tile: sX <- x ; dW += ...
-__device__ __forceinline__ void wg_begin(const f32x16& d, const Scratch& S, int lane) { tstore(S.sA, d, lane); }
-template <int WG>
-__device__ __forceinline__ void wg_block(const Slab& A, int base, int ldk, int kofs, int kvalid, const f32x16& x,
-                                         const Scratch& S, int lane) {
-  tstore(S.sX, x, lane);
-  lds_sync();
-  dw_block<WG>(A, base, ldk, kofs, kvalid, S, lane);
-  lds_sync();
-}
-template <int WG>
-__device__ __forceinline__ void wg_end(const Slab& A, int base, const Scratch& S, int lane) {
-  lds_sync();
-  db_vec<WG>(A, base, S, lane);
-  lds_sync();
-}
-
-// ------------------------------------------------------------------------------------------
-// MLP with Fourier embedding (decoder.py:177-203): forward
-//   layer-3's embedding product is formed right after layer 0, so the 48-register embedding
-//   dies early (the MFMA work is unchanged).
-// ------------------------------------------------------------------------------------------
-template <int NC>
-__device__ __forceinline__ f32x16 fc_branch(const float* __restrict__ pk, const XyzPack& L, int i,
-                                            const f32x16 (&cin)[NC], int lane) {
-  f32x16 z = vec_tile(pk + L.BiasC(i), lane);
-#pragma unroll
-  for (int c = 0; c < NC; ++c) gemm_acc(z, pk + L.FC(i, c) * NSLAM_FRAG, cin[c], lane);
-  return z;
-}
-
-template <int NC, bool KEEP, bool PHF = false>
-__device__ __forceinline__ f32x16 xyz_forward(const float* __restrict__ pk, const f32x16 (&cin)[NC],
-                                              const float x[3], int lane, uint32_t m[5], f32x16* hs,
-                                              float* __restrict__ tape = nullptr) {
-  const XyzPack L{NC};
-#define PHF_(k) \
-  if (PHF) PHASE(0, k)
-  f32x16 a = vec_tile(pk + L.Bias(0), lane);
-  f32x16 a3 = vec_tile(pk + L.Bias(3), lane);
-#pragma unroll
-  for (int b = 0; b < 3; ++b) {
-    const f32x16 e = emb_tile<false>(pk + L.FB(), x, b, lane);
-    gemm_acc(a, pk + (L.L0() + b) * NSLAM_FRAG, e, lane);
-    gemm_acc(a3, pk + (L.L3() + b) * NSLAM_FRAG, e, lane);
-  }
-  PHF_(5);
-  m[0] = mask16(a);
-  f32x16 h = relu16(a) + fc_branch<NC>(pk, L, 0, cin, lane);
-  if (KEEP) hs[0] = h;
-  if (tape) tape_store(tape, 0, h, lane);
-  a = vec_tile(pk + L.Bias(1), lane);
-  gemm_acc(a, pk + L.L1() * NSLAM_FRAG, h, lane);
-  m[1] = mask16(a);
-  h = relu16(a) + fc_branch<NC>(pk, L, 1, cin, lane);
-  if (KEEP) hs[1] = h;
-  if (tape) tape_store(tape, 1, h, lane);
-  PHF_(6);
-  a = vec_tile(pk + L.Bias(2), lane);
-  gemm_acc(a, pk + L.L2() * NSLAM_FRAG, h, lane);
-  m[2] = mask16(a);
-  h = relu16(a) + fc_branch<NC>(pk, L, 2, cin, lane);
-  if (KEEP) hs[2] = h;
-  if (tape) tape_store(tape, 2, h, lane);
-  gemm_acc(a3, pk + (L.L3() + 3) * NSLAM_FRAG, h, lane);
-  m[3] = mask16(a3);
-  h = relu16(a3) + fc_branch<NC>(pk, L, 3, cin, lane);
-  if (KEEP) hs[3] = h;
-  if (tape) tape_store(tape, 3, h, lane);
-  PHF_(7);
-  a = vec_tile(pk + L.Bias(4), lane);
-  gemm_acc(a, pk + L.L4() * NSLAM_FRAG, h, lane);
-  m[4] = mask16(a);
-  h = relu16(a) + fc_branch<NC>(pk, L, 4, cin, lane);
-  if (tape) tape_store(tape, 4, h, lane);
-  PHF_(8);
-  return h;
-#undef PHF_
-}
-
-// output_linear row j: sum_f Wo[j][f] h4[f] + bo[j]  (complete in both halves)
-__device__ __forceinline__ float out_row(const float* __restrict__ Wo, const float* __restrict__ bo, int j,
-                                         const f32x16& h4, int lane) {
-  const f32x16 w = vec_tile(Wo + 32 * j, lane);
-  float s = 0.f;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) s += w[r] * h4[r];
-  return (s + xor32(s)) + bo[j];
-}
-
-// ------------------------------------------------------------------------------------------
-// MLP with Fourier embedding: backward (forward recomputed first).
-//   gall[GOFS + j], j < NOUT : cotangents of the decoder outputs (per point, both halves)
-//   dc : out, d/d(feature block 0) (C layout);  gx : out, d/dx through the embedding (if EMBG)
-// Parameter gradients (WG) go through LDS transposes + MFMA over the 32 points and are added
-// with atomics shaped as two 128-B row segments.
-// ------------------------------------------------------------------------------------------
-template <int NC, int WG>
-__device__ __forceinline__ void fc_bwd(const float* __restrict__ pk, const XyzPack& L, int i,
-                                       const f32x16 (&cin)[NC], const f32x16& dh, const nslam_dec_grad& dg,
-                                       const Slab& A, const Scratch& S, int lane, f32x16& dc) {
-  gemm_acc(dc, pk + L.FCT(i) * NSLAM_FRAG, dh, lane);  // dz_i = dh_i
-  if (WG) {
-    wg_begin(dh, S, lane);
-#pragma unroll
-    for (int c = 0; c < NC; ++c) wg_block<WG>(A, dg.wc[i], 32 * NC, 32 * c, 32, cin[c], S, lane);
-    wg_end<WG>(A, dg.bc[i], S, lane);
-  }
-}
-
-template <int NC, int NOUT, int GOFS, int WG, bool EMBG>
-__device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const f32x16 (&cin)[NC],
-                                             const float x[3], const float (&gall)[4], const nslam_dec_grad& dg,
-                                             const Slab& A, const Scratch& S, int lane, f32x16& dc, float gx[3]) {
-  const XyzPack L{NC};
-  constexpr int DEC_ = NOUT == 3 ? 3 : (NC == 2 ? 2 : 1);
-  const int h = lane >> 5;
-  uint32_t m[5];
-  f32x16 hs[4];
-  const f32x16 h4 = xyz_forward<NC, WG != 0>(pk, cin, x, lane, m, hs);
-  PHASE(DEC_, 4);
-
-  // output layer: dh4 = Wo^T g
-  f32x16 dh = zero16();
-#pragma unroll
-  for (int j = 0; j < NOUT; ++j) {
-    const f32x16 w = vec_tile(pk + L.Wo() + 32 * j, lane);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dh[r] += w[r] * gall[GOFS + j];
-  }
-  if (WG) {
-    tstore(S.sX, h4, lane);
-    lds_sync();
-    const int f = lane & 31;
-#pragma unroll
-    for (int j = 0; j < NOUT; ++j) {
-      float s = 0.f;
-#pragma unroll
-      for (int t = 0; t < 16; ++t) {
-        const int p = 2 * t + h;
-        s += S.gtab[p * 4 + GOFS + j] * S.sX[p * TPITCH + f];
-      }
-      s += xor32(s);
-      if (h == 0) put<WG>(A, f, dg.wo + 32 * j, s);
-      if (lane == 0) {
-        float sb = 0.f;
-        for (int p = 0; p < 32; ++p) sb += S.gtab[p * 4 + GOFS + j];
-        put<WG>(A, 0, dg.bo + j, sb);
-      }
-    }
-    if (WG == 1 && GOFS + NOUT < 4 && GOFS == 0) {  // colour: output row 3 is never used, store zeros
-#pragma unroll
-      for (int j = NOUT; j < 4; ++j) {
-        if (h == 0) put<1>(A, f, dg.wo + 32 * j, 0.f);
-        if (lane == 0) put<1>(A, 0, dg.bo + j, 0.f);
-      }
-    }
-    lds_sync();
-  }
-  dc = zero16();
-  const float* FB = pk + L.FB();
-  PHASE(DEC_, 5);
-
-  // layer 4
-  fc_bwd<NC, WG>(pk, L, 4, cin, dh, dg, A, S, lane, dc);
-  f32x16 da = apply_mask(dh, m[4]);
-  if (WG) {
-    wg_begin(da, S, lane);
-    wg_block<WG>(A, dg.w[4], 32, 0, 32, hs[3], S, lane);
-    wg_end<WG>(A, dg.b[4], S, lane);
-  }
-  dh = zero16();
-  gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
-  PHASE(DEC_, 6);
-  // layer 3 (input = [emb | h2])
-  fc_bwd<NC, WG>(pk, L, 3, cin, dh, dg, A, S, lane, dc);
-  const f32x16 da3 = apply_mask(dh, m[3]);
-  if (WG) {
-    wg_begin(da3, S, lane);
-#pragma unroll
-    for (int b = 0; b < 3; ++b)
-      wg_block<WG>(A, dg.w[3], 125, 32 * b, b < 2 ? 32 : 29, emb_tile<false>(FB, x, b, lane), S, lane);
-    wg_block<WG>(A, dg.w[3], 125, 93, 32, hs[2], S, lane);
-    wg_end<WG>(A, dg.b[3], S, lane);
-  }
-  dh = zero16();
-  gemm_acc(dh, pk + (L.L3T() + 3) * NSLAM_FRAG, da3, lane);
-  PHASE(DEC_, 7);
-  // layer 2
-  fc_bwd<NC, WG>(pk, L, 2, cin, dh, dg, A, S, lane, dc);
-  da = apply_mask(dh, m[2]);
-  if (WG) {
-    wg_begin(da, S, lane);
-    wg_block<WG>(A, dg.w[2], 32, 0, 32, hs[1], S, lane);
-    wg_end<WG>(A, dg.b[2], S, lane);
-  }
-  dh = zero16();
-  gemm_acc(dh, pk + L.L2T() * NSLAM_FRAG, da, lane);
-  PHASE(DEC_, 8);
-  // layer 1
-  fc_bwd<NC, WG>(pk, L, 1, cin, dh, dg, A, S, lane, dc);
-  da = apply_mask(dh, m[1]);
-  if (WG) {
-    wg_begin(da, S, lane);
-    wg_block<WG>(A, dg.w[1], 32, 0, 32, hs[0], S, lane);
-    wg_end<WG>(A, dg.b[1], S, lane);
-  }
-  dh = zero16();
-  gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
-  PHASE(DEC_, 9);
-  // layer 0 (input = emb)
-  fc_bwd<NC, WG>(pk, L, 0, cin, dh, dg, A, S, lane, dc);
-  da = apply_mask(dh, m[0]);
-  if (WG) {
-    wg_begin(da, S, lane);
-#pragma unroll
-    for (int b = 0; b < 3; ++b)
-      wg_block<WG>(A, dg.w[0], 93, 32 * b, b < 2 ? 32 : 29, emb_tile<false>(FB, x, b, lane), S, lane);
-    wg_end<WG>(A, dg.b[0], S, lane);
-  }
-
-  PHASE(DEC_, 10);
-  // Fourier features: de_b = L3T_b da3 + L0T_b da0 ; G = de * cos(theta)
-  gx[0] = gx[1] = gx[2] = 0.f;
-  if (EMBG) {
-#pragma unroll
-    for (int b = 0; b < 3; ++b) {
-      f32x16 de = zero16();
-      gemm_acc(de, pk + (L.L3T() + b) * NSLAM_FRAG, da3, lane);
-      gemm_acc(de, pk + (L.L0T() + b) * NSLAM_FRAG, da, lane);
-      const f32x16 cs = emb_tile<true>(FB, x, b, lane);
-      f32x16 G;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int k = 32 * b + 8 * i + 4 * h;
-        const f32x4 B0 = *reinterpret_cast<const f32x4*>(FB + k);
-        const f32x4 B1 = *reinterpret_cast<const f32x4*>(FB + 96 + k);
-        const f32x4 B2 = *reinterpret_cast<const f32x4*>(FB + 192 + k);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float gk = de[4 * i + j] * cs[4 * i + j];
-          G[4 * i + j] = gk;
-          gx[0] += gk * B0[j];
-          gx[1] += gk * B1[j];
-          gx[2] += gk * B2[j];
-        }
-      }
-      if (WG) {  // dB[j][k] += sum_p x_j[p] G[k][p]
-        tstore(S.sA, G, lane);
-        lds_sync();
-        const int jj = lane & 31;
-        const int jc = jj < 3 ? jj : 0;
-        f32x16 acc = zero16();
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-          const int p = 2 * s + h;
-          const float xv = jj < 3 ? S.xtab[p * 3 + jc] : 0.f;
-          acc = mfma32(S.sA[p * TPITCH + jj], xv, acc);
-        }
-        if (jj < 3) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int k = 32 * b + fidx(r, h);
-            if (k < NSLAM_EMB) put<WG>(A, jj * NSLAM_EMB + 4 * h, dg.B + 32 * b + (r & 3) + 8 * (r >> 2), acc[r]);
-          }
-        }
-        lds_sync();
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) gx[k] += xor32(gx[k]);
-  }
-  PHASE(DEC_, 11);
-}
-
-// ------------------------------------------------------------------------------------------
-// MLP_no_xyz (coarse, decoder.py:262-274): forward / backward
-// ------------------------------------------------------------------------------------------
-template <bool KEEP>
-__device__ __forceinline__ f32x16 noxyz_forward(const float* __restrict__ pk, const f32x16& c, int lane,
-                                                uint32_t m[5], f32x16* hs) {
-  const NoXyzPack L;
-  f32x16 a = vec_tile(pk + L.Bias(0), lane);
-  gemm_acc(a, pk + L.L0() * NSLAM_FRAG, c, lane);
-  f32x16 a3 = vec_tile(pk + L.Bias(3), lane);
-  gemm_acc(a3, pk + L.L3() * NSLAM_FRAG, c, lane);
-  m[0] = mask16(a);
-  f32x16 h = relu16(a);
-  if (KEEP) hs[0] = h;
-  a = vec_tile(pk + L.Bias(1), lane);
-  gemm_acc(a, pk + L.L1() * NSLAM_FRAG, h, lane);
-  m[1] = mask16(a);
-  h = relu16(a);
-  if (KEEP) hs[1] = h;
-  a = vec_tile(pk + L.Bias(2), lane);
-  gemm_acc(a, pk + L.L2() * NSLAM_FRAG, h, lane);
-  m[2] = mask16(a);
-  h = relu16(a);
-  if (KEEP) hs[2] = h;
-  gemm_acc(a3, pk + (L.L3() + 1) * NSLAM_FRAG, h, lane);
-  m[3] = mask16(a3);
-  h = relu16(a3);
-  if (KEEP) hs[3] = h;
-  a = vec_tile(pk + L.Bias(4), lane);
-  gemm_acc(a, pk + L.L4() * NSLAM_FRAG, h, lane);
-  m[4] = mask16(a);
-  return relu16(a);
-}
-
-template <int WG>
-__device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, const f32x16& c, float g,
-                                               const nslam_dec_grad& dg, const Slab& A, const Scratch& S, int lane,
-                                               f32x16& dc) {
-  const NoXyzPack L;
-  const int h = lane >> 5;
-  uint32_t m[5];
-  f32x16 hs[4];
-  const f32x16 h4 = noxyz_forward<WG != 0>(pk, c, lane, m, hs);
-  f32x16 dh;
-  {
-    const f32x16 w = vec_tile(pk + L.Wo(), lane);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dh[r] = w[r] * g;
-  }
-  if (WG) {
-    tstore(S.sX, h4, lane);
-    lds_sync();
-    const int f = lane & 31;
-    float s = 0.f;
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const int p = 2 * t + h;
-      s += S.gtab[p * 4 + 3] * S.sX[p * TPITCH + f];
-    }
-    s += xor32(s);
-    if (h == 0) put<WG>(A, f, dg.wo, s);
-    if (lane == 0) {
-      float sb = 0.f;
-      for (int p = 0; p < 32; ++p) sb += S.gtab[p * 4 + 3];
-      put<WG>(A, 0, dg.bo, sb);
-    }
-    lds_sync();
-  }
-  dc = zero16();
-  // layer 4
-  f32x16 da = apply_mask(dh, m[4]);
-  if (WG) {
-    wg_begin(da, S, lane);
-    wg_block<WG>(A, dg.w[4], 32, 0, 32, hs[3], S, lane);
-    wg_end<WG>(A, dg.b[4], S, lane);
-  }
-  dh = zero16();
-  gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
-  // layer 3 (input = [c | h2])
-  da = apply_mask(dh, m[3]);
-  if (WG) {
-    wg_begin(da, S, lane);
-    wg_block<WG>(A, dg.w[3], 64, 0, 32, c, S, lane);
-    wg_block<WG>(A, dg.w[3], 64, 32, 32, hs[2], S, lane);
-    wg_end<WG>(A, dg.b[3], S, lane);
-  }
-  gemm_acc(dc, pk + L.L3T() * NSLAM_FRAG, da, lane);
-  dh = zero16();
-  gemm_acc(dh, pk + (L.L3T() + 1) * NSLAM_FRAG, da, lane);
-  // layer 2
-  da = apply_mask(dh, m[2]);
-  if (WG) {
-    wg_begin(da, S, lane);
-    wg_block<WG>(A, dg.w[2], 32, 0, 32, hs[1], S, lane);
-    wg_end<WG>(A, dg.b[2], S, lane);
-  }
-  dh = zero16();
-  gemm_acc(dh, pk + L.L2T() * NSLAM_FRAG, da, lane);
-  // layer 1
-  da = apply_mask(dh, m[1]);
-  if (WG) {
-    wg_begin(da, S, lane);
-    wg_block<WG>(A, dg.w[1], 32, 0, 32, hs[0], S, lane);
-    wg_end<WG>(A, dg.b[1], S, lane);
-  }
-  dh = zero16();
-  gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
-  // layer 0 (input = c)
-  da = apply_mask(dh, m[0]);
-  if (WG) {
-    wg_begin(da, S, lane);
-    wg_block<WG>(A, dg.w[0], 32, 0, 32, c, S, lane);
-    wg_end<WG>(A, dg.b[0], S, lane);
-  }
-  gemm_acc(dc, pk + L.L0T() * NSLAM_FRAG, da, lane);
-}
-
-// ------------------------------------------------------------------------------------------
-// Backward from saved ReLU masks (decoders without parameter gradients): no forward recompute,
-// no embedding sin, no feature gather.  dh_4 = Wo^T g; for i = 4..0: dc += FCT_i dh_i and
-// dh_{i-1} = L_iT mask_i(dh_i) (layer 3 through its hidden block); EMBG adds d/dx through the
-// Fourier features from mask_3(dh_3) and mask_0(dh_0).
-// ------------------------------------------------------------------------------------------
-template <int NC, int NOUT, int GOFS, bool EMBG>
-__device__ __forceinline__ void xyz_backward_saved(const float* __restrict__ pk, const uint32_t m[5],
-                                                   const float x[3], const float (&gall)[4], int lane, f32x16& dc,
-                                                   float gx[3]) {
-  const XyzPack L{NC};
-  const int h = lane >> 5;
-  f32x16 dh = zero16();
-#pragma unroll
-  for (int j = 0; j < NOUT; ++j) {
-    const f32x16 w = vec_tile(pk + L.Wo() + 32 * j, lane);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dh[r] += w[r] * gall[GOFS + j];
-  }
-  dc = zero16();
-  gemm_acc(dc, pk + L.FCT(4) * NSLAM_FRAG, dh, lane);
-  f32x16 da = apply_mask(dh, m[4]);
-  dh = zero16();
-  gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
-  gemm_acc(dc, pk + L.FCT(3) * NSLAM_FRAG, dh, lane);
-  const f32x16 da3 = apply_mask(dh, m[3]);
-  dh = zero16();
-  gemm_acc(dh, pk + (L.L3T() + 3) * NSLAM_FRAG, da3, lane);
-  gemm_acc(dc, pk + L.FCT(2) * NSLAM_FRAG, dh, lane);
-  da = apply_mask(dh, m[2]);
-  dh = zero16();
-  gemm_acc(dh, pk + L.L2T() * NSLAM_FRAG, da, lane);
-  gemm_acc(dc, pk + L.FCT(1) * NSLAM_FRAG, dh, lane);
-  da = apply_mask(dh, m[1]);
-  dh = zero16();
-  gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
-  gemm_acc(dc, pk + L.FCT(0) * NSLAM_FRAG, dh, lane);
-  gx[0] = gx[1] = gx[2] = 0.f;
-  if (EMBG) {
-    da = apply_mask(dh, m[0]);
-    const float* FB = pk + L.FB();
-#pragma unroll
-    for (int b = 0; b < 3; ++b) {
-      f32x16 de = zero16();
-      gemm_acc(de, pk + (L.L3T() + b) * NSLAM_FRAG, da3, lane);
-      gemm_acc(de, pk + (L.L0T() + b) * NSLAM_FRAG, da, lane);
-      const f32x16 cs = emb_tile<true>(FB, x, b, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int k = 32 * b + 8 * i + 4 * h;
-        const f32x4 B0 = *reinterpret_cast<const f32x4*>(FB + k);
-        const f32x4 B1 = *reinterpret_cast<const f32x4*>(FB + 96 + k);
-        const f32x4 B2 = *reinterpret_cast<const f32x4*>(FB + 192 + k);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float gk = de[4 * i + j] * cs[4 * i + j];
-          gx[0] += gk * B0[j];
-          gx[1] += gk * B1[j];
-          gx[2] += gk * B2[j];
-        }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) gx[k] += xor32(gx[k]);
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// Colour decoder backward from the forward's masks + activation tape (no forward recompute):
-// the dh chain is the mask-only one; every weight gradient takes its input tile from the tape
-// (h0..h4) or from the colour feature `cin`; the embedding is evaluated ONCE at the end, per
-// block b: sin_b feeds both dW3's and dW0's embedding columns (the layer-3 and layer-0
-// cotangents wait in LDS images sD3 / sA), cos_b the Fourier backward G_b = de_b * cos_b -> dB.
-// ------------------------------------------------------------------------------------------
-template <int WG>
-__device__ __forceinline__ void color_backward_tape(const float* __restrict__ pk, const f32x16& cin, const float x[3],
-                                                    const float (&gall)[4], const uint32_t m[5],
-                                                    const float* __restrict__ tape, const nslam_dec_grad& dg,
-                                                    const Slab& A, const Scratch& S, int lane, f32x16& dc) {
-  const XyzPack L{1};
-  const int h = lane >> 5, f = lane & 31;
-  const f32x16 c1[1] = {cin};
-  // output layer (3 rows used; row 3 is overwritten by the stage combiner, decoder.py:331-334)
-  f32x16 dh = zero16();
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const f32x16 w = vec_tile(pk + L.Wo() + 32 * j, lane);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dh[r] += w[r] * gall[j];
-  }
-  tstore(S.sX, tape_load(tape, 4, lane), lane);
-  lds_sync();
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    float sw = 0.f;
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const int p = 2 * t + h;
-      sw += S.gtab[p * 4 + j] * S.sX[p * TPITCH + f];
-    }
-    sw += xor32(sw);
-    if (h == 0) put<WG>(A, f, dg.wo + 32 * j, sw);
-    // dbo[j] = sum over the tile's points: butterfly over the 32 point lanes of half 0
-    float sb = gall[j];
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) sb += __shfl_xor(sb, o, 64);
-    if (lane == 0) put<WG>(A, 0, dg.bo + j, sb);
-  }
-  if (WG == 1) {
-    if (h == 0) put<1>(A, f, dg.wo + 96, 0.f);
-    if (lane == 0) put<1>(A, 0, dg.bo + 3, 0.f);
-  }
-  lds_sync();
-  dc = zero16();
-  // layer 4 (input h3)
-  fc_bwd<1, WG>(pk, L, 4, c1, dh, dg, A, S, lane, dc);
-  f32x16 da = apply_mask(dh, m[4]);
-  wg_begin(da, S, lane);
-  wg_block<WG>(A, dg.w[4], 32, 0, 32, tape_load(tape, 3, lane), S, lane);
-  wg_end<WG>(A, dg.b[4], S, lane);
-  dh = zero16();
-  gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
-  // layer 3 (input [emb | h2]): the h2 columns now, the embedding columns at the end
-  fc_bwd<1, WG>(pk, L, 3, c1, dh, dg, A, S, lane, dc);
-  const f32x16 da3 = apply_mask(dh, m[3]);
-  tstore(S.sD3, da3, lane);
-  tstore(S.sX, tape_load(tape, 2, lane), lane);
-  lds_sync();
-  dw_block_img<WG>(A, dg.w[3], 125, 93, 32, S.sD3, S.sX, lane);
-  db_vec_img<WG>(A, dg.b[3], S.sD3, lane);
-  lds_sync();
-  dh = zero16();
-  gemm_acc(dh, pk + (L.L3T() + 3) * NSLAM_FRAG, da3, lane);
-  // layer 2 (input h1)
-  fc_bwd<1, WG>(pk, L, 2, c1, dh, dg, A, S, lane, dc);
-  da = apply_mask(dh, m[2]);
-  wg_begin(da, S, lane);
-  wg_block<WG>(A, dg.w[2], 32, 0, 32, tape_load(tape, 1, lane), S, lane);
-  wg_end<WG>(A, dg.b[2], S, lane);
-  dh = zero16();
-  gemm_acc(dh, pk + L.L2T() * NSLAM_FRAG, da, lane);
-  // layer 1 (input h0)
-  fc_bwd<1, WG>(pk, L, 1, c1, dh, dg, A, S, lane, dc);
-  da = apply_mask(dh, m[1]);
-  wg_begin(da, S, lane);
-  wg_block<WG>(A, dg.w[1], 32, 0, 32, tape_load(tape, 0, lane), S, lane);
-  wg_end<WG>(A, dg.b[1], S, lane);
-  dh = zero16();
-  gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
-  // layer 0 (input emb): its cotangent stays in sA for the embedding blocks
-  fc_bwd<1, WG>(pk, L, 0, c1, dh, dg, A, S, lane, dc);
-  da = apply_mask(dh, m[0]);
-  wg_begin(da, S, lane);
-  wg_end<WG>(A, dg.b[0], S, lane);
-  // embedding blocks: sin_b -> dW3 / dW0 columns; cos_b -> G_b = (L3T_b da3 + L0T_b da0) cos_b -> dB
-  const float* FB = pk + L.FB();
-#pragma nounroll
-  for (int b = 0; b < 3; ++b) {
-    f32x16 sn, cs;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = 32 * b + 8 * i + 4 * h;
-      const f32x4 B0 = *reinterpret_cast<const f32x4*>(FB + k);
-      const f32x4 B1 = *reinterpret_cast<const f32x4*>(FB + 96 + k);
-      const f32x4 B2 = *reinterpret_cast<const f32x4*>(FB + 192 + k);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float sv, cv;
-        fsincos(fourier_arg(x, B0[j], B1[j], B2[j]), sv, cv);
-        sn[4 * i + j] = sv;
-        cs[4 * i + j] = cv;
-      }
-    }
-    const int kv = b < 2 ? 32 : 29;
-    tstore(S.sX, sn, lane);
-    lds_sync();
-    dw_block_img<WG>(A, dg.w[3], 125, 32 * b, kv, S.sD3, S.sX, lane);
-    dw_block_img<WG>(A, dg.w[0], 93, 32 * b, kv, S.sA, S.sX, lane);
-    lds_sync();
-    f32x16 de = zero16();
-    gemm_acc(de, pk + (L.L3T() + b) * NSLAM_FRAG, da3, lane);
-    gemm_acc(de, pk + (L.L0T() + b) * NSLAM_FRAG, da, lane);
-    f32x16 G;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) G[r] = de[r] * cs[r];
-    tstore(S.sX, G, lane);
-    lds_sync();
-    // dB[j][k] += sum_p x_j[p] G[k][p]
-    const int jc = f < 3 ? f : 0;
-    f32x16 acc = zero16();
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const int p = 2 * t + h;
-      const float xv = f < 3 ? S.xtab[p * 3 + jc] : 0.f;
-      acc = mfma32(S.sX[p * TPITCH + f], xv, acc);
-    }
-    if (f < 3) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int k = 32 * b + fidx(r, h);
-        if (k < NSLAM_EMB) put<WG>(A, f * NSLAM_EMB + 4 * h, dg.B + 32 * b + (r & 3) + 8 * (r >> 2), acc[r]);
-      }
-    }
-    lds_sync();
-  }
-}
-
-__device__ __forceinline__ void noxyz_backward_saved(const float* __restrict__ pk, const uint32_t m[5], float g,
-                                                     int lane, f32x16& dc) {
-  const NoXyzPack L;
-  f32x16 dh;
-  {
-    const f32x16 w = vec_tile(pk + L.Wo(), lane);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dh[r] = w[r] * g;
-  }
-  dc = zero16();
-  f32x16 da = apply_mask(dh, m[4]);
-  dh = zero16();
-  gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
-  da = apply_mask(dh, m[3]);
-  gemm_acc(dc, pk + L.L3T() * NSLAM_FRAG, da, lane);
-  dh = zero16();
-  gemm_acc(dh, pk + (L.L3T() + 1) * NSLAM_FRAG, da, lane);
-  da = apply_mask(dh, m[2]);
-  dh = zero16();
-  gemm_acc(dh, pk + L.L2T() * NSLAM_FRAG, da, lane);
-  da = apply_mask(dh, m[1]);
-  dh = zero16();
-  gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
-  da = apply_mask(dh, m[0]);
-  gemm_acc(dc, pk + L.L0T() * NSLAM_FRAG, da, lane);
-}
-
-// ------------------------------------------------------------------------------------------
-// grid gradient scatter (atomics shaped as two 128-B row segments per wave-instruction) and
-// coordinate gradient through the trilinear weights
-// ------------------------------------------------------------------------------------------
-// Stage a tile's corner rows / weights for the scatter.  With a slot map (ABI v6: frustum-
-// compacted grid gradient, Mapper.py:314-333) corner row r accumulates into compact row slot[r];
-// corners outside the frustum selection (slot -1) get weight 0, i.e. no atomic: the reference
-// never forms their gradient (its optimised tensor is the masked vector, Mapper.py:394-401).
-__device__ __forceinline__ void stage_corners(const Corners& cr, const int32_t* __restrict__ slot, bool valid,
-                                              const Scratch& S, int lane) {
-  if (lane < 32) {
-    const int p = lane;
-    S.ccell[p] = cr.cell;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      int r = cr.row[k];
-      float w = valid ? cr.w[k] : 0.f;
-      if (slot) {
-        r = slot[r];
-        if (r < 0) {
-          r = 0;
-          w = 0.f;
-        }
-      }
-      S.crow[p * 8 + k] = r;
-      S.cw[p * 8 + k] = w;
-    }
-  }
-}
-
-__device__ __forceinline__ int cell_axis(int c, int a) { return (c >> (10 * a)) & 1023; }
-
-__device__ __forceinline__ void scatter_grid_grad_uniform(float* __restrict__ grad, const int32_t* __restrict__ slot,
-                                                          const Corners& cr, const f32x16& dc, bool valid,
-                                                          const Scratch& S, int lane) {
-  // Points of a tile are consecutive samples of (mostly) one ray, so their cells form a walk.
-  // The whole wave walks the tile's 32 points in step (uniform control flow); lane (h, ch) owns
-  // channel ch of corners 2j + h, j = 0..3 — corners 2j and 2j+1 differ only in x, i.e. are
-  // adjacent rows of the channels-last grid, so every flush wave-instruction adds one contiguous
-  // 256-B segment (the full-rate shape of a float atomic).  Samples in the same cell are summed
-  // in registers; when the walk steps to a neighbouring cell (|delta| <= 1 on every axis) the
-  // corners the two cells share are CARRIED into the new cell's corner slots (a register move,
-  // or a swap of lane halves for an x step) instead of being flushed: each voxel costs one
-  // atomic per run of cells touching it, not one per cell.
-  const int h = lane >> 5, ch = lane & 31;
-  tstore(S.sA, dc, lane);
-  stage_corners(cr, slot, valid, S, lane);
-  lds_sync();
-  float acc[4], wsum[4];
-  int rows[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    acc[j] = 0.f;
-    wsum[j] = 0.f;
-    rows[j] = 0;
-  }
-  int cur = -1;
-  for (int t = 0; t < 32; ++t) {
-    const int cell = __builtin_amdgcn_readfirstlane(S.ccell[t]);
-    if (cell != cur) {
-      int ax = 2, ay = 2, az = 2;
-      if (cur >= 0) {
-        ax = cell_axis(cell, 0) - cell_axis(cur, 0);
-        ay = cell_axis(cell, 1) - cell_axis(cur, 1);
-        az = cell_axis(cell, 2) - cell_axis(cur, 2);
-      }
-      const bool adj = ax >= -1 && ax <= 1 && ay >= -1 && ay <= 1 && az >= -1 && az <= 1;  // wave-uniform
-      // old corner (h, j&1, j>>1) lands on new corner (h-ax, (j&1)-ay, (j>>1)-az): flush it if outside
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int nx = h - ax, ny = (j & 1) - ay, nz = (j >> 1) - az;
-        const bool keep = adj && nx >= 0 && nx <= 1 && ny >= 0 && ny <= 1 && nz >= 0 && nz <= 1;
-        if (!keep && wsum[j] != 0.f) unsafeAtomicAdd(grad + (size_t)rows[j] * NSLAM_C_DIM + ch, acc[j]);
-      }
-      // new corner (h, j&1, j>>1) takes old corner (h+ax, (j&1)+ay, (j>>1)+az) when that exists
-      float nacc[4], nws[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int sy = (j & 1) + ay, sz = (j >> 1) + az;  // wave-uniform source register
-        const bool in_yz = adj && sy >= 0 && sy <= 1 && sz >= 0 && sz <= 1;
-        const int js = in_yz ? sy + 2 * sz : 0;
-        float va = js == 0 ? acc[0] : js == 1 ? acc[1] : js == 2 ? acc[2] : acc[3];
-        float vw = js == 0 ? wsum[0] : js == 1 ? wsum[1] : js == 2 ? wsum[2] : wsum[3];
-        if (ax != 0) {  // source half h+ax: the other half of the wave (uniform branch)
-          va = xor32(va);
-          vw = xor32(vw);
-        }
-        const int sx = h + ax;
-        const bool in = in_yz && sx >= 0 && sx <= 1;
-        nacc[j] = in ? va : 0.f;
-        nws[j] = in ? vw : 0.f;
-      }
-      cur = cell;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc[j] = nacc[j];
-        wsum[j] = nws[j];
-        rows[j] = S.crow[t * 8 + 2 * j + h];
-      }
-    }
-    const float v = S.sA[t * TPITCH + ch];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float w = S.cw[t * 8 + 2 * j + h];
-      acc[j] += w * v;
-      wsum[j] += w;
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (wsum[j] != 0.f) unsafeAtomicAdd(grad + (size_t)rows[j] * NSLAM_C_DIM + ch, acc[j]);
-  lds_sync();
-}
-
-// Per-half variant (weight-gradient kernels): half h walks points 16h..16h+15 on its own, every
-// flush wave-instruction is one 128-B row segment.  Kept for the register-starved weight-gradient
-// kernels, where the uniform variant above coincided with an illegal-address fault in the fine
-// decoder's kernel (both runs of tests/test_gpu_parity.py eval fine, r1k and r1l).
-__device__ __forceinline__ void scatter_grid_grad_halves(float* __restrict__ grad, const int32_t* __restrict__ slot,
-                                                         const Corners& cr, const f32x16& dc, bool valid,
-                                                         const Scratch& S, int lane) {
-  const int h = lane >> 5, ch = lane & 31;
-  tstore(S.sA, dc, lane);
-  stage_corners(cr, slot, valid, S, lane);
-  lds_sync();
-  float acc[8], wsum[8];
-  int rows[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    acc[k] = 0.f;
-    wsum[k] = 0.f;
-    rows[k] = 0;
-  }
-  int cur = -1;
-  for (int t = 0; t < 16; ++t) {
-    const int pp = 16 * h + t;
-    const int cell = S.ccell[pp];
-    if (cell != cur) {
-      if (cur >= 0) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (wsum[k] != 0.f) unsafeAtomicAdd(grad + (size_t)rows[k] * NSLAM_C_DIM + ch, acc[k]);
-      }
-      cur = cell;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        acc[k] = 0.f;
-        wsum[k] = 0.f;
-        rows[k] = S.crow[pp * 8 + k];
-      }
-    }
-    const float v = S.sA[pp * TPITCH + ch];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float w = S.cw[pp * 8 + k];
-      acc[k] += w * v;
-      wsum[k] += w;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 8; ++k)
-    if (wsum[k] != 0.f) unsafeAtomicAdd(grad + (size_t)rows[k] * NSLAM_C_DIM + ch, acc[k]);
-  lds_sync();
-}
-
-__device__ __forceinline__ void coord_grad(const nslam_grid& g, const Corners& cr, const f32x16& dc, int lane,
-                                           double gp[3]) {
-  float part[3];
-  coord_grad_partial(g.data, cr, dc, lane, part);
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const float gn = (part[k] + xor32(part[k])) * cr.gmul[k];
-    gp[k] += ((double)gn * 2.0) / (g.hi[k] - g.lo[k]);
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// kernels
-// ------------------------------------------------------------------------------------------
-template <int STAGE>
-__global__ __launch_bounds__(256, 2) void k_query_fwd(QueryKArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int64_t tile = (int64_t)blockIdx.x * 4 + wave_id();
-  if (tile * 32 >= a.n) return;  // wave-uniform
-  const int h = lane >> 5;
-  const Pt q = load_point(a, tile * 32 + (lane & 31));
-  float out[4] = {0.f, 0.f, 0.f, 0.f};
-  uint32_t m[5];
-  if (STAGE == NSLAM_STAGE_COARSE) {
-    Corners cr;
-    grid_corners(cr, a.c.grid[NSLAM_DEC_COARSE], q);
-    const f32x16 c = gather_tile(a.c.grid[NSLAM_DEC_COARSE].data, cr, lane);
-    const float* pk = a.c.packed[NSLAM_DEC_COARSE];
-    const NoXyzPack L;
-    const f32x16 h4 = noxyz_forward<false>(pk, c, lane, m, nullptr);
-    save_masks(a, NSLAM_DEC_COARSE, tile, m, lane);
-    out[3] = out_row(pk + L.Wo(), pk + L.Bo(), 0, h4, lane);
-  } else {
-    Corners cr;
-    grid_corners(cr, a.c.grid[NSLAM_DEC_MIDDLE], q);
-    const f32x16 cm[1] = {gather_tile(a.c.grid[NSLAM_DEC_MIDDLE].data, cr, lane)};
-    {
-      const float* pk = a.c.packed[NSLAM_DEC_MIDDLE];
-      const XyzPack L{1};
-      const f32x16 h4 = xyz_forward<1, false>(pk, cm, q.x, lane, m, nullptr);
-      save_masks(a, NSLAM_DEC_MIDDLE, tile, m, lane);
-      out[3] = out_row(pk + L.Wo(), pk + L.Bo(), 0, h4, lane);
-    }
-    if (STAGE >= NSLAM_STAGE_FINE) {
-      grid_corners(cr, a.c.grid[NSLAM_DEC_FINE], q);
-      const f32x16 cf[2] = {gather_tile(a.c.grid[NSLAM_DEC_FINE].data, cr, lane), cm[0]};
-      const float* pk = a.c.packed[NSLAM_DEC_FINE];
-      const XyzPack L{2};
-      const f32x16 h4 = xyz_forward<2, false>(pk, cf, q.x, lane, m, nullptr);
-      save_masks(a, NSLAM_DEC_FINE, tile, m, lane);
-      out[3] = out_row(pk + L.Wo(), pk + L.Bo(), 0, h4, lane) + out[3];  // fine_occ + middle_occ
-    }
-    if (STAGE == NSLAM_STAGE_COLOR) {
-      grid_corners(cr, a.c.grid[NSLAM_DEC_COLOR], q);
-      const f32x16 cc[1] = {gather_tile(a.c.grid[NSLAM_DEC_COLOR].data, cr, lane)};
-      const float* pk = a.c.packed[NSLAM_DEC_COLOR];
-      const XyzPack L{1};
-      float* tp = a.c.act_tape ? a.c.act_tape + tile * kTapeFloats : nullptr;
-      const f32x16 h4 = xyz_forward<1, false>(pk, cc, q.x, lane, m, nullptr, tp);
-      save_masks(a, NSLAM_DEC_COLOR, tile, m, lane);
-#pragma unroll
-      for (int j = 0; j < 3; ++j) out[j] = out_row(pk + L.Wo(), pk + L.Bo(), j, h4, lane);
-    }
-  }
-  if (!q.inside) out[3] = 100.f;  // Renderer.py:57
-  if (h == 0 && q.valid) {
-    f32x4 v;
-    v[0] = out[0];
-    v[1] = out[1];
-    v[2] = out[2];
-    v[3] = out[3];
-    *reinterpret_cast<f32x4*>(a.raw + (tile * 32 + (lane & 31)) * 4) = v;
-  }
-}
-
-// Decoder-parallel forward (fine and colour stages): each workgroup evaluates ONE decoder for its
-// 4 tiles, so a launch has 2-3x the waves of k_query_fwd (room0 mapping: 4500 instead of 1500 on
-// 1024 SIMDs) and every wave a third of the serial MFMA/gather chain.  Parts are interleaved
-// over blockIdx (heavy fine and light middle/colour workgroups mix on every CU):
-//   part 0  middle: occ_mid[p] = inside ? middle_occ : 100
-//   part 1  fine:   raw[p][3]  = inside ? fine_occ : 0     (fine stage: the whole row)
-//   part 2  colour: raw[p][0..2]
-// and k_occ_combine then forms raw[p][3] = fine_occ + middle_occ (decoder.py:331-334, the
-// reference's operand order) — exactly 100 outside the bound (0 + 100; Renderer.py:57).
-template <int STAGE>
-__global__ __launch_bounds__(256, 2) void k_query_fwd_parts(QueryKArgs a, float* __restrict__ occ_mid) {
-  constexpr int NPARTS = STAGE == NSLAM_STAGE_COLOR ? 3 : 2;
-  const int part = (int)(blockIdx.x % NPARTS);
-  const int lane = threadIdx.x & 63;
-  const int64_t tile = (int64_t)(blockIdx.x / NPARTS) * 4 + wave_id();
-  if (tile * 32 >= a.n) return;  // wave-uniform
-  const int h = lane >> 5;
-  const int64_t idx = tile * 32 + (lane & 31);
-  PHASE(0, 0);
-  const Pt q = load_point(a, idx);
-  PHASE(0, 1);
-  uint32_t m[5];
-  Corners cr;
-  if (part == 0) {
-    grid_corners(cr, a.c.grid[NSLAM_DEC_MIDDLE], q);
-    PHASE(0, 2);
-    const f32x16 cm = gather_tile(a.c.grid[NSLAM_DEC_MIDDLE].data, cr, lane);
-    PHASE(0, 3);
-    const float* pk = a.c.packed[NSLAM_DEC_MIDDLE];
-    const XyzPack L{1};
-    const f32x16 cms[1] = {cm};
-    const f32x16 h4 = xyz_forward<1, false, true>(pk, cms, q.x, lane, m, nullptr);
-    save_masks(a, NSLAM_DEC_MIDDLE, tile, m, lane);
-    float o = out_row(pk + L.Wo(), pk + L.Bo(), 0, h4, lane);
-    if (!q.inside) o = 100.f;
-    if (h == 0 && q.valid) occ_mid[idx] = o;
-  } else if (part == 1) {  // the fine decoder also reads the middle feature (decoder.py:184-187)
-    Corners cm;
-    grid_corners(cm, a.c.grid[NSLAM_DEC_MIDDLE], q);
-    grid_corners(cr, a.c.grid[NSLAM_DEC_FINE], q);
-    PHASE(0, 2);
-    const f32x16 cf[2] = {gather_tile(a.c.grid[NSLAM_DEC_FINE].data, cr, lane),
-                          gather_tile(a.c.grid[NSLAM_DEC_MIDDLE].data, cm, lane)};
-    PHASE(0, 3);
-    const float* pk = a.c.packed[NSLAM_DEC_FINE];
-    const XyzPack L{2};
-    const f32x16 h4 = xyz_forward<2, false, true>(pk, cf, q.x, lane, m, nullptr);
-    save_masks(a, NSLAM_DEC_FINE, tile, m, lane);
-    float o = out_row(pk + L.Wo(), pk + L.Bo(), 0, h4, lane);
-    if (!q.inside) o = 0.f;
-    if (h == 0 && q.valid) {
-      if (STAGE == NSLAM_STAGE_COLOR) {
-        a.raw[idx * 4 + 3] = o;
-      } else {
-        f32x4 v = {0.f, 0.f, 0.f, o};
-        *reinterpret_cast<f32x4*>(a.raw + idx * 4) = v;
-      }
-    }
-  } else if (STAGE == NSLAM_STAGE_COLOR) {
-    grid_corners(cr, a.c.grid[NSLAM_DEC_COLOR], q);
-    PHASE(0, 2);
-    const f32x16 cc[1] = {gather_tile(a.c.grid[NSLAM_DEC_COLOR].data, cr, lane)};
-    PHASE(0, 3);
-    const float* pk = a.c.packed[NSLAM_DEC_COLOR];
-    const XyzPack L{1};
-    float* tp = a.c.act_tape ? a.c.act_tape + tile * kTapeFloats : nullptr;
-    const f32x16 h4 = xyz_forward<1, false, true>(pk, cc, q.x, lane, m, nullptr, tp);
-    save_masks(a, NSLAM_DEC_COLOR, tile, m, lane);
-    float o[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) o[j] = out_row(pk + L.Wo(), pk + L.Bo(), j, h4, lane);
-    if (h == 0 && q.valid) {
-#pragma unroll
-      for (int j = 0; j < 3; ++j) a.raw[idx * 4 + j] = o[j];
-    }
-  }
-  PHASE(0, 9);
-}
-
-__global__ __launch_bounds__(256) void k_occ_combine(float* __restrict__ raw, const float* __restrict__ occ_mid,
-                                                     int64_t n) {
-  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (p < n) raw[p * 4 + 3] = raw[p * 4 + 3] + occ_mid[p];
-}
-
-// One backward launch per decoder: the decoder's forward is recomputed, its grid gradient is
-// scattered, its parameter gradients are accumulated and its share of d/dpts is added into g_pts
-// (launches on one stream are ordered and each point is owned by one lane pair: plain
-// read-modify-write, no atomics).  With parameter gradients every wave owns a slab of the
-// workspace (WG == 1: one tile per wave, slab = tile; WG == 2: a fixed number of waves walk the
-// tiles over pre-zeroed slabs) and k_slab_reduce sums the slabs in a fixed order
-// (deterministic).  LDS holds only each wave's transpose scratch: LDS float atomics
-// (ds_add_f32, one RMW per lane) were the bottleneck of the previous shared-accumulator design.
-constexpr int kScratchFloats = 2 * TILE_FLOATS + 32 * 4 + 32 * 3 + 32 * 8 * 2 + 32;
-constexpr int kWavesBwd = 4;
-constexpr int kMaxSlabs = 4096;  // WG == 2 above this many tiles
-
-template <int DEC, int WG, bool PG, bool FIRST, bool SAVED>
-__device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, const Slab& A, const Scratch& S,
-                                             int lane) {
-  // Every scratch / slab address is a function of the lane only, i.e. invariant across the tile
-  // loop; letting LICM hoist the ~300 of them pins (and spills) the register file.  Re-derive
-  // them per tile.
-  asm volatile("" : "+v"(lane));
-  PHASE(DEC, 0);
-  const int h = lane >> 5, p = lane & 31;
-  const int64_t idx = tile * 32 + p;
-  const Pt q = load_point(a, idx);
-  float g[4] = {0.f, 0.f, 0.f, 0.f};
-  if (q.valid) {
-    const f32x4 v = *reinterpret_cast<const f32x4*>(a.g_raw + idx * 4);
-    g[0] = v[0];
-    g[1] = v[1];
-    g[2] = v[2];
-    g[3] = q.inside ? v[3] : 0.f;  // ret[~mask,3]=100 blocks the occupancy gradient
-  }
-  if (WG) {
-    if (h == 0) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) S.gtab[p * 4 + j] = g[j];
-#pragma unroll
-      for (int j = 0; j < 3; ++j) S.xtab[p * 3 + j] = q.x[j];
-    }
-    lds_sync();
-  }
-  const nslam_grid& gr = a.c.grid[DEC];
-  const nslam_dec_grad& dg = a.c.dgrad[DEC];
-  const float* pk = a.c.packed[DEC];
-  // The weight fragments are loop-invariant across the tile loop; hoisting their ~100 loads out of
-  // the loop would pin hundreds of registers.  Launder the base pointer per tile so they stay put.
-  asm volatile("" : "+s"(pk));
-  PHASE(DEC, 1);
-  Corners cr;
-  grid_corners(cr, gr, q);
-  PHASE(DEC, 2);
-  f32x16 dc;
-  float gx[3] = {0.f, 0.f, 0.f};
-  if constexpr (SAVED && WG != 0) {  // colour weight gradients from the masks + activation tape
-    uint32_t m[5];
-    load_masks(a, DEC, tile, m, lane);
-    const f32x16 c = gather_tile(gr.data, cr, lane);
-    PHASE(DEC, 3);
-    color_backward_tape<WG>(pk, c, q.x, g, m, a.c.act_tape + tile * kTapeFloats, dg, A, S, lane, dc);
-  } else if (SAVED) {  // masks from the forward: no recompute (decoders without parameter gradients)
-    uint32_t m[5];
-    load_masks(a, DEC, tile, m, lane);
-    if (DEC == NSLAM_DEC_COARSE)
-      noxyz_backward_saved(pk, m, g[3], lane, dc);
-    else if (DEC == NSLAM_DEC_FINE)
-      xyz_backward_saved<2, 1, 3, PG>(pk, m, q.x, g, lane, dc, gx);
-    else if (DEC == NSLAM_DEC_COLOR)
-      xyz_backward_saved<1, 3, 0, PG>(pk, m, q.x, g, lane, dc, gx);
-    else
-      xyz_backward_saved<1, 1, 3, PG>(pk, m, q.x, g, lane, dc, gx);
-  } else if (DEC == NSLAM_DEC_COARSE) {
-    const f32x16 c = gather_tile(gr.data, cr, lane);
-    noxyz_backward<WG>(pk, c, g[3], dg, A, S, lane, dc);
-  } else if (DEC == NSLAM_DEC_FINE) {
-    Corners cm;
-    grid_corners(cm, a.c.grid[NSLAM_DEC_MIDDLE], q);
-    // the middle feature enters the fine decoder under torch.no_grad (decoder.py:184-187)
-    const f32x16 cf[2] = {gather_tile(gr.data, cr, lane), gather_tile(a.c.grid[NSLAM_DEC_MIDDLE].data, cm, lane)};
-    xyz_backward<2, 1, 3, WG, PG || WG>(pk, cf, q.x, g, dg, A, S, lane, dc, gx);
-  } else {
-    const f32x16 c[1] = {gather_tile(gr.data, cr, lane)};
-    PHASE(DEC, 3);
-    if (DEC == NSLAM_DEC_COLOR)  // the colour decoder's 4th output is overwritten by the combiner
-      xyz_backward<1, 3, 0, WG, PG || WG>(pk, c, q.x, g, dg, A, S, lane, dc, gx);
-    else
-      xyz_backward<1, 1, 3, WG, PG || WG>(pk, c, q.x, g, dg, A, S, lane, dc, gx);
-  }
-  PHASE(DEC, 12);
-#ifdef NSLAM_EXP_NOSCATTER  // timing experiment only: no grid-gradient atomics
-  if (false) {
-#else
-  if (gr.grad) {
-#endif
-    if (WG)
-      scatter_grid_grad_halves(gr.grad, gr.slot, cr, dc, q.valid, S, lane);
-    else
-      scatter_grid_grad_uniform(gr.grad, gr.slot, cr, dc, q.valid, S, lane);
-  }
-  PHASE(DEC, 13);
-  if (PG) {
-    double gp[3] = {(double)gx[0], (double)gx[1], (double)gx[2]};
-    coord_grad(gr, cr, dc, lane, gp);
-    if (h == 0 && q.valid) {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) a.g_pts[idx * 3 + k] = FIRST ? gp[k] : a.g_pts[idx * 3 + k] + gp[k];
-    }
-  }
-  PHASE(DEC, 14);
-}
-
-template <int DEC, int WG, bool PG, bool FIRST, bool SAVED>
-__global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd(QueryKArgs a, float* __restrict__ slab,
-                                                                 int acc_floats) {
-  // per-wave scratch: the scatter needs sA + corner rows/weights; weight gradients add sX and
-  // the per-point tables (sizing LDS per variant keeps the lean kernels at 5+ waves/SIMD)
-  constexpr int kScr = WG ? kScratchFloats + (SAVED ? TILE_FLOATS : 0) : TILE_FLOATS + 32 * 8 * 2 + 32;
-  __shared__ __attribute__((aligned(16))) float lds[kWavesBwd * kScr];
-  const int lane = threadIdx.x & 63, wave = wave_id();
-  float* sc = lds + wave * kScr;
-  Scratch S;
-  S.sA = sc;
-  S.sD3 = nullptr;
-  if (WG) {
-    S.sX = sc + TILE_FLOATS;
-    S.gtab = sc + 2 * TILE_FLOATS;
-    S.xtab = S.gtab + 32 * 4;
-    S.crow = reinterpret_cast<int*>(S.xtab + 32 * 3);
-  } else {
-    S.sX = S.gtab = S.xtab = nullptr;
-    S.crow = reinterpret_cast<int*>(sc + TILE_FLOATS);
-  }
-  S.cw = reinterpret_cast<float*>(S.crow + 32 * 8);
-  S.ccell = reinterpret_cast<int*>(S.cw + 32 * 8);
-  if (WG && SAVED) S.sD3 = reinterpret_cast<float*>(S.ccell + 32);
-  const int64_t ntiles = (a.n + 31) / 32;
-  const int64_t w = (int64_t)blockIdx.x * kWavesBwd + wave;
-  const Slab A = make_slab(WG ? slab + (size_t)w * acc_floats : slab, WG ? acc_floats : 0);
-  if (WG != 2) {  // one tile per wave (grid covers all tiles)
-    if (w < ntiles) dec_bwd_tile<DEC, WG, PG, FIRST, SAVED>(a, w, A, S, lane);
-    return;
-  }
-#pragma nounroll
-  for (int64_t tile = w; tile < ntiles; tile += (int64_t)gridDim.x * kWavesBwd)
-    dec_bwd_tile<DEC, WG, PG, FIRST, SAVED>(a, tile, A, S, lane);
-}
-
-// base[j] += sum_b slab[b][j].  A workgroup owns 64 parameters; lane (r, c) of a wave reads the
-// float4 c of slab r of every 64th slab group, so the 16 waves x 4 lane rows keep 64 slab streams
-// in flight per workgroup (~count/64 workgroups fill the chip; a wave load is 4 x 256-B
-// segments).  The 64 partials are combined in LDS in a fixed order: deterministic.
-constexpr int kReduceWaves = 16;
-__global__ __launch_bounds__(64 * kReduceWaves) void k_slab_reduce(const float* __restrict__ slab, int64_t nslab,
-                                                                   int acc_floats, int count,
-                                                                   float* __restrict__ base) {
-  __shared__ f32x4 part[kReduceWaves * 4][16];
-  const int lane = threadIdx.x & 63, wave = wave_id();
-  const int c = lane & 15, r = wave * 4 + (lane >> 4);  // r: slab stream 0..63
-  const int j = (blockIdx.x * 16 + c) * 4;
-  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
-  if (j < count) {
-    const float* p = slab + j;
-    int64_t b = r;
-    for (; b + 64 < nslab; b += 128) {
-      s0 += *reinterpret_cast<const f32x4*>(p + b * acc_floats);
-      s1 += *reinterpret_cast<const f32x4*>(p + (b + 64) * acc_floats);
-    }
-    if (b < nslab) s0 += *reinterpret_cast<const f32x4*>(p + b * acc_floats);
-  }
-  part[r][c] = s0 + s1;
-  __syncthreads();
-  if (threadIdx.x < 16 && j < count) {
-    f32x4 t = part[0][c];
-#pragma unroll 8
-    for (int k = 1; k < kReduceWaves * 4; ++k) t += part[k][c];
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if (j + e < count) base[j + e] += t[e];
-  }
-}
-
-bool grid_ok(const nslam_grid& g) {
-  // every axis <= 1024: the scatter packs a cell's coordinates into 10 bits each (Corners::cell)
-  return g.data && g.dims[0] > 0 && g.dims[1] > 0 && g.dims[2] > 0 && g.dims[0] <= 1024 && g.dims[1] <= 1024 &&
-         g.dims[2] <= 1024 && (((uintptr_t)g.data) & 15) == 0;
-}
-
-int check_cfg(const nslam_query_cfg* c, bool bwd) {
-  if (!c || c->stage < 0 || c->stage > 3) return NSLAM_EINVAL;
-  const int st = c->stage;
-  bool need[4] = {st == NSLAM_STAGE_COARSE, st != NSLAM_STAGE_COARSE, st >= NSLAM_STAGE_FINE,
-                  st == NSLAM_STAGE_COLOR};
-  for (int d = 0; d < 4; ++d) {
-    if (!need[d]) continue;
-    if (!grid_ok(c->grid[d]) || !c->packed[d]) return NSLAM_EINVAL;
-    if ((((uintptr_t)c->packed[d]) & 15) != 0) return NSLAM_EINVAL;
-  }
-  if (c->rays_o) {
-    if (!c->rays_d || !c->z_vals || c->n_samples <= 0) return NSLAM_EINVAL;
-  }
-  return NSLAM_OK;
-}
-
-int hip_status() {
-  const hipError_t e = hipGetLastError();
-  return e == hipSuccess ? NSLAM_OK : NSLAM_EHIP - (int)e;
-}
-
-}  // namespace
+using namespace nslamq;
 
 extern "C" int nslam_query_fwd(const nslam_query_cfg* cfg, const double* pts, int64_t n_pts, float* raw,
                                void* stream) {
@@ -1440,128 +52,6 @@ extern "C" int nslam_query_fwd_ws(const nslam_query_cfg* cfg, const double* pts,
   return hip_status();
 }
 
-namespace {
-
-int acc_floats_of(const nslam_dec_grad& dg) { return (int)((dg.count + 3) & ~int64_t(3)); }
-
-// Slab cap: kMaxSlabs, or NSLAM_MAX_SLABS from the environment (tests use it to reach the
-// multi-tile read-modify-write mode at small sizes).
-int64_t max_slabs() {
-  const char* e = getenv("NSLAM_MAX_SLABS");
-  const long v = e ? strtol(e, nullptr, 10) : 0;
-  return v > 0 ? v : kMaxSlabs;
-}
-
-// parameter-gradient slabs for a decoder: one per tile up to the cap, else one per launched wave
-// (the cap rounded up to whole workgroups), each wave walking tiles with grid stride
-int64_t n_slabs(int64_t tiles) {
-  const int64_t cap = max_slabs();
-  return tiles <= cap ? tiles : (cap + kWavesBwd - 1) / kWavesBwd * kWavesBwd;
-}
-
-template <int DEC, int WG, bool PG, bool FIRST, bool SAVED = false>
-int launch_one(const QueryKArgs& a, float* slab, int acc, int64_t blocks, hipStream_t s) {
-  hipLaunchKernelGGL((k_dec_bwd<DEC, WG, PG, FIRST, SAVED>), dim3((unsigned)blocks), dim3(64 * kWavesBwd), 0, s, a,
-                     slab, acc);
-  return hip_status();
-}
-
-template <int DEC, int WG, bool PG>
-int launch_dec_bwd(const QueryKArgs& a, bool first, float* slab, hipStream_t s) {
-  const int64_t tiles = (a.n + 31) / 32;
-  if (WG == 0) {
-    const int64_t blocks = (tiles + kWavesBwd - 1) / kWavesBwd;
-    if (a.c.saved_masks)
-      return first ? launch_one<DEC, 0, PG, true, true>(a, nullptr, 0, blocks, s)
-                   : launch_one<DEC, 0, PG, false, true>(a, nullptr, 0, blocks, s);
-    return first ? launch_one<DEC, 0, PG, true>(a, nullptr, 0, blocks, s)
-                 : launch_one<DEC, 0, PG, false>(a, nullptr, 0, blocks, s);
-  }
-  const nslam_dec_grad& dg = a.c.dgrad[DEC];
-  const int acc = acc_floats_of(dg);
-  const int64_t nslab = n_slabs(tiles);
-  const int64_t blocks = (nslab + kWavesBwd - 1) / kWavesBwd;
-  // the colour decoder's weight gradients read the forward's activation tape when it is there
-  constexpr bool kTapeable = DEC == NSLAM_DEC_COLOR && !PG;
-  const bool tape = kTapeable && a.c.act_tape && a.c.saved_masks;
-  int rc;
-  if (tiles > max_slabs() && hipMemsetAsync(slab, 0, (size_t)nslab * acc * sizeof(float), s) != hipSuccess)
-    return hip_status();
-  if constexpr (kTapeable) {
-    if (tape) {
-      if (tiles <= max_slabs())
-        rc = first ? launch_one<DEC, 1, PG, true, true>(a, slab, acc, blocks, s)
-                   : launch_one<DEC, 1, PG, false, true>(a, slab, acc, blocks, s);
-      else
-        rc = first ? launch_one<DEC, 2, PG, true, true>(a, slab, acc, blocks, s)
-                   : launch_one<DEC, 2, PG, false, true>(a, slab, acc, blocks, s);
-      if (rc) return rc;
-      hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((dg.count + 63) / 64)), dim3(64 * kReduceWaves), 0, s, slab,
-                         nslab, acc, (int)dg.count, dg.base);
-      return hip_status();
-    }
-  }
-  if (tiles <= max_slabs()) {
-    rc = first ? launch_one<DEC, 1, PG, true>(a, slab, acc, blocks, s)
-               : launch_one<DEC, 1, PG, false>(a, slab, acc, blocks, s);
-  } else {
-    rc = first ? launch_one<DEC, 2, PG, true>(a, slab, acc, blocks, s)
-               : launch_one<DEC, 2, PG, false>(a, slab, acc, blocks, s);
-  }
-  if (rc) return rc;
-  hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((dg.count + 63) / 64)), dim3(64 * kReduceWaves), 0, s, slab,
-                     nslab, acc, (int)dg.count, dg.base);
-  return hip_status();
-}
-
-template <int DEC>
-int dispatch_dec_bwd(const QueryKArgs& a, bool first, float* slab, hipStream_t s) {
-  const bool wg = a.c.dgrad[DEC].base != nullptr;
-  const bool pg = a.c.need_pts_grad != 0;
-  if (wg && pg && a.c.saved_masks) {
-    // Split instead of the combined kernel (which spills ~100 VGPRs): parameter + grid gradients
-    // first, then d/dpts from the saved masks with the grid scatter switched off.
-    int rc = launch_dec_bwd<DEC, 1, false>(a, first, slab, s);
-    if (rc) return rc;
-    QueryKArgs b = a;
-    b.c.grid[DEC].grad = nullptr;
-    b.c.dgrad[DEC].base = nullptr;
-    return launch_dec_bwd<DEC, 0, true>(b, first, nullptr, s);
-  }
-  if (wg && pg) return launch_dec_bwd<DEC, 1, true>(a, first, slab, s);
-  if (wg) return launch_dec_bwd<DEC, 1, false>(a, first, slab, s);
-  if (pg) return launch_dec_bwd<DEC, 0, true>(a, first, slab, s);
-  return launch_dec_bwd<DEC, 0, false>(a, first, slab, s);
-}
-
-size_t bwd_ws_bytes(const nslam_query_cfg* cfg, int64_t n_pts) {
-  size_t need = 0;
-  const int64_t tiles = (n_pts + 31) / 32;
-  for (int d = 0; d < 4; ++d) {
-    const nslam_dec_grad& dg = cfg->dgrad[d];
-    if (!dg.base || dg.count <= 0) continue;
-    const size_t b = (size_t)n_slabs(tiles) * acc_floats_of(dg) * sizeof(float);
-    need = b > need ? b : need;  // decoders run one after the other on the stream: one region
-  }
-  return need;
-}
-
-size_t dec_ws_bytes(const nslam_query_cfg* cfg, int dec, int64_t n_pts) {
-  const nslam_dec_grad& dg = cfg->dgrad[dec];
-  if (!dg.base || dg.count <= 0) return 0;
-  return (size_t)n_slabs((n_pts + 31) / 32) * acc_floats_of(dg) * sizeof(float);
-}
-
-bool stage_uses(int stage, int dec) {
-  switch (stage) {
-    case NSLAM_STAGE_COARSE: return dec == NSLAM_DEC_COARSE;
-    case NSLAM_STAGE_MIDDLE: return dec == NSLAM_DEC_MIDDLE;
-    case NSLAM_STAGE_FINE: return dec == NSLAM_DEC_MIDDLE || dec == NSLAM_DEC_FINE;
-    default: return dec != NSLAM_DEC_COARSE;
-  }
-}
-
-}  // namespace
 
 extern "C" int nslam_query_bwd_decoder(const nslam_query_cfg* cfg, int32_t dec, int32_t accumulate_pts,
                                        const double* pts, int64_t n_pts, const float* g_raw, double* g_pts, void* ws,

@@ -81,10 +81,54 @@ def stats(sc, ro, rd, z, keep, perm, dev):
                 u += int(torch.unique(r).numel())
             uniq[g] = u
         inmask = int((m[rt.reshape(-1)].view(T, 32, 8) & kt[..., None]).sum())
+        # flush wave-instructions of the uniform walk (one per corner pair (2j, 2j+1) with a nonzero
+        # frustum weight), run-merge only vs with the carry-over of shared corners
+        ins_run, ins_carry = walk_counts(rt, ct, kt, m, dims)
         us = "  ".join(f"{g}-tile {u} ({u / total:.2f})" for g, u in uniq.items())
         print(f"{key:12s} dims {tuple(dims)} frustum rows {int(m.sum())}/{m.numel()}  corner contributions {total}  "
               f"after run-merge {runs} ({runs / total:.2f})  unique rows per {us}  "
-              f"on frustum rows {inmask} ({inmask / total:.2f})", flush=True)
+              f"on frustum rows {inmask} ({inmask / total:.2f})  flush instructions run-merge {ins_run} "
+              f"carry {ins_carry} ({ins_carry / max(ins_run, 1):.2f})", flush=True)
+
+
+def walk_counts(rt, ct, kt, m, dims):
+    Z, Y, X = dims
+    rt, ct, kt, m = rt.cpu().numpy(), ct.cpu().numpy(), kt.cpu().numpy(), m.cpu().numpy()
+    n_run = n_carry = 0
+    for t in range(rt.shape[0]):
+        live_run = [False] * 8
+        live_c = [False] * 8
+        cur = None
+        for p in range(32):
+            c = int(ct[t, p])
+            on = [bool(kt[t, p] and m[rt[t, p, k]]) for k in range(8)]
+            if c != cur:
+                if cur is not None:
+                    n_run += sum(1 for j in range(4) if live_run[2 * j] or live_run[2 * j + 1])
+                    cz, cy, cx = cur // (Y * X), (cur // X) % Y, cur % X
+                    nz, ny, nx = c // (Y * X), (c // X) % Y, c % X
+                    ax, ay, az = nx - cx, ny - cy, nz - cz
+                    adj = max(abs(ax), abs(ay), abs(az)) <= 1
+                    flushed = [False] * 8
+                    new = [False] * 8
+                    for k in range(8):
+                        dx, dy, dz = k & 1, (k >> 1) & 1, k >> 2
+                        mx, my, mz = dx - ax, dy - ay, dz - az
+                        if adj and 0 <= mx <= 1 and 0 <= my <= 1 and 0 <= mz <= 1:
+                            new[mx + 2 * my + 4 * mz] = live_c[k]
+                        else:
+                            flushed[k] = live_c[k]
+                    n_carry += sum(1 for j in range(4) if flushed[2 * j] or flushed[2 * j + 1])
+                    live_c = new
+                else:
+                    live_c = [False] * 8
+                live_run = [False] * 8
+                cur = c
+            live_run = [a or b for a, b in zip(live_run, on)]
+            live_c = [a or b for a, b in zip(live_c, on)]
+        n_run += sum(1 for j in range(4) if live_run[2 * j] or live_run[2 * j + 1])
+        n_carry += sum(1 for j in range(4) if live_c[2 * j] or live_c[2 * j + 1])
+    return n_run, n_carry
 
 
 if __name__ == "__main__":
