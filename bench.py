@@ -26,6 +26,10 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 # configs/Replica/room0.yaml:3, configs/Replica/replica.yaml cam + mapping, configs/nice_slam.yaml
+# the next iteration's pixel gather + sampler run beside this iteration's render/backward
+# (engine.MappingEngine.iteration(prefetch=True)); --no-prefetch for the strictly serial step
+PREFETCH = True
+
 ROOM0 = {
     "bound": [[-2.9, 8.9], [-3.2, 5.5], [-3.5, 3.3]], "bound_divisible": 0.32,
     "grid_len": {"coarse": 2.0, "middle": 0.32, "fine": 0.16, "color": 0.16},
@@ -97,6 +101,31 @@ def rot(yaw, pitch):
     Rz = torch.tensor([[cy, -sy, 0], [sy, cy, 0], [0, 0, 1]], dtype=torch.float64)
     Rx = torch.tensor([[1, 0, 0], [0, cp, -sp], [0, sp, cp]], dtype=torch.float64)
     return Rz @ Rx
+
+
+def capture_step_graphs(fn, n=2):
+    """Capture `n` consecutive calls of fn as hipGraphs, replayed in turn (a prefetching engine
+    alternates between two ray-buffer sets, so consecutive iterations are two different graphs).
+    Returns (replay callable, mode)."""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2 * n):
+            fn()
+    torch.cuda.current_stream().wait_stream(side)
+    graphs = []
+    for _ in range(n):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            fn()
+        graphs.append(g)
+    state = {"i": 0}
+
+    def replay():
+        graphs[state["i"]].replay()
+        state["i"] = (state["i"] + 1) % n
+
+    return replay, "hipgraph"
 
 
 class Room0Scene:
@@ -214,7 +243,7 @@ class Room0Scene:
         self.engine.iteration(
             stage, self.frames, None, n, (H, W), (cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"]), self.opt,
             trainable_decoders=("color",), exchange=self.exchange if sharded else None, n_kept=self.kept,
-            seed=1000, world=world, rank=self.rank if sharded else 0)
+            seed=1000, world=world, rank=self.rank if sharded else 0, prefetch=PREFETCH)
 
     def step_autograd(self, stage="color", sharded=False):
         """The same iteration through the autograd drop-in path (dense Adam, torch glue ops).
@@ -482,16 +511,8 @@ def room0_frame_rate(scene, reps=20):
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            fn()
-        torch.cuda.current_stream().wait_stream(side)
         try:
-            with torch.cuda.graph(g):
-                fn()
-            run, mode = g.replay, "hipgraph"
+            run, mode = capture_step_graphs(fn)
         except Exception:  # pragma: no cover - eager fallback
             run, mode = fn, "eager"
         run()
@@ -574,9 +595,13 @@ def main():
                     help="override mapping pixels per iteration (scaling studies; the metric uses room0's 1000)")
     ap.add_argument("--path", choices=("fused", "autograd"), default="fused",
                     help="fused engine (default) or the autograd drop-in path")
+    ap.add_argument("--no-prefetch", action="store_true",
+                    help="draw + sample each iteration's rays inside it (no overlap with the previous backward)")
     ap.add_argument("--leg", choices=("frames", "stress", "bulk", "frame_io"), default=None,
                     help="run one auxiliary measurement and print its JSON (bench.py spawns these itself)")
     args = ap.parse_args()
+    global PREFETCH
+    PREFETCH = not args.no_prefetch
     if args.leg:
         return leg_main(args.leg)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -602,19 +627,12 @@ def main():
     torch.cuda.synchronize()
     graph, mode = None, "eager"
     if not args.eager and not (world > 1 and args.backend == "gloo"):
-        try:  # capture one whole mapping iteration as a hipGraph (removes per-op host launch cost)
-            side = torch.cuda.Stream()
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                for _ in range(2):
-                    scene.step(sharded=sharded)
-            torch.cuda.current_stream().wait_stream(side)
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                scene.step(sharded=sharded)
-            graph.replay()
+        try:  # whole mapping iterations as hipGraphs (removes per-op host launch cost); two of them,
+            # replayed in turn, since the prefetching engine alternates its ray buffers
+            graph, mode = capture_step_graphs(lambda: scene.step(sharded=sharded))
+            graph()
+            graph()
             torch.cuda.synchronize()
-            mode = "hipgraph"
         except Exception as e:  # pragma: no cover - fall back to eager launches
             print(f"graph capture failed, eager mode: {e!r}", file=sys.stderr)
             graph = None
@@ -625,7 +643,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         if graph is not None:
-            graph.replay()
+            graph()
         else:
             scene.step(sharded=sharded)
     torch.cuda.synchronize()
@@ -662,7 +680,7 @@ def main():
             "metric": "ray-samples/sec (fwd+bwd) per mapping iter; frames/sec on Replica room0",
             "value": samples_all / dt_max, "unit": "ray-samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt_max / args.steps * 1e3, "higher_is_better": True,
-            "launch_mode": mode,
+            "launch_mode": mode, "ray_prefetch": PREFETCH,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32 (z, depth, var in f64)",
             "data": "synthetic room0-shaped frames (analytic depth, random colour), seeded random-init decoders",
             "config": {"workload": "Replica room0 mapping iteration, colour stage: 1000 pixels x 48 samples "

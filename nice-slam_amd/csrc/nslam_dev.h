@@ -101,9 +101,16 @@ __device__ __forceinline__ f32x16 zero16() {
   return z;
 }
 
+#ifdef NSLAM_EXP_HOTFRAG  // timing experiment only: every fragment read hits one 4 KiB block
+__device__ float g_hot_frag[1024];
+#endif
+
 // acc += Wblock * X   (frag: packed [lane][16])
 __device__ __forceinline__ void gemm_acc(f32x16& acc, const float* __restrict__ frag, const f32x16& x,
                                          int lane) {
+#ifdef NSLAM_EXP_HOTFRAG
+  frag = g_hot_frag;
+#endif
   const f32x4* f = reinterpret_cast<const f32x4*>(frag) + lane * 4;
   const f32x4 a0 = f[0], a1 = f[1], a2 = f[2], a3 = f[3];
   acc = mfma32(a0[0], x[0], acc);

@@ -43,10 +43,26 @@ extern "C" int nslam_query_fwd_ws(const nslam_query_cfg* cfg, const double* pts,
   const int64_t groups = ((n_pts + 31) / 32 + 3) / 4;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   float* occ = reinterpret_cast<float*>(ws);
+  static const int color_parts = [] {  // NSLAM_FWD_PARTS=2|3 (experiments); default 3
+    const char* e = getenv("NSLAM_FWD_PARTS");
+    return e && atoi(e) == 2 ? 2 : 3;
+  }();
+  const dim3 b256(256);
   if (cfg->stage == NSLAM_STAGE_FINE)
-    hipLaunchKernelGGL(k_query_fwd_parts<NSLAM_STAGE_FINE>, dim3((unsigned)(groups * 2)), dim3(256), 0, s, a, occ);
+    hipLaunchKernelGGL((k_query_fwd_parts<NSLAM_STAGE_FINE, 2, false>), dim3((unsigned)(groups * 2)), b256, 0, s, a,
+                       occ);
+  else if (color_parts == 2 && cfg->act_tape)
+    hipLaunchKernelGGL((k_query_fwd_parts<NSLAM_STAGE_COLOR, 2, true>), dim3((unsigned)(groups * 2)), b256, 0, s, a,
+                       occ);
+  else if (color_parts == 2)
+    hipLaunchKernelGGL((k_query_fwd_parts<NSLAM_STAGE_COLOR, 2, false>), dim3((unsigned)(groups * 2)), b256, 0, s, a,
+                       occ);
+  else if (cfg->act_tape)
+    hipLaunchKernelGGL((k_query_fwd_parts<NSLAM_STAGE_COLOR, 3, true>), dim3((unsigned)(groups * 3)), b256, 0, s, a,
+                       occ);
   else
-    hipLaunchKernelGGL(k_query_fwd_parts<NSLAM_STAGE_COLOR>, dim3((unsigned)(groups * 3)), dim3(256), 0, s, a, occ);
+    hipLaunchKernelGGL((k_query_fwd_parts<NSLAM_STAGE_COLOR, 3, false>), dim3((unsigned)(groups * 3)), b256, 0, s, a,
+                       occ);
   if (!cfg->defer_occ)  // else the consumer adds ws on read (nslam_loss_cfg.occ_add)
     hipLaunchKernelGGL(k_occ_combine, dim3((unsigned)((n_pts + 255) / 256)), dim3(256), 0, s, raw, occ, n_pts);
   return hip_status();

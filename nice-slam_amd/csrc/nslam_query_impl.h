@@ -147,35 +147,24 @@ __device__ __forceinline__ void load_masks(const QueryKArgs& a, int dec, int64_t
 }
 
 // Activation tape of the colour decoder (ABI v9 nslam_query_cfg.act_tape): the forward stores the
-// post-ReLU hidden tiles h0..h4 of every tile (C layout, [tile][layer][q][64 lanes] float4, so one
-// store / load instruction moves 1 KiB contiguous) and the weight-gradient backward reads them
+// post-ReLU hidden tiles h0..h4 of every tile (C layout) and the weight-gradient backward reads them
 // instead of recomputing the decoder (it needs them as the inputs of dW; Mapper.py:503).
 constexpr int kTapeFloats = 5 * 16 * 64;  // per tile
+// Layout [tile][layer][register r][64 lanes] float: every store / load instruction moves 256 B
+// contiguous, and no 4-register grouping of the tile is needed (a float4 layout cost the forward
+// ~30 VGPRs of copies).
 __device__ __forceinline__ void tape_store(float* __restrict__ t, int i, const f32x16& v, int lane) {
-  f32x4* p = reinterpret_cast<f32x4*>(t) + i * 256 + lane;
+  float* p = t + i * 1024 + lane;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    f32x4 w;
-    w[0] = v[4 * q];
-    w[1] = v[4 * q + 1];
-    w[2] = v[4 * q + 2];
-    w[3] = v[4 * q + 3];
-    p[q * 64] = w;
-  }
+  for (int r = 0; r < 16; ++r) p[r * 64] = v[r];
 }
 __device__ __forceinline__ f32x16 tape_load(const float* __restrict__ t, int i, int lane) {
   // laundered base: keeps the scheduler from hoisting all five tile loads (80 VGPRs) to the top
   asm volatile("" : "+s"(t));
-  const f32x4* p = reinterpret_cast<const f32x4*>(t) + i * 256 + lane;
+  const float* p = t + i * 1024 + lane;
   f32x16 v;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const f32x4 w = p[q * 64];
-    v[4 * q] = w[0];
-    v[4 * q + 1] = w[1];
-    v[4 * q + 2] = w[2];
-    v[4 * q + 3] = w[3];
-  }
+  for (int r = 0; r < 16; ++r) v[r] = p[r * 64];
   return v;
 }
 
@@ -269,7 +258,7 @@ __device__ __forceinline__ f32x16 fc_branch(const float* __restrict__ pk, const 
   return z;
 }
 
-template <int NC, bool KEEP, bool PHF = false>
+template <int NC, bool KEEP, bool PHF = false, bool TAPE = false>
 __device__ __forceinline__ f32x16 xyz_forward(const float* __restrict__ pk, const f32x16 (&cin)[NC],
                                               const float x[3], int lane, uint32_t m[5], f32x16* hs,
                                               float* __restrict__ tape = nullptr) {
@@ -288,31 +277,31 @@ __device__ __forceinline__ f32x16 xyz_forward(const float* __restrict__ pk, cons
   m[0] = mask16(a);
   f32x16 h = relu16(a) + fc_branch<NC>(pk, L, 0, cin, lane);
   if (KEEP) hs[0] = h;
-  if (tape) tape_store(tape, 0, h, lane);
+  if (TAPE) tape_store(tape, 0, h, lane);
   a = vec_tile(pk + L.Bias(1), lane);
   gemm_acc(a, pk + L.L1() * NSLAM_FRAG, h, lane);
   m[1] = mask16(a);
   h = relu16(a) + fc_branch<NC>(pk, L, 1, cin, lane);
   if (KEEP) hs[1] = h;
-  if (tape) tape_store(tape, 1, h, lane);
+  if (TAPE) tape_store(tape, 1, h, lane);
   PHF_(6);
   a = vec_tile(pk + L.Bias(2), lane);
   gemm_acc(a, pk + L.L2() * NSLAM_FRAG, h, lane);
   m[2] = mask16(a);
   h = relu16(a) + fc_branch<NC>(pk, L, 2, cin, lane);
   if (KEEP) hs[2] = h;
-  if (tape) tape_store(tape, 2, h, lane);
+  if (TAPE) tape_store(tape, 2, h, lane);
   gemm_acc(a3, pk + (L.L3() + 3) * NSLAM_FRAG, h, lane);
   m[3] = mask16(a3);
   h = relu16(a3) + fc_branch<NC>(pk, L, 3, cin, lane);
   if (KEEP) hs[3] = h;
-  if (tape) tape_store(tape, 3, h, lane);
+  if (TAPE) tape_store(tape, 3, h, lane);
   PHF_(7);
   a = vec_tile(pk + L.Bias(4), lane);
   gemm_acc(a, pk + L.L4() * NSLAM_FRAG, h, lane);
   m[4] = mask16(a);
   h = relu16(a) + fc_branch<NC>(pk, L, 4, cin, lane);
-  if (tape) tape_store(tape, 4, h, lane);
+  if (TAPE) tape_store(tape, 4, h, lane);
   PHF_(8);
   return h;
 #undef PHF_
@@ -900,6 +889,8 @@ __device__ __forceinline__ void stage_corners(const Corners& cr, const int32_t* 
 __device__ __forceinline__ void grid_add(float* p, float v) {
 #if defined(NSLAM_EXP_NOATOMIC)
   asm volatile("" ::"v"(v), "v"(p));
+#elif defined(NSLAM_EXP_HALFATOMIC)  // every other grid row only: sensitivity to the atomic count
+  if (((reinterpret_cast<uintptr_t>(p) >> 7) & 1) == 0) unsafeAtomicAdd(p, v);
 #elif defined(NSLAM_EXP_STOREATOMIC)
   __builtin_nontemporal_store(v, p);
 #else
@@ -1139,8 +1130,11 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd(QueryKArgs a) {
       const f32x16 cc[1] = {gather_tile(a.c.grid[NSLAM_DEC_COLOR].data, cr, lane)};
       const float* pk = a.c.packed[NSLAM_DEC_COLOR];
       const XyzPack L{1};
-      float* tp = a.c.act_tape ? a.c.act_tape + tile * kTapeFloats : nullptr;
-      const f32x16 h4 = xyz_forward<1, false>(pk, cc, q.x, lane, m, nullptr, tp);
+      f32x16 h4;
+      if (a.c.act_tape)
+        h4 = xyz_forward<1, false, false, true>(pk, cc, q.x, lane, m, nullptr, a.c.act_tape + tile * kTapeFloats);
+      else
+        h4 = xyz_forward<1, false>(pk, cc, q.x, lane, m, nullptr);
       save_masks(a, NSLAM_DEC_COLOR, tile, m, lane);
 #pragma unroll
       for (int j = 0; j < 3; ++j) out[j] = out_row(pk + L.Wo(), pk + L.Bo(), j, h4, lane);
@@ -1166,72 +1160,112 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd(QueryKArgs a) {
 //   part 2  colour: raw[p][0..2]
 // and k_occ_combine then forms raw[p][3] = fine_occ + middle_occ (decoder.py:331-334, the
 // reference's operand order) — exactly 100 outside the bound (0 + 100; Renderer.py:57).
+// One decoder of the decoder-parallel forward for this wave's tile.
+__device__ __forceinline__ void fwd_part_middle(const QueryKArgs& a, const Pt& q, int64_t tile, int64_t idx, int lane,
+                                                float* __restrict__ occ_mid) {
+  const int h = lane >> 5;
+  uint32_t m[5];
+  Corners cr;
+  grid_corners(cr, a.c.grid[NSLAM_DEC_MIDDLE], q);
+  PHASE(0, 2);
+  const f32x16 cm = gather_tile(a.c.grid[NSLAM_DEC_MIDDLE].data, cr, lane);
+  PHASE(0, 3);
+  const float* pk = a.c.packed[NSLAM_DEC_MIDDLE];
+  const XyzPack L{1};
+  const f32x16 cms[1] = {cm};
+  const f32x16 h4 = xyz_forward<1, false, true>(pk, cms, q.x, lane, m, nullptr);
+  save_masks(a, NSLAM_DEC_MIDDLE, tile, m, lane);
+  float o = out_row(pk + L.Wo(), pk + L.Bo(), 0, h4, lane);
+  if (!q.inside) o = 100.f;
+  if (h == 0 && q.valid) occ_mid[idx] = o;
+}
+
 template <int STAGE>
+__device__ __forceinline__ void fwd_part_fine(const QueryKArgs& a, const Pt& q, int64_t tile, int64_t idx, int lane) {
+  // the fine decoder also reads the middle feature (decoder.py:184-187)
+  const int h = lane >> 5;
+  uint32_t m[5];
+  Corners cm, cr;
+  grid_corners(cm, a.c.grid[NSLAM_DEC_MIDDLE], q);
+  grid_corners(cr, a.c.grid[NSLAM_DEC_FINE], q);
+  PHASE(0, 2);
+  const f32x16 cf[2] = {gather_tile(a.c.grid[NSLAM_DEC_FINE].data, cr, lane),
+                        gather_tile(a.c.grid[NSLAM_DEC_MIDDLE].data, cm, lane)};
+  PHASE(0, 3);
+  const float* pk = a.c.packed[NSLAM_DEC_FINE];
+  const XyzPack L{2};
+  const f32x16 h4 = xyz_forward<2, false, true>(pk, cf, q.x, lane, m, nullptr);
+  save_masks(a, NSLAM_DEC_FINE, tile, m, lane);
+  float o = out_row(pk + L.Wo(), pk + L.Bo(), 0, h4, lane);
+  if (!q.inside) o = 0.f;
+  if (h == 0 && q.valid) {
+    if (STAGE == NSLAM_STAGE_COLOR) {
+      a.raw[idx * 4 + 3] = o;
+    } else {
+      f32x4 v = {0.f, 0.f, 0.f, o};
+      *reinterpret_cast<f32x4*>(a.raw + idx * 4) = v;
+    }
+  }
+}
+
+template <bool TAPE>
+__device__ __forceinline__ void fwd_part_color(const QueryKArgs& a, const Pt& q, int64_t tile, int64_t idx, int lane) {
+  const int h = lane >> 5;
+  uint32_t m[5];
+  Corners cr;
+  grid_corners(cr, a.c.grid[NSLAM_DEC_COLOR], q);
+  PHASE(0, 2);
+  const f32x16 cc[1] = {gather_tile(a.c.grid[NSLAM_DEC_COLOR].data, cr, lane)};
+  PHASE(0, 3);
+  const float* pk = a.c.packed[NSLAM_DEC_COLOR];
+  const XyzPack L{1};
+  float* tp = TAPE ? a.c.act_tape + tile * kTapeFloats : nullptr;
+  const f32x16 h4 = xyz_forward<1, false, true, TAPE>(pk, cc, q.x, lane, m, nullptr, tp);
+  save_masks(a, NSLAM_DEC_COLOR, tile, m, lane);
+  float o[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) o[j] = out_row(pk + L.Wo(), pk + L.Bo(), j, h4, lane);
+  if (h == 0 && q.valid) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) a.raw[idx * 4 + j] = o[j];
+  }
+}
+
+// Decoder-parallel forward (fine and colour stages): each workgroup evaluates ONE part for its 4
+// tiles, so a launch has 2-3x the waves of k_query_fwd and every wave a fraction of the serial
+// MFMA/gather chain.  Parts are interleaved over blockIdx (heavy and light workgroups mix on
+// every CU).  NPARTS = 3 (colour stage): middle | fine | colour; NPARTS = 2: fine stage middle |
+// fine, or colour stage (middle then colour) | fine — fewer, balanced waves (3000 at room0) that
+// fit the chip's wave slots in one round.
+//   middle: occ_mid[p] = inside ? middle_occ : 100
+//   fine:   raw[p][3]  = inside ? fine_occ : 0     (fine stage: the whole row)
+//   colour: raw[p][0..2]
+// and k_occ_combine (or the loss kernel, defer_occ) then forms raw[p][3] = fine_occ + middle_occ
+// (decoder.py:331-334, the reference's operand order) — exactly 100 outside the bound (0 + 100;
+// Renderer.py:57).
+template <int STAGE, int NPARTS, bool TAPE>
 __global__ __launch_bounds__(256, 2) void k_query_fwd_parts(QueryKArgs a, float* __restrict__ occ_mid) {
-  constexpr int NPARTS = STAGE == NSLAM_STAGE_COLOR ? 3 : 2;
   const int part = (int)(blockIdx.x % NPARTS);
   const int lane = threadIdx.x & 63;
   const int64_t tile = (int64_t)(blockIdx.x / NPARTS) * 4 + wave_id();
   if (tile * 32 >= a.n) return;  // wave-uniform
-  const int h = lane >> 5;
   const int64_t idx = tile * 32 + (lane & 31);
   PHASE(0, 0);
   const Pt q = load_point(a, idx);
   PHASE(0, 1);
-  uint32_t m[5];
-  Corners cr;
-  if (part == 0) {
-    grid_corners(cr, a.c.grid[NSLAM_DEC_MIDDLE], q);
-    PHASE(0, 2);
-    const f32x16 cm = gather_tile(a.c.grid[NSLAM_DEC_MIDDLE].data, cr, lane);
-    PHASE(0, 3);
-    const float* pk = a.c.packed[NSLAM_DEC_MIDDLE];
-    const XyzPack L{1};
-    const f32x16 cms[1] = {cm};
-    const f32x16 h4 = xyz_forward<1, false, true>(pk, cms, q.x, lane, m, nullptr);
-    save_masks(a, NSLAM_DEC_MIDDLE, tile, m, lane);
-    float o = out_row(pk + L.Wo(), pk + L.Bo(), 0, h4, lane);
-    if (!q.inside) o = 100.f;
-    if (h == 0 && q.valid) occ_mid[idx] = o;
-  } else if (part == 1) {  // the fine decoder also reads the middle feature (decoder.py:184-187)
-    Corners cm;
-    grid_corners(cm, a.c.grid[NSLAM_DEC_MIDDLE], q);
-    grid_corners(cr, a.c.grid[NSLAM_DEC_FINE], q);
-    PHASE(0, 2);
-    const f32x16 cf[2] = {gather_tile(a.c.grid[NSLAM_DEC_FINE].data, cr, lane),
-                          gather_tile(a.c.grid[NSLAM_DEC_MIDDLE].data, cm, lane)};
-    PHASE(0, 3);
-    const float* pk = a.c.packed[NSLAM_DEC_FINE];
-    const XyzPack L{2};
-    const f32x16 h4 = xyz_forward<2, false, true>(pk, cf, q.x, lane, m, nullptr);
-    save_masks(a, NSLAM_DEC_FINE, tile, m, lane);
-    float o = out_row(pk + L.Wo(), pk + L.Bo(), 0, h4, lane);
-    if (!q.inside) o = 0.f;
-    if (h == 0 && q.valid) {
-      if (STAGE == NSLAM_STAGE_COLOR) {
-        a.raw[idx * 4 + 3] = o;
-      } else {
-        f32x4 v = {0.f, 0.f, 0.f, o};
-        *reinterpret_cast<f32x4*>(a.raw + idx * 4) = v;
-      }
+  if (NPARTS == 2 && STAGE == NSLAM_STAGE_COLOR) {
+    if (part == 0) {
+      fwd_part_middle(a, q, tile, idx, lane, occ_mid);
+      fwd_part_color<TAPE>(a, q, tile, idx, lane);
+    } else {
+      fwd_part_fine<STAGE>(a, q, tile, idx, lane);
     }
+  } else if (part == 0) {
+    fwd_part_middle(a, q, tile, idx, lane, occ_mid);
+  } else if (part == 1) {
+    fwd_part_fine<STAGE>(a, q, tile, idx, lane);
   } else if (STAGE == NSLAM_STAGE_COLOR) {
-    grid_corners(cr, a.c.grid[NSLAM_DEC_COLOR], q);
-    PHASE(0, 2);
-    const f32x16 cc[1] = {gather_tile(a.c.grid[NSLAM_DEC_COLOR].data, cr, lane)};
-    PHASE(0, 3);
-    const float* pk = a.c.packed[NSLAM_DEC_COLOR];
-    const XyzPack L{1};
-    float* tp = a.c.act_tape ? a.c.act_tape + tile * kTapeFloats : nullptr;
-    const f32x16 h4 = xyz_forward<1, false, true>(pk, cc, q.x, lane, m, nullptr, tp);
-    save_masks(a, NSLAM_DEC_COLOR, tile, m, lane);
-    float o[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) o[j] = out_row(pk + L.Wo(), pk + L.Bo(), j, h4, lane);
-    if (h == 0 && q.valid) {
-#pragma unroll
-      for (int j = 0; j < 3; ++j) a.raw[idx * 4 + j] = o[j];
-    }
+    fwd_part_color<TAPE>(a, q, tile, idx, lane);
   }
   PHASE(0, 9);
 }

@@ -93,6 +93,9 @@ class MappingEngine:
         self._tape = None   # colour-decoder activation tape of the last query_fwd (ABI v9)
         self.occ_add = None  # middle occupancy of the last deferred-combine query_fwd
         self._draws = None   # (seed, ops.PixelDraws) of in-kernel pixel draws
+        self._pre = None     # (key, [buffer set 0, buffer set 1]) ray batches of the prefetch loop
+        self._parity = 0     # which set holds this iteration's batch
+        self._pre_stream = None
         self._side = []     # side streams of the concurrent decoder backward
         self.concurrent = True
         self.priority = False  # concurrent: run the weight-gradient branch on a high-priority stream
@@ -249,7 +252,7 @@ class MappingEngine:
 
     def iteration(self, stage, frames, pix, n_per, hw, intrinsics, optimizer, trainable_decoders=("color",),
                   gt_max=None, allreduce=None, use_gt_in_sampler=True, exchange=None, n_kept=None, seed=0,
-                  world=1, rank=0):
+                  world=1, rank=0, prefetch=False):
         """One mapping iteration; returns (ray_loss f64 [N], keep uint8 [N]) as device tensors.
 
         frames: [(depth, color, c2w)] of the window; pix: int64 [len(frames)*n_per] randint
@@ -263,6 +266,12 @@ class MappingEngine:
         allreduce: callable(list of grads) run before Adam (ray sharding, dense);
         exchange: callable(grid keys, decoder names) run before Adam instead — the frustum-compacted
         exchange (distributed.SparseGradExchange).
+        prefetch (device draws only): the pixel gather and sampler of the NEXT iteration run on a side
+        stream while this one renders and back-propagates — they depend only on the frames and the
+        device draw counter, not on the map.  Batches alternate between two persistent buffer sets
+        (self._parity), so a hipGraph of an even and one of an odd iteration replay alternately
+        with no copies.  Each call still draws, samples, renders and updates one batch; the first
+        call draws its own batch first.
         """
         H, W = hw
         fx, fy, cx, cy = intrinsics
@@ -272,16 +281,42 @@ class MappingEngine:
             if self._draws is None or self._draws[0] != key:
                 self._draws = (key, ops.PixelDraws(seed, self.device, world, rank, with_max=world > 1))
             draw = self._draws[1]
-        ro, rd, gd, gc, keep = ops.gather_rays(frames, pix, n_per, H, W, (0, H, 0, W), fx, fy, cx, cy, self.bound,
-                                               draw=draw, n_kept=n_kept)
-        gsamp = gd if (use_gt_in_sampler and stage != "coarse") else None
-        if gsamp is None:
-            gm = None
-        elif draw is not None and draw.gt_max is not None:  # global batch max from the gather kernel
-            gm = draw.gt_max
+
+        def rays(out=None):  # pixels → rays + inside mask, then the sampler (Mapper.py:457-484, Renderer.py:82-174)
+            ro, rd, gd, gc, keep = ops.gather_rays(frames, pix, n_per, H, W, (0, H, 0, W), fx, fy, cx, cy,
+                                                   self.bound, draw=draw, n_kept=n_kept,
+                                                   out=None if out is None else out[:5])
+            gsamp = gd if (use_gt_in_sampler and stage != "coarse") else None
+            if gsamp is None:
+                gm = None
+            elif draw is not None and draw.gt_max is not None:  # global batch max from the gather kernel
+                gm = draw.gt_max
+            else:
+                gm = gt_max(gd) if gt_max is not None else None
+            z = ops.sample_z(ro, rd, gsamp, self.bound, self.n_strat, self.n_surf, self.lindisp, gt_max=gm,
+                             out=None if out is None else out[5])
+            return [ro, rd, gd, gc, keep, z]
+
+        prefetch = prefetch and pix is None
+        side = None
+        if prefetch:
+            pkey = (stage, len(frames), n_per, hw, use_gt_in_sampler, seed, world, rank)
+            if self._pre is None or self._pre[0] != pkey:
+                first = rays()  # first call: this iteration's batch (set 0), then a same-shaped set 1
+                self._pre = (pkey, [first, [torch.empty_like(t) for t in first]])
+                self._parity = 0
+            cur, nxt = self._pre[1][self._parity], self._pre[1][1 - self._parity]
+            self._parity ^= 1
+            main = torch.cuda.current_stream(self.device)
+            if self._pre_stream is None:
+                self._pre_stream = torch.cuda.Stream(self.device)
+            side = self._pre_stream
+            side.wait_stream(main)  # the previous iteration's backward has released `nxt`
+            with torch.cuda.stream(side):
+                rays(out=nxt)  # the next iteration's batch, beside this iteration's render + backward
+            ro, rd, gd, gc, keep, z = cur
         else:
-            gm = gt_max(gd) if gt_max is not None else None
-        z = ops.sample_z(ro, rd, gsamp, self.bound, self.n_strat, self.n_surf, self.lindisp, gt_max=gm)
+            ro, rd, gd, gc, keep, z = rays()
         keys, dnames = self.grads_for(stage, trainable_decoders)
         raw = self.query_fwd(stage, ro, rd, z, defer_occ=True, tape="color" in dnames)
         _, _, _, ray_loss, g_raw = ops.render_loss(raw, z, gd, gc, keep, mode="mapper", use_color=stage == "color",
@@ -294,6 +329,8 @@ class MappingEngine:
             exchange(keys, dnames)
         elif allreduce is not None:  # the grid gradients as one flat buffer, plus the decoder gradients
             allreduce([self.gbuf] + [self.decs[n].grad for n in dnames])
+        if side is not None:  # join: the next call reads the prefetched set
+            main.wait_stream(side)
         # Adam resets every gradient entry it reads.  With compact gradients for every grid of the
         # stage that is every entry the backward wrote, so the next iteration needs no memsets.
         clean = all(k in self.rows for k in keys)

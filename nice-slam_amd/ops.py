@@ -110,16 +110,22 @@ def _t_tables(device, s0, s1):
     return _T_CACHE[key]
 
 
-def sample_z(rays_o, rays_d, gt_depth, bound, n_strat, n_surf, lindisp=False, gt_max=None):
+def sample_z(rays_o, rays_d, gt_depth, bound, n_strat, n_surf, lindisp=False, gt_max=None, out=None):
     """z_vals [N, n_strat(+n_surf)] float64 (surface samples only when gt_depth is given).
 
     gt_max: optional device float scalar = max(gt_depth) over the FULL batch (ray sharding).
+    out: optional preallocated z tensor of that shape (persistent buffers of a captured loop).
     """
     ro = rays_o.detach().float().contiguous()
     rd = rays_d.detach().float().contiguous()
     n = ro.shape[0]
     s1 = n_surf if gt_depth is not None else 0
-    z = torch.empty(n, n_strat + s1, dtype=torch.float64, device=ro.device)
+    if out is not None:
+        if tuple(out.shape) != (n, n_strat + s1) or out.dtype != torch.float64 or not out.is_contiguous():
+            raise ValueError("out must be a contiguous float64 [N, S] tensor")
+        z = out
+    else:
+        z = torch.empty(n, n_strat + s1, dtype=torch.float64, device=ro.device)
     if n == 0:
         return z
     gt = gt_depth.detach().float().reshape(-1).contiguous() if gt_depth is not None else None
@@ -405,7 +411,7 @@ def grid_sample(grid, coords):
 # ----------------------------------------------------------------------------------------------
 # fused mapping / tracking iteration (ABI v4): pixel gather, render loss, ray-form query, Adam
 # ----------------------------------------------------------------------------------------------
-def gather_rays(frames, pix, n_per, H, W, window, fx, fy, cx, cy, bound=None, draw=None, n_kept=None):
+def gather_rays(frames, pix, n_per, H, W, window, fx, fy, cx, cy, bound=None, draw=None, n_kept=None, out=None):
     """get_samples (src/common.py:92-134) for every frame of a window in one launch, plus the
     inside-mask prefilter (Mapper.py:469-481) when `bound` is given.
 
@@ -414,7 +420,8 @@ def gather_rays(frames, pix, n_per, H, W, window, fx, fy, cx, cy, bound=None, dr
     (h0, h1, w0, w1).  Returns rays_o, rays_d [N,3] f32, gt_depth [N] f32 (0 for dropped rays),
     gt_color [N,3] f32, keep [N] uint8.
     pix=None: draw the pixels on the device (`draw`: PixelDraws, ABI v7); n_kept: optional device
-    int64 [1] incremented by the number of kept rays.
+    int64 [1] incremented by the number of kept rays; out: optional preallocated
+    (rays_o, rays_d, gt_depth, gt_color, keep) to write into.
     """
     nf = len(frames)
     if nf == 0 or nf > _lib.MAX_FRAMES:
@@ -435,11 +442,19 @@ def gather_rays(frames, pix, n_per, H, W, window, fx, fy, cx, cy, bound=None, dr
     if pix is not None:
         pix = pix.to(torch.int64).contiguous()
     n = nf * n_per
-    ro = torch.empty(n, 3, dtype=torch.float32, device=dev)
-    rd = torch.empty(n, 3, dtype=torch.float32, device=dev)
-    gd = torch.empty(n, dtype=torch.float32, device=dev)
-    gc = torch.empty(n, 3, dtype=torch.float32, device=dev)
-    keep = torch.empty(n, dtype=torch.uint8, device=dev)
+    if out is not None:
+        ro, rd, gd, gc, keep = out
+        want = ((n, 3, torch.float32), (n, 3, torch.float32), (n, torch.float32), (n, 3, torch.float32),
+                (n, torch.uint8))
+        for t, w in zip(out, want):
+            if tuple(t.shape) != tuple(w[:-1]) or t.dtype != w[-1] or not t.is_contiguous():
+                raise ValueError("out tensors must match gather_rays' outputs")
+    else:
+        ro = torch.empty(n, 3, dtype=torch.float32, device=dev)
+        rd = torch.empty(n, 3, dtype=torch.float32, device=dev)
+        gd = torch.empty(n, dtype=torch.float32, device=dev)
+        gc = torch.empty(n, 3, dtype=torch.float32, device=dev)
+        keep = torch.empty(n, dtype=torch.uint8, device=dev)
     h0, h1, w0, w1 = window
     if bound is not None:
         lo, hi = _bound_list(bound)

@@ -268,6 +268,35 @@ def test_engine_loss_decreases(tiny):
     assert losses[-1] < losses[0]
 
 
+def test_engine_prefetch_matches_serial(tiny):
+    """iteration(prefetch=True): the next batch's gather + sampler run on a side stream during this
+    iteration's render/backward.  The device draw stream is consumed in the same order, so after
+    the same number of iterations the map equals the serial engine's (up to float-atomic order),
+    and the kept-ray counter covers one batch ahead."""
+    sc, frames = _frames(tiny)
+    out = {}
+    for pre in (False, True):
+        nice, c = _nice(sc)
+        eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV)
+        opt = P.ops.FusedAdam([{"params": [eng.decs["color"].param], "lr": 0.005}] +
+                              [{"params": [c[k]], "lr": 0.005} for k in ("grid_middle", "grid_fine", "grid_color")])
+        kept = torch.zeros(1, dtype=torch.int64, device=DEV)
+        losses = []
+        for _ in range(4):
+            rl, _ = eng.iteration("color", frames, None, 150, (96, 128), (sc.fx, sc.fy, sc.cx, sc.cy), opt,
+                                  seed=11, n_kept=kept, prefetch=pre)
+            losses.append(rl.clone())
+        torch.cuda.synchronize()
+        out[pre] = (losses, {k: v.detach().clone() for k, v in c.items()}, eng.decs["color"].param.detach().clone(),
+                    int(kept))
+    for a, b in zip(out[False][0], out[True][0]):
+        assert rel_l2(b, a) < 1e-5
+    for k in out[False][1]:
+        assert rel_l2(out[True][1][k], out[False][1][k]) < 1e-5, k
+    assert rel_l2(out[True][2], out[False][2]) < 1e-5
+    assert out[True][3] >= out[False][3] > 0  # prefetch has drawn (and counted) one batch more
+
+
 def test_rows_pack_unpack_bitexact():
     """nslam_rows_pack / nslam_rows_unpack (the sparse gradient exchange) vs torch indexing."""
     g = torch.Generator(device=DEV).manual_seed(9)

@@ -16,20 +16,14 @@ import bench  # noqa: E402
 def graph_ms(fn, reps=100):
     for _ in range(3):
         fn()
-    side = torch.cuda.Stream()
-    side.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(side):
-        fn()
-    torch.cuda.current_stream().wait_stream(side)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        fn()
-    g.replay()
+    run, _ = bench.capture_step_graphs(fn)
+    run()
+    run()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
     for _ in range(reps):
-        g.replay()
+        run()
     b.record()
     torch.cuda.synchronize()
     return a.elapsed_time(b) / reps * 1e3
