@@ -279,6 +279,9 @@ typedef struct nslam_adam_seg {
   const int32_t* mirror_idx;
   float* mirror;
 } nslam_adam_seg;
+/* ticket: NULL = the step counts advance in a second single-wave launch; else a device uint32
+ * (zero-initialised, re-armed by the call itself) with which the update kernel's last workgroup
+ * advances them — one launch per step (ABI v9). */
 int nslam_adam_step(const nslam_adam_seg* segs, int32_t n_segs, float beta1, float beta2, float eps,
                     int32_t zero_grad, uint32_t* ticket, void* stream);
 

@@ -174,6 +174,15 @@ __device__ __forceinline__ void tstore(float* s, const f32x16& v, int lane) {
   for (int r = 0; r < 16; ++r) s[p * TPITCH + fidx(r, h)] = v[r];
 }
 
+// read a C-layout tile back from a [point][feature] LDS image (inverse of tstore)
+__device__ __forceinline__ f32x16 tload(const float* s, int lane) {
+  const int p = lane & 31, h = lane >> 5;
+  f32x16 v;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = s[p * TPITCH + fidx(r, h)];
+  return v;
+}
+
 __device__ __forceinline__ float xor32(float v) { return __shfl_xor(v, 32, 64); }
 __device__ __forceinline__ double xor32d(double v) { return __shfl_xor(v, 32, 64); }
 

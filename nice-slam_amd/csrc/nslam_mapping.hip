@@ -171,6 +171,7 @@ struct AdamArgs {
   int32_t nseg;
   float b1, b2, eps;
   int32_t zero_grad;
+  uint32_t* ticket;  // non-NULL: the last workgroup advances the step counts (no second launch)
 };
 
 constexpr int kAdamThreads = 256;
@@ -249,6 +250,20 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam(AdamArgs a) {
       *reinterpret_cast<f32x4*>(sg.exp_avg + sbase) = m;
       *reinterpret_cast<f32x4*>(sg.exp_avg_sq + sbase) = v;
       if (a.zero_grad) *reinterpret_cast<f32x4*>(sg.grad + gbase) = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  if (a.ticket) {
+    // Every workgroup read its segment's step count at its start (the value was consumed long
+    // before this point), so once all of them have drawn a ticket no read is outstanding and the
+    // last one may advance every count and re-arm the ticket for the next launch.  The next
+    // launch is a later kernel: its reads see these stores across the kernel boundary.
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t tk = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tk == gridDim.x - 1) {
+        for (int k = 0; k < a.nseg; ++k) *a.seg[k].step += 1.f;
+        __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
 }
@@ -398,12 +413,12 @@ extern "C" int nslam_adam_step(const nslam_adam_seg* segs, int32_t n_segs, float
   a.b2 = beta2;
   a.eps = eps;
   a.zero_grad = zero_grad;
-  (void)ticket;
+  a.ticket = ticket;
   if (blocks == 0) return NSLAM_EINVAL;  // every segment empty: nothing would advance the steps
   if (blocks >= (int64_t(1) << 31)) return NSLAM_EUNSUPPORTED;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(kAdamThreads), 0, s, a);
-  hipLaunchKernelGGL(k_adam_steps, dim3(1), dim3(64), 0, s, a);
+  if (!ticket) hipLaunchKernelGGL(k_adam_steps, dim3(1), dim3(64), 0, s, a);
   return hip_status();
 }
 

@@ -1370,10 +1370,13 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
 #else
   if (gr.grad) {
 #endif
-    if (WG)
+    if (WG && !SAVED) {
       scatter_grid_grad_halves(gr.grad, gr.slot, cr, dc, q.valid, S, lane);
-    else
+    } else {
+      // the tape kernel (256 VGPRs) resolves its corners here rather than across the backward
+      if (WG) scn = resolve_corners(gr.slot, cr, q.valid, lane);
       scatter_grid_grad_uniform(gr.grad, scn, cr.cell, dc, S, lane);
+    }
   }
   PHASE(DEC, 13);
   if (PG) {
@@ -1392,7 +1395,8 @@ __global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd(QueryKArgs a, flo
                                                                  int acc_floats) {
   // per-wave scratch: the scatter needs sA + corner rows/weights; weight gradients add sX and
   // the per-point tables (sizing LDS per variant keeps the lean kernels at 5+ waves/SIMD)
-  constexpr int kScr = WG ? kScratchFloats + (SAVED ? TILE_FLOATS : 0) : TILE_FLOATS + 32 * 8 * 2 + 32;
+  // (the lean kernels' register-resident scatter walk needs only the sA transpose image)
+  constexpr int kScr = WG ? kScratchFloats + (SAVED ? TILE_FLOATS : 0) : TILE_FLOATS;
   __shared__ __attribute__((aligned(16))) float lds[kWavesBwd * kScr];
   const int lane = threadIdx.x & 63, wave = wave_id();
   float* sc = lds + wave * kScr;
@@ -1404,13 +1408,13 @@ __global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd(QueryKArgs a, flo
     S.gtab = sc + 2 * TILE_FLOATS;
     S.xtab = S.gtab + 32 * 4;
     S.crow = reinterpret_cast<int*>(S.xtab + 32 * 3);
+    S.cw = reinterpret_cast<float*>(S.crow + 32 * 8);
+    S.ccell = reinterpret_cast<int*>(S.cw + 32 * 8);
+    if (SAVED) S.sD3 = reinterpret_cast<float*>(S.ccell + 32);
   } else {
-    S.sX = S.gtab = S.xtab = nullptr;
-    S.crow = reinterpret_cast<int*>(sc + TILE_FLOATS);
+    S.sX = S.gtab = S.xtab = S.cw = nullptr;
+    S.crow = S.ccell = nullptr;
   }
-  S.cw = reinterpret_cast<float*>(S.crow + 32 * 8);
-  S.ccell = reinterpret_cast<int*>(S.cw + 32 * 8);
-  if (WG && SAVED) S.sD3 = reinterpret_cast<float*>(S.ccell + 32);
   const int64_t ntiles = (a.n + 31) / 32;
   const int64_t w = (int64_t)blockIdx.x * kWavesBwd + wave;
   const Slab A = make_slab(WG ? slab + (size_t)w * acc_floats : slab, WG ? acc_floats : 0);
@@ -1528,22 +1532,24 @@ int launch_dec_bwd(const QueryKArgs& a, bool first, float* slab, hipStream_t s) 
   constexpr bool kTapeable = DEC == NSLAM_DEC_COLOR && !PG;
   const bool tape = kTapeable && a.c.act_tape && a.c.saved_masks;
   int rc;
-  if (tiles > max_slabs() && hipMemsetAsync(slab, 0, (size_t)nslab * acc * sizeof(float), s) != hipSuccess)
-    return hip_status();
   if constexpr (kTapeable) {
     if (tape) {
       if (tiles <= max_slabs())
         rc = first ? launch_one<DEC, 1, PG, true, true>(a, slab, acc, blocks, s)
                    : launch_one<DEC, 1, PG, false, true>(a, slab, acc, blocks, s);
       else
-        rc = first ? launch_one<DEC, 2, PG, true, true>(a, slab, acc, blocks, s)
-                   : launch_one<DEC, 2, PG, false, true>(a, slab, acc, blocks, s);
+        rc = (hipMemsetAsync(slab, 0, (size_t)nslab * acc * sizeof(float), s) != hipSuccess)
+                 ? hip_status()
+                 : (first ? launch_one<DEC, 2, PG, true, true>(a, slab, acc, blocks, s)
+                          : launch_one<DEC, 2, PG, false, true>(a, slab, acc, blocks, s));
       if (rc) return rc;
       hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((dg.count + 63) / 64)), dim3(64 * kReduceWaves), 0, s, slab,
                          nslab, acc, (int)dg.count, dg.base);
       return hip_status();
     }
   }
+  if (tiles > max_slabs() && hipMemsetAsync(slab, 0, (size_t)nslab * acc * sizeof(float), s) != hipSuccess)
+    return hip_status();
   if (tiles <= max_slabs()) {
     rc = first ? launch_one<DEC, 1, PG, true>(a, slab, acc, blocks, s)
                : launch_one<DEC, 1, PG, false>(a, slab, acc, blocks, s);

@@ -664,7 +664,7 @@ class FusedAdam:
         arr = (_lib.NslamAdamSeg * len(segs))(*[s for s, _, _ in segs])
         b1, b2 = self.betas
         with _span("adam"):
-            rc = lib().nslam_adam_step(arr, len(segs), b1, b2, self.eps, int(bool(zero_grad)), None,
+            rc = lib().nslam_adam_step(arr, len(segs), b1, b2, self.eps, int(bool(zero_grad)), ptr(self.ticket),
                                        stream_ptr(self.device))
         check(rc, "nslam_adam_step")
 
