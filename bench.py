@@ -103,29 +103,54 @@ def rot(yaw, pitch):
     return Rz @ Rx
 
 
-def capture_step_graphs(fn, n=2):
-    """Capture `n` consecutive calls of fn as hipGraphs, replayed in turn (a prefetching engine
-    alternates between two ray-buffer sets, so consecutive iterations are two different graphs).
-    Returns (replay callable, mode)."""
-    side = torch.cuda.Stream()
-    side.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(side):
-        for _ in range(2 * n):
-            fn()
-    torch.cuda.current_stream().wait_stream(side)
-    graphs = []
-    for _ in range(n):
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            fn()
-        graphs.append(g)
-    state = {"i": 0}
+class StepGraphs:
+    """Whole mapping iterations as hipGraphs.  `block` (even) consecutive iterations form one
+    graph, so the launch bubble between two graph replays (~20 us on MI355X: the next replay starts
+    only after the previous one has drained) is paid once per block; two single-iteration graphs
+    (one per ray-buffer parity of the prefetching engine) cover remainders.  run(k) executes exactly
+    k iterations; finish() re-aligns the engine's host-side buffer parity (sync) with the device."""
 
-    def replay():
-        graphs[state["i"]].replay()
-        state["i"] = (state["i"] + 1) % n
+    def __init__(self, fn, block=10, sync=None):
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                fn()
+        torch.cuda.current_stream().wait_stream(side)
+        self.single = []
+        for _ in range(2):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                fn()
+            self.single.append(g)
+        self.block = max(2, block - block % 2)
+        self.blockg = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.blockg):
+            for _ in range(self.block):
+                fn()
+        self.par = 0  # device-side parity relative to the capture start
+        self.sync = sync
 
-    return replay, "hipgraph"
+    def run(self, k=1):
+        while self.par == 0 and k >= self.block:
+            self.blockg.replay()
+            k -= self.block
+        for _ in range(k):
+            self.single[self.par].replay()
+            self.par ^= 1
+
+    def __call__(self):
+        self.run(1)
+
+    def finish(self):
+        if self.par and self.sync is not None:
+            self.sync()
+        self.par = 0
+
+
+def capture_step_graphs(fn, block=10, sync=None):
+    """(StepGraphs, "hipgraph") for fn = one mapping iteration."""
+    return StepGraphs(fn, block, sync), "hipgraph"
 
 
 class Room0Scene:
@@ -244,6 +269,12 @@ class Room0Scene:
             stage, self.frames, None, n, (H, W), (cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"]), self.opt,
             trainable_decoders=("color",), exchange=self.exchange if sharded else None, n_kept=self.kept,
             seed=1000, world=world, rank=self.rank if sharded else 0, prefetch=PREFETCH)
+
+    def flip_parity(self):
+        """The prefetching engine's host-side ray-buffer parity, after an odd number of replayed
+        iterations (StepGraphs.finish)."""
+        if self.path == "fused":
+            self.engine._parity ^= 1
 
     def step_autograd(self, stage="color", sharded=False):
         """The same iteration through the autograd drop-in path (dense Adam, torch glue ops).
@@ -512,16 +543,23 @@ def room0_frame_rate(scene, reps=20):
             fn()
         torch.cuda.synchronize()
         try:
-            run, mode = capture_step_graphs(fn)
+            g, mode = capture_step_graphs(fn, sync=scene.flip_parity)
+            run = g.run
         except Exception:  # pragma: no cover - eager fallback
-            run, mode = fn, "eager"
-        run()
+            g, mode = None, "eager"
+
+            def run(k):
+                for _ in range(k):
+                    fn()
+        run(10)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(reps):
-            run()
+        run(reps)
         torch.cuda.synchronize()
-        return (time.perf_counter() - t0) / reps * 1e3, mode
+        dt = (time.perf_counter() - t0) / reps * 1e3
+        if g is not None:
+            g.finish()
+        return dt, mode
 
     ms = {}
     for stage in ("middle", "fine", "color"):
@@ -629,9 +667,8 @@ def main():
     if not args.eager and not (world > 1 and args.backend == "gloo"):
         try:  # whole mapping iterations as hipGraphs (removes per-op host launch cost); two of them,
             # replayed in turn, since the prefetching engine alternates its ray buffers
-            graph, mode = capture_step_graphs(lambda: scene.step(sharded=sharded))
-            graph()
-            graph()
+            graph, mode = capture_step_graphs(lambda: scene.step(sharded=sharded), sync=scene.flip_parity)
+            graph.run(graph.block)
             torch.cuda.synchronize()
         except Exception as e:  # pragma: no cover - fall back to eager launches
             print(f"graph capture failed, eager mode: {e!r}", file=sys.stderr)
@@ -641,10 +678,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        if graph is not None:
-            graph()
-        else:
+    if graph is not None:
+        graph.run(args.steps)
+    else:
+        for _ in range(args.steps):
             scene.step(sharded=sharded)
     torch.cuda.synchronize()
     if world > 1:
@@ -653,6 +690,8 @@ def main():
     samples = int(scene.kept) * (cfg["n_strat"] + cfg["n_surf"])
     # per-kernel durations: HIP events around each C-ABI launch, on the launching stream, over
     # extra eager steps of the same kernels (events cannot bracket single kernels inside a replay)
+    if graph is not None:
+        graph.finish()
     P.ops.TIMER = P.ops.KernelTimer()
     for _ in range(max(5, args.steps // 4)):
         scene.step(sharded=sharded)

@@ -182,7 +182,8 @@ class MappingEngine:
         self.occ_add = ops.query_fwd_launch(cfg, None, n, raw, defer_occ=defer_occ)
         return raw
 
-    def query_bwd(self, stage, ro, rd, z, g_raw, grid_grads, dec_grads, concurrent=None, pts_grad=False):
+    def query_bwd(self, stage, ro, rd, z, g_raw, grid_grads, dec_grads, concurrent=None, pts_grad=False,
+                  on_branch=None):
         """Backward into the engine's gradient buffers.  The decoders write disjoint buffers, so
         each runs as its own launch; with `concurrent` the frozen decoders (mask-only backward,
         atomics-heavy) run on side streams beside the one with weight gradients (MFMA-heavy) —
@@ -190,7 +191,9 @@ class MappingEngine:
 
         pts_grad: also return d loss / d pts [N*S, 3] float64 (tracking, bundle adjustment): every
         decoder writes its share into its own buffer (so the branches stay independent) and the
-        shares are summed afterwards."""
+        shares are summed afterwards.
+        on_branch(name): called on each decoder's stream right after its backward (the per-branch
+        Adam of the mapping iteration: its grid's rows depend on that branch alone)."""
         n = z.numel()
         self._clean = False
         concurrent = self.concurrent if concurrent is None else concurrent
@@ -225,7 +228,9 @@ class MappingEngine:
                         rc = lib().nslam_query_bwd_decoder(ctypes.byref(cfg), d, 0, None, n, ptr(g_raw),
                                                            ptr(gp[i]) if pts_grad else None, ptr(ws), wsb,
                                                            st.cuda_stream)
-                check(rc, "nslam_query_bwd_decoder")
+                    check(rc, "nslam_query_bwd_decoder")
+                    if on_branch is not None:
+                        on_branch(name)
                 if pts_grad and st is not main:
                     gp[i].record_stream(st)
             for st in used:
@@ -323,14 +328,6 @@ class MappingEngine:
                                                    w_color=self.w_color, occ_add=self.occ_add)
         if not self._clean:
             self.gall.zero_()  # grid and decoder gradients: one memset
-        self.query_bwd(stage, ro, rd, z, g_raw, keys, dnames)
-        grads = self.adam_grads(stage, trainable_decoders)
-        if exchange is not None:  # frustum-compacted all-reduce (distributed.SparseGradExchange)
-            exchange(keys, dnames)
-        elif allreduce is not None:  # the grid gradients as one flat buffer, plus the decoder gradients
-            allreduce([self.gbuf] + [self.decs[n].grad for n in dnames])
-        if side is not None:  # join: the next call reads the prefetched set
-            main.wait_stream(side)
         # Adam resets every gradient entry it reads.  With compact gradients for every grid of the
         # stage that is every entry the backward wrote, so the next iteration needs no memsets.
         clean = all(k in self.rows for k in keys)
@@ -340,7 +337,27 @@ class MappingEngine:
                 d = self.decs[n]
                 if d.param not in optimizer.mirrors:
                     optimizer.set_mirror(d.param, d.mirror_idx, d.packed)
-        optimizer.step(grads=grads, zero_grad=clean)
+        grads = self.adam_grads(stage, trainable_decoders)
+        on_branch = None
+        if exchange is None and allreduce is None and mirror:
+            # one rank: each decoder branch updates its own grid's rows (+ the trainable decoder's
+            # parameters, after its slab reduction) on its own stream — the update of a grid needs
+            # that branch's gradients alone, so no branch waits for the others before its Adam
+            def on_branch(name):
+                sub = {self.c[_GRID_OF[name]]: grads[self.c[_GRID_OF[name]]]} if _GRID_OF[name] in keys else {}
+                if name in dnames:
+                    sub[self.decs[name].param] = grads[self.decs[name].param]
+                if sub:
+                    optimizer.step(grads=sub, zero_grad=clean)
+        self.query_bwd(stage, ro, rd, z, g_raw, keys, dnames, on_branch=on_branch)
+        if exchange is not None:  # frustum-compacted all-reduce (distributed.SparseGradExchange)
+            exchange(keys, dnames)
+        elif allreduce is not None:  # the grid gradients as one flat buffer, plus the decoder gradients
+            allreduce([self.gbuf] + [self.decs[n].grad for n in dnames])
+        if side is not None:  # join: the next call reads the prefetched set
+            main.wait_stream(side)
+        if on_branch is None:
+            optimizer.step(grads=grads, zero_grad=clean)
         self._clean = clean
         if not mirror:
             for n in dnames:

@@ -598,6 +598,7 @@ class FusedAdam:
                 dev = p.device
         self.device = dev
         self.ticket = torch.zeros(1, dtype=torch.int32, device=dev) if dev is not None else None
+        self._tickets = {}  # one step ticket per parameter subset (subsets may step concurrently)
         self.mirrors = {}
 
     def set_mirror(self, p, idx, dst):
@@ -663,8 +664,12 @@ class FusedAdam:
             raise ValueError(f"at most {_lib.ADAM_MAX_SEGS} parameter tensors per step (flatten the decoders)")
         arr = (_lib.NslamAdamSeg * len(segs))(*[s for s, _, _ in segs])
         b1, b2 = self.betas
+        key = tuple(id(p) for _, p, _ in segs)
+        ticket = self._tickets.get(key)
+        if ticket is None:  # first step of this subset (eager, before any graph capture)
+            ticket = self._tickets[key] = torch.zeros(1, dtype=torch.int32, device=self.device)
         with _span("adam"):
-            rc = lib().nslam_adam_step(arr, len(segs), b1, b2, self.eps, int(bool(zero_grad)), ptr(self.ticket),
+            rc = lib().nslam_adam_step(arr, len(segs), b1, b2, self.eps, int(bool(zero_grad)), ptr(ticket),
                                        stream_ptr(self.device))
         check(rc, "nslam_adam_step")
 

@@ -13,19 +13,21 @@ sys.path.insert(0, REPO)
 import bench  # noqa: E402
 
 
+SCENE = None
+
+
 def graph_ms(fn, reps=100):
     for _ in range(3):
         fn()
-    run, _ = bench.capture_step_graphs(fn)
-    run()
-    run()
+    g, _ = bench.capture_step_graphs(fn, sync=SCENE.flip_parity)
+    g.run(g.block)
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
-    for _ in range(reps):
-        run()
+    g.run(reps)
     b.record()
     torch.cuda.synchronize()
+    g.finish()
     return a.elapsed_time(b) / reps * 1e3
 
 
@@ -33,6 +35,8 @@ def main():
     dev = torch.device("cuda:0")
     P = bench.pkg()
     sc = bench.Room0Scene(dev, 0, path="fused")
+    global SCENE
+    SCENE = sc
     eng = sc.engine
     variants = [("sequential", False, False), ("concurrent", True, False), ("concurrent+priority", True, True)]
     for rnd in range(2):
