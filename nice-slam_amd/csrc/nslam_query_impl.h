@@ -1418,8 +1418,24 @@ __global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd(QueryKArgs a, flo
   const int64_t ntiles = (a.n + 31) / 32;
   const int64_t w = (int64_t)blockIdx.x * kWavesBwd + wave;
   const Slab A = make_slab(WG ? slab + (size_t)w * acc_floats : slab, WG ? acc_floats : 0);
-  if (WG != 2) {  // one tile per wave (grid covers all tiles)
+  if (WG == 0) {  // one tile per wave (grid covers all tiles)
     if (w < ntiles) dec_bwd_tile<DEC, WG, PG, FIRST, SAVED>(a, w, A, S, lane);
+    return;
+  }
+  if (WG == 1) {  // one tile per wave, then the workgroup folds its waves' slabs into its first one
+    if (w < ntiles) dec_bwd_tile<DEC, WG, PG, FIRST, SAVED>(a, w, A, S, lane);
+    // the slabs were just written by this CU (L2-resident): summing them here in wave order (a
+    // fixed order: deterministic) leaves k_slab_reduce a quarter of the bytes to read
+    __syncthreads();
+    const int64_t w0 = (int64_t)blockIdx.x * kWavesBwd;
+    const int nv = (int)(ntiles - w0 < kWavesBwd ? ntiles - w0 : kWavesBwd);
+    f32x4* s0 = reinterpret_cast<f32x4*>(slab + (size_t)w0 * acc_floats);
+    const int q = acc_floats / 4;
+    for (int i = threadIdx.x; i < q; i += blockDim.x) {
+      f32x4 t = s0[i];
+      for (int v = 1; v < nv; ++v) t += s0[(size_t)v * q + i];
+      s0[i] = t;
+    }
     return;
   }
 #pragma nounroll
@@ -1513,6 +1529,16 @@ int launch_one(const QueryKArgs& a, float* slab, int acc, int64_t blocks, hipStr
   return hip_status();
 }
 
+// WG == 1 launches leave one folded slab per workgroup (stride kWavesBwd slabs); WG == 2 one per wave
+inline int slab_reduce(const nslam_dec_grad& dg, float* slab, bool folded, int64_t nslab, int64_t blocks, int acc,
+                       hipStream_t s) {
+  const int64_t n = folded ? blocks : nslab;
+  const int stride = folded ? acc * kWavesBwd : acc;
+  hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((dg.count + 63) / 64)), dim3(64 * kReduceWaves), 0, s, slab, n,
+                     stride, (int)dg.count, dg.base);
+  return hip_status();
+}
+
 template <int DEC, int WG, bool PG>
 int launch_dec_bwd(const QueryKArgs& a, bool first, float* slab, hipStream_t s) {
   const int64_t tiles = (a.n + 31) / 32;
@@ -1543,9 +1569,7 @@ int launch_dec_bwd(const QueryKArgs& a, bool first, float* slab, hipStream_t s) 
                  : (first ? launch_one<DEC, 2, PG, true, true>(a, slab, acc, blocks, s)
                           : launch_one<DEC, 2, PG, false, true>(a, slab, acc, blocks, s));
       if (rc) return rc;
-      hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((dg.count + 63) / 64)), dim3(64 * kReduceWaves), 0, s, slab,
-                         nslab, acc, (int)dg.count, dg.base);
-      return hip_status();
+      return slab_reduce(dg, slab, tiles <= max_slabs(), nslab, blocks, acc, s);
     }
   }
   if (tiles > max_slabs() && hipMemsetAsync(slab, 0, (size_t)nslab * acc * sizeof(float), s) != hipSuccess)
@@ -1558,9 +1582,7 @@ int launch_dec_bwd(const QueryKArgs& a, bool first, float* slab, hipStream_t s) 
                : launch_one<DEC, 2, PG, false>(a, slab, acc, blocks, s);
   }
   if (rc) return rc;
-  hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((dg.count + 63) / 64)), dim3(64 * kReduceWaves), 0, s, slab,
-                     nslab, acc, (int)dg.count, dg.base);
-  return hip_status();
+  return slab_reduce(dg, slab, tiles <= max_slabs(), nslab, blocks, acc, s);
 }
 
 template <int DEC>
