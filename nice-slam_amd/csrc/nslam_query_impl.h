@@ -251,8 +251,10 @@ __device__ __forceinline__ void wg_end(const Slab& A, int base, const Scratch& S
 // ------------------------------------------------------------------------------------------
 template <int NC>
 __device__ __forceinline__ f32x16 fc_branch(const float* __restrict__ pk, const XyzPack& L, int i,
-                                            const f32x16 (&cin)[NC], int lane) {
-  f32x16 z = vec_tile(pk + L.BiasC(i), lane);
+                                            const f32x16 (&cin)[NC], int lane, const float* vec = nullptr) {
+  // vec: the decoder's vector section (biases, output row, Fourier B) — an LDS copy in the
+  // decoder-parallel forward, else pk + L.V()
+  f32x16 z = vec_tile((vec ? vec : pk + L.V()) + (L.BiasC(i) - L.V()), lane);
 #pragma unroll
   for (int c = 0; c < NC; ++c) gemm_acc(z, pk + L.FC(i, c) * NSLAM_FRAG, cin[c], lane);
   return z;
@@ -261,46 +263,47 @@ __device__ __forceinline__ f32x16 fc_branch(const float* __restrict__ pk, const 
 template <int NC, bool KEEP, bool PHF = false, bool TAPE = false>
 __device__ __forceinline__ f32x16 xyz_forward(const float* __restrict__ pk, const f32x16 (&cin)[NC],
                                               const float x[3], int lane, uint32_t m[5], f32x16* hs,
-                                              float* __restrict__ tape = nullptr) {
+                                              float* __restrict__ tape = nullptr, const float* vec = nullptr) {
   const XyzPack L{NC};
+  const float* vs = vec ? vec : pk + L.V();  // vector section (LDS copy or global)
 #define PHF_(k) \
   if (PHF) PHASE(0, k)
-  f32x16 a = vec_tile(pk + L.Bias(0), lane);
-  f32x16 a3 = vec_tile(pk + L.Bias(3), lane);
+  f32x16 a = vec_tile(vs + (L.Bias(0) - L.V()), lane);
+  f32x16 a3 = vec_tile(vs + (L.Bias(3) - L.V()), lane);
 #pragma unroll
   for (int b = 0; b < 3; ++b) {
-    const f32x16 e = emb_tile<false>(pk + L.FB(), x, b, lane);
+    const f32x16 e = emb_tile<false>(vs + (L.FB() - L.V()), x, b, lane);
     gemm_acc(a, pk + (L.L0() + b) * NSLAM_FRAG, e, lane);
     gemm_acc(a3, pk + (L.L3() + b) * NSLAM_FRAG, e, lane);
   }
   PHF_(5);
   m[0] = mask16(a);
-  f32x16 h = relu16(a) + fc_branch<NC>(pk, L, 0, cin, lane);
+  f32x16 h = relu16(a) + fc_branch<NC>(pk, L, 0, cin, lane, vs);
   if (KEEP) hs[0] = h;
   if (TAPE) tape_store(tape, 0, h, lane);
-  a = vec_tile(pk + L.Bias(1), lane);
+  a = vec_tile(vs + (L.Bias(1) - L.V()), lane);
   gemm_acc(a, pk + L.L1() * NSLAM_FRAG, h, lane);
   m[1] = mask16(a);
-  h = relu16(a) + fc_branch<NC>(pk, L, 1, cin, lane);
+  h = relu16(a) + fc_branch<NC>(pk, L, 1, cin, lane, vs);
   if (KEEP) hs[1] = h;
   if (TAPE) tape_store(tape, 1, h, lane);
   PHF_(6);
-  a = vec_tile(pk + L.Bias(2), lane);
+  a = vec_tile(vs + (L.Bias(2) - L.V()), lane);
   gemm_acc(a, pk + L.L2() * NSLAM_FRAG, h, lane);
   m[2] = mask16(a);
-  h = relu16(a) + fc_branch<NC>(pk, L, 2, cin, lane);
+  h = relu16(a) + fc_branch<NC>(pk, L, 2, cin, lane, vs);
   if (KEEP) hs[2] = h;
   if (TAPE) tape_store(tape, 2, h, lane);
   gemm_acc(a3, pk + (L.L3() + 3) * NSLAM_FRAG, h, lane);
   m[3] = mask16(a3);
-  h = relu16(a3) + fc_branch<NC>(pk, L, 3, cin, lane);
+  h = relu16(a3) + fc_branch<NC>(pk, L, 3, cin, lane, vs);
   if (KEEP) hs[3] = h;
   if (TAPE) tape_store(tape, 3, h, lane);
   PHF_(7);
-  a = vec_tile(pk + L.Bias(4), lane);
+  a = vec_tile(vs + (L.Bias(4) - L.V()), lane);
   gemm_acc(a, pk + L.L4() * NSLAM_FRAG, h, lane);
   m[4] = mask16(a);
-  h = relu16(a) + fc_branch<NC>(pk, L, 4, cin, lane);
+  h = relu16(a) + fc_branch<NC>(pk, L, 4, cin, lane, vs);
   if (TAPE) tape_store(tape, 4, h, lane);
   PHF_(8);
   return h;
@@ -1162,7 +1165,7 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd(QueryKArgs a) {
 // reference's operand order) — exactly 100 outside the bound (0 + 100; Renderer.py:57).
 // One decoder of the decoder-parallel forward for this wave's tile.
 __device__ __forceinline__ void fwd_part_middle(const QueryKArgs& a, const Pt& q, int64_t tile, int64_t idx, int lane,
-                                                float* __restrict__ occ_mid) {
+                                                float* __restrict__ occ_mid, const float* vec) {
   const int h = lane >> 5;
   uint32_t m[5];
   Corners cr;
@@ -1173,15 +1176,16 @@ __device__ __forceinline__ void fwd_part_middle(const QueryKArgs& a, const Pt& q
   const float* pk = a.c.packed[NSLAM_DEC_MIDDLE];
   const XyzPack L{1};
   const f32x16 cms[1] = {cm};
-  const f32x16 h4 = xyz_forward<1, false, true>(pk, cms, q.x, lane, m, nullptr);
+  const f32x16 h4 = xyz_forward<1, false, true>(pk, cms, q.x, lane, m, nullptr, nullptr, vec);
   save_masks(a, NSLAM_DEC_MIDDLE, tile, m, lane);
-  float o = out_row(pk + L.Wo(), pk + L.Bo(), 0, h4, lane);
+  float o = out_row(vec + (L.Wo() - L.V()), vec + (L.Bo() - L.V()), 0, h4, lane);
   if (!q.inside) o = 100.f;
   if (h == 0 && q.valid) occ_mid[idx] = o;
 }
 
 template <int STAGE>
-__device__ __forceinline__ void fwd_part_fine(const QueryKArgs& a, const Pt& q, int64_t tile, int64_t idx, int lane) {
+__device__ __forceinline__ void fwd_part_fine(const QueryKArgs& a, const Pt& q, int64_t tile, int64_t idx, int lane,
+                                              const float* vec) {
   // the fine decoder also reads the middle feature (decoder.py:184-187)
   const int h = lane >> 5;
   uint32_t m[5];
@@ -1194,9 +1198,9 @@ __device__ __forceinline__ void fwd_part_fine(const QueryKArgs& a, const Pt& q, 
   PHASE(0, 3);
   const float* pk = a.c.packed[NSLAM_DEC_FINE];
   const XyzPack L{2};
-  const f32x16 h4 = xyz_forward<2, false, true>(pk, cf, q.x, lane, m, nullptr);
+  const f32x16 h4 = xyz_forward<2, false, true>(pk, cf, q.x, lane, m, nullptr, nullptr, vec);
   save_masks(a, NSLAM_DEC_FINE, tile, m, lane);
-  float o = out_row(pk + L.Wo(), pk + L.Bo(), 0, h4, lane);
+  float o = out_row(vec + (L.Wo() - L.V()), vec + (L.Bo() - L.V()), 0, h4, lane);
   if (!q.inside) o = 0.f;
   if (h == 0 && q.valid) {
     if (STAGE == NSLAM_STAGE_COLOR) {
@@ -1209,7 +1213,8 @@ __device__ __forceinline__ void fwd_part_fine(const QueryKArgs& a, const Pt& q, 
 }
 
 template <bool TAPE>
-__device__ __forceinline__ void fwd_part_color(const QueryKArgs& a, const Pt& q, int64_t tile, int64_t idx, int lane) {
+__device__ __forceinline__ void fwd_part_color(const QueryKArgs& a, const Pt& q, int64_t tile, int64_t idx, int lane,
+                                               const float* vec) {
   const int h = lane >> 5;
   uint32_t m[5];
   Corners cr;
@@ -1220,11 +1225,11 @@ __device__ __forceinline__ void fwd_part_color(const QueryKArgs& a, const Pt& q,
   const float* pk = a.c.packed[NSLAM_DEC_COLOR];
   const XyzPack L{1};
   float* tp = TAPE ? a.c.act_tape + tile * kTapeFloats : nullptr;
-  const f32x16 h4 = xyz_forward<1, false, true, TAPE>(pk, cc, q.x, lane, m, nullptr, tp);
+  const f32x16 h4 = xyz_forward<1, false, true, TAPE>(pk, cc, q.x, lane, m, nullptr, tp, vec);
   save_masks(a, NSLAM_DEC_COLOR, tile, m, lane);
   float o[3];
 #pragma unroll
-  for (int j = 0; j < 3; ++j) o[j] = out_row(pk + L.Wo(), pk + L.Bo(), j, h4, lane);
+  for (int j = 0; j < 3; ++j) o[j] = out_row(vec + (L.Wo() - L.V()), vec + (L.Bo() - L.V()), j, h4, lane);
   if (h == 0 && q.valid) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) a.raw[idx * 4 + j] = o[j];
@@ -1243,10 +1248,30 @@ __device__ __forceinline__ void fwd_part_color(const QueryKArgs& a, const Pt& q,
 // and k_occ_combine (or the loss kernel, defer_occ) then forms raw[p][3] = fine_occ + middle_occ
 // (decoder.py:331-334, the reference's operand order) — exactly 100 outside the bound (0 + 100;
 // Renderer.py:57).
+#ifndef NSLAM_FWD_LB
+#define NSLAM_FWD_LB 2  // min waves per SIMD (experiments: 3..5 trade VGPRs for occupancy)
+#endif
+constexpr int kVecFloats = 744;  // XyzPack vector section (740) rounded to float4s
 template <int STAGE, int NPARTS, bool TAPE>
-__global__ __launch_bounds__(256, 2) void k_query_fwd_parts(QueryKArgs a, float* __restrict__ occ_mid) {
+__global__ __launch_bounds__(256, NSLAM_FWD_LB) void k_query_fwd_parts(QueryKArgs a, float* __restrict__ occ_mid) {
   const int part = (int)(blockIdx.x % NPARTS);
   const int lane = threadIdx.x & 63;
+  // The part's decoder vector sections (biases, output rows, Fourier B: ~3 KiB each) are read by
+  // every layer of every wave: an LDS copy per workgroup turns ~90 global loads per wave into
+  // ds_reads.  Part 0 of the 2-part colour forward evaluates middle then colour: two copies.
+  __shared__ __attribute__((aligned(16))) float vsec[2][kVecFloats];
+  {
+    const int d0 = part == 0 ? NSLAM_DEC_MIDDLE : part == 1 ? NSLAM_DEC_FINE : NSLAM_DEC_COLOR;
+    const int nc0 = d0 == NSLAM_DEC_FINE ? 2 : 1;
+    const float* src0 = a.c.packed[d0] + XyzPack{nc0}.V();
+    const bool two = NPARTS == 2 && STAGE == NSLAM_STAGE_COLOR && part == 0;
+    const float* src1 = two ? a.c.packed[NSLAM_DEC_COLOR] + XyzPack{1}.V() : nullptr;
+    for (int i = threadIdx.x; i < 740; i += 256) {
+      vsec[0][i] = src0[i];
+      if (two) vsec[1][i] = src1[i];
+    }
+    __syncthreads();
+  }
   const int64_t tile = (int64_t)(blockIdx.x / NPARTS) * 4 + wave_id();
   if (tile * 32 >= a.n) return;  // wave-uniform
   const int64_t idx = tile * 32 + (lane & 31);
@@ -1255,17 +1280,17 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd_parts(QueryKArgs a, float*
   PHASE(0, 1);
   if (NPARTS == 2 && STAGE == NSLAM_STAGE_COLOR) {
     if (part == 0) {
-      fwd_part_middle(a, q, tile, idx, lane, occ_mid);
-      fwd_part_color<TAPE>(a, q, tile, idx, lane);
+      fwd_part_middle(a, q, tile, idx, lane, occ_mid, vsec[0]);
+      fwd_part_color<TAPE>(a, q, tile, idx, lane, vsec[1]);
     } else {
-      fwd_part_fine<STAGE>(a, q, tile, idx, lane);
+      fwd_part_fine<STAGE>(a, q, tile, idx, lane, vsec[0]);
     }
   } else if (part == 0) {
-    fwd_part_middle(a, q, tile, idx, lane, occ_mid);
+    fwd_part_middle(a, q, tile, idx, lane, occ_mid, vsec[0]);
   } else if (part == 1) {
-    fwd_part_fine<STAGE>(a, q, tile, idx, lane);
+    fwd_part_fine<STAGE>(a, q, tile, idx, lane, vsec[0]);
   } else if (STAGE == NSLAM_STAGE_COLOR) {
-    fwd_part_color<TAPE>(a, q, tile, idx, lane);
+    fwd_part_color<TAPE>(a, q, tile, idx, lane, vsec[0]);
   }
   PHASE(0, 9);
 }

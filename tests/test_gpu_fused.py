@@ -297,6 +297,30 @@ def test_engine_prefetch_matches_serial(tiny):
     assert out[True][3] >= out[False][3] > 0  # prefetch has drawn (and counted) one batch more
 
 
+def test_engine_per_branch_adam_matches_single_adam(tiny):
+    """One rank: each decoder branch updates its own grid's rows (and the colour decoder) on its
+    own stream right after its backward.  The same iterations with ONE Adam call after all the
+    branches (the path an all-reduce hook takes) must give the same map."""
+    sc, frames = _frames(tiny)
+    out = {}
+    for single in (False, True):
+        nice, c = _nice(sc)
+        eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV)
+        opt = P.ops.FusedAdam([{"params": [eng.decs["color"].param], "lr": 0.005}] +
+                              [{"params": [c[k]], "lr": 0.005} for k in ("grid_middle", "grid_fine", "grid_color")])
+        pix = torch.randint(96 * 128, (3 * 150,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(12))
+        for _ in range(3):
+            eng.iteration("color", frames, pix, 150, (96, 128), (sc.fx, sc.fy, sc.cx, sc.cy), opt,
+                          allreduce=(lambda grads: None) if single else None)
+        torch.cuda.synchronize()
+        out[single] = ({k: v.detach().clone() for k, v in c.items()}, eng.decs["color"].param.detach().clone(),
+                       {id(p): float(st["step"]) for p, st in opt.state.items()})
+    for k in out[False][0]:
+        assert rel_l2(out[True][0][k], out[False][0][k]) < 1e-5, k
+    assert rel_l2(out[True][1], out[False][1]) < 1e-5
+    assert sorted(out[True][2].values()) == sorted(out[False][2].values()) == [3.0] * 4
+
+
 def test_rows_pack_unpack_bitexact():
     """nslam_rows_pack / nslam_rows_unpack (the sparse gradient exchange) vs torch indexing."""
     g = torch.Generator(device=DEV).manual_seed(9)

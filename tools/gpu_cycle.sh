@@ -12,7 +12,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 stop() { echo "STOP $1 rc=$2"; exit $2; }
 summ() { python -c "
-import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], round(d['value']/1e6,2), 'M/s', round(d['ms_per_step'],4), 'ms', d.get('kernels_ms'))
+import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[2], round(d['value']/1e6,2), 'M/s', round(d['ms_per_step'],4), 'ms', d.get('kernels_ms'))
 r=d.get('room0'); print('  room0', r) if r else None" "$1" "$2"; }
 for s in $STEPS; do
   case $s in
