@@ -61,7 +61,7 @@ SPAN_KERNELS = {
     "query_bwd.fine": ("k_dec_bwd<2,",),
     "query_bwd.middle": ("k_dec_bwd<1,",),
 }
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r01_traffic.json")
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r02_traffic.json")
 
 
 def pmc_traffic(span):
@@ -521,10 +521,10 @@ def kernel_roofline(name, avg_ms, pts):
             "frac": achieved / peak, "traffic": pmc_traffic(name), "avg_launch_ms": avg_ms,
             "ray_samples_per_launch": pts, "flop_per_sample": fl, "bytes_per_sample": by,
             # the HIP-event span brackets these rocprofv3 kernels back to back: compare its average
-            # with the SUM of their average durations in profiles/r01_room0_kernels_*.md
+            # with the SUM of their average durations in profiles/r02_room0_kernels.md
             "rocprof_kernels": list(SPAN_KERNELS.get(name, ())),
             "traffic_note": "HBM bytes per launch: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, "
-                            "profiles/r01_traffic.json"}
+                            "profiles/r02_traffic.json"}
 
 
 def room0_frame_rate(scene, reps=20):

@@ -735,6 +735,7 @@ __device__ __forceinline__ void color_backward_tape(const float* __restrict__ pk
     if (lane == 0) put<1>(A, 0, dg.bo + 3, 0.f);
   }
   lds_sync();
+  PHASE(3, 5);
   dc = zero16();
   // layer 4 (input h3)
   fc_bwd<1, WG>(pk, L, 4, c1, dh, dg, A, S, lane, dc);
@@ -744,6 +745,7 @@ __device__ __forceinline__ void color_backward_tape(const float* __restrict__ pk
   wg_end<WG>(A, dg.b[4], S, lane);
   dh = zero16();
   gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
+  PHASE(3, 6);
   // layer 3 (input [emb | h2]): the h2 columns now, the embedding columns at the end
   fc_bwd<1, WG>(pk, L, 3, c1, dh, dg, A, S, lane, dc);
   const f32x16 da3 = apply_mask(dh, m[3]);
@@ -755,6 +757,7 @@ __device__ __forceinline__ void color_backward_tape(const float* __restrict__ pk
   lds_sync();
   dh = zero16();
   gemm_acc(dh, pk + (L.L3T() + 3) * NSLAM_FRAG, da3, lane);
+  PHASE(3, 7);
   // layer 2 (input h1)
   fc_bwd<1, WG>(pk, L, 2, c1, dh, dg, A, S, lane, dc);
   da = apply_mask(dh, m[2]);
@@ -763,6 +766,7 @@ __device__ __forceinline__ void color_backward_tape(const float* __restrict__ pk
   wg_end<WG>(A, dg.b[2], S, lane);
   dh = zero16();
   gemm_acc(dh, pk + L.L2T() * NSLAM_FRAG, da, lane);
+  PHASE(3, 8);
   // layer 1 (input h0)
   fc_bwd<1, WG>(pk, L, 1, c1, dh, dg, A, S, lane, dc);
   da = apply_mask(dh, m[1]);
@@ -771,11 +775,13 @@ __device__ __forceinline__ void color_backward_tape(const float* __restrict__ pk
   wg_end<WG>(A, dg.b[1], S, lane);
   dh = zero16();
   gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
+  PHASE(3, 9);
   // layer 0 (input emb): its cotangent stays in sA for the embedding blocks
   fc_bwd<1, WG>(pk, L, 0, c1, dh, dg, A, S, lane, dc);
   da = apply_mask(dh, m[0]);
   wg_begin(da, S, lane);
   wg_end<WG>(A, dg.b[0], S, lane);
+  PHASE(3, 10);
   // embedding blocks: sin_b -> dW3 / dW0 columns; cos_b -> G_b = (L3T_b da3 + L0T_b da0) cos_b -> dB
   const float* FB = pk + L.FB();
 #pragma nounroll
