@@ -20,6 +20,7 @@
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 #define NSLAM_FRAG 1024  // floats per packed fragment block (16 steps x 64 lanes)
 #define TPITCH 33        // LDS row pitch of a transposed tile [32 points][33]
@@ -183,8 +184,20 @@ __device__ __forceinline__ f32x16 tload(const float* s, int lane) {
   return v;
 }
 
-__device__ __forceinline__ float xor32(float v) { return __shfl_xor(v, 32, 64); }
-__device__ __forceinline__ double xor32d(double v) { return __shfl_xor(v, 32, 64); }
+// value of lane l ^ 32: one v_permlane32_swap (gfx950; swaps the upper half of its first operand
+// with the lower half of its second) and a half select, instead of an LDS ds_bpermute round trip
+__device__ __forceinline__ unsigned xor32u(unsigned v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return (threadIdx.x & 32) ? r[0] : r[1];
+}
+__device__ __forceinline__ float xor32(float v) {
+  return __builtin_bit_cast(float, xor32u(__builtin_bit_cast(unsigned, v)));
+}
+__device__ __forceinline__ double xor32d(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = xor32u((unsigned)u), hi = xor32u((unsigned)(u >> 32));
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
 
 // ------------------------------------------------------------------------------------------
 // trilinear corners (F.grid_sample 5-D, bilinear, padding 'border', align_corners=True)

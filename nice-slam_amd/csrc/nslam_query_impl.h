@@ -939,25 +939,50 @@ __device__ __forceinline__ ScatterCorners resolve_corners(const int32_t* __restr
   return sc;
 }
 
+// The walk keeps each corner voxel of the current cell in a register chosen by the voxel's own
+// coordinate parities, not by its position in the cell: lane half h holds the corners with
+// x & 1 == h, register j those with (y & 1) + 2 (z & 1) == j.  Stepping to a neighbouring cell then
+// leaves every shared voxel where it is (its running sum simply continues), and only the voxels
+// that leave the cell are flushed and their registers cleared — no data moves between registers.
+// Walk table of one tile (per wave, kWalkFloats): entry (p, h) holds point p's weights (then its
+// frustum rows) of the four corners in lane half h, register order j, so one ds_read_b128 with a
+// half-uniform address (an LDS broadcast) fetches them.
+constexpr int kWalkFloats = 2 * 32 * 8;
+__device__ __forceinline__ void stage_walk_table(float* __restrict__ tab, const ScatterCorners& sc, int cellk,
+                                                 int lane) {
+  // lane (hz, p) resolved corners 4 hz + i, i = dx + 2 dy, of the cell with lower corner cellk
+  const int hz = lane >> 5, p = lane & 31;
+  const int px = cellk & 1, py = (cellk >> 10) & 1, pz = (cellk >> 20) & 1;
+  float* w = tab + p * 8;
+  int* r = reinterpret_cast<int*>(tab + 256) + p * 8;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e = (((i & 1) ^ px) << 2) | ((i >> 1) ^ py) | ((hz ^ pz) << 1);
+    w[e] = sc.wk[i];
+    r[e] = sc.rk[i];
+  }
+}
+
 __device__ __forceinline__ void scatter_grid_grad_uniform(float* __restrict__ grad, const ScatterCorners& sc,
-                                                          int cellk, const f32x16& dc, const Scratch& S, int lane) {
-  // Points of a tile are consecutive samples of (mostly) one ray: runs of samples in the same cell
-  // are summed in registers and flushed once (and corners shared with the next cell carried).  The whole wave walks the tile's 32 points in step
-  // (fully unrolled, uniform control flow); lane (h, ch) owns channel ch of corners 2j + h,
-  // j = 0..3 — corners 2j and 2j+1 differ only in x, i.e. are adjacent rows of the channels-last
-  // grid, so every flush wave-instruction adds one contiguous 256-B segment (the full-rate shape
-  // of a float atomic).  The walk reads no LDS per point: the cell, corner weights and corner rows
-  // of point t are broadcast with v_readlane from the two lanes that own it (lane (h, t) resolves
-  // corners 4h..4h+3, including the frustum slot lookup), and the cotangent column of channel ch
-  // comes through one LDS transpose.
+                                                          int cellk, const f32x16& dc, float* __restrict__ img,
+                                                          float* __restrict__ tab, int lane) {
+  // Points of a tile are consecutive samples of (mostly) one ray: a voxel's contributions from a
+  // run of cells touching it are summed in one register and flushed once (one atomic per voxel per
+  // run).  The whole wave walks the tile's 32 points in step (fully unrolled, uniform control
+  // flow); lane (h, ch) owns channel ch of its half's four corners, and the two halves hold x-
+  // neighbours, i.e. adjacent rows of the channels-last grid, so every flush wave-instruction adds
+  // one contiguous 256-B segment (the full-rate shape of a float atomic).  Per point: the cell by
+  // v_readlane (it steers the uniform branch), weights and rows by broadcast LDS reads of the walk
+  // table, and the cotangent column of channel ch from one LDS transpose of dc.
   const int h = lane >> 5, ch = lane & 31;
-  const int* rk = sc.rk;
-  const float* wk = sc.wk;
-  tstore(S.sA, dc, lane);
+  tstore(img, dc, lane);
+  stage_walk_table(tab, sc, cellk, lane);
   lds_sync();
   float vcol[32];
 #pragma unroll
-  for (int t = 0; t < 32; ++t) vcol[t] = S.sA[t * TPITCH + ch];
+  for (int t = 0; t < 32; ++t) vcol[t] = img[t * TPITCH + ch];
+  const f32x4* wt = reinterpret_cast<const f32x4*>(tab) + h;        // (t, h) at wt[2 t]
+  const i32x4* rt = reinterpret_cast<const i32x4*>(tab + 256) + h;  // (t, h) at rt[2 t]
   float acc[4], wsum[4];
   int rows[4];
 #pragma unroll
@@ -970,59 +995,38 @@ __device__ __forceinline__ void scatter_grid_grad_uniform(float* __restrict__ gr
 #pragma unroll
   for (int t = 0; t < 32; ++t) {
     const int cell = __builtin_amdgcn_readlane(cellk, t);
+    const f32x4 w = wt[2 * t];
+    const i32x4 nr = rt[2 * t];
     if (cell != cur) {  // wave-uniform
-      // Carry-over: when the walk steps to a neighbouring cell (|delta| <= 1 per axis) the corners
-      // the two cells share keep accumulating (a register move, or a swap of lane halves for an x
-      // step) instead of being flushed — one atomic per voxel per run of cells touching it.
-      int ax = 2, ay = 2, az = 2;
+      // a voxel of the old cell at offset d (0/1) along an axis stays in the new cell iff the step
+      // a along that axis is 0, or +1 with d == 1, or -1 with d == 0; d = register parity ^ cell parity
+      int ax = 2, ay = 2, az = 2, px = 0, py = 0, pz = 0;
       if (cur >= 0) {
         ax = (cell & 1023) - (cur & 1023);
         ay = ((cell >> 10) & 1023) - ((cur >> 10) & 1023);
         az = (cell >> 20) - (cur >> 20);
+        px = cur & 1;
+        py = (cur >> 10) & 1;
+        pz = (cur >> 20) & 1;
       }
-      const bool adj = ax >= -1 && ax <= 1 && ay >= -1 && ay <= 1 && az >= -1 && az <= 1;
-      // old corner (h, j&1, j>>1) lands on new corner (h-ax, (j&1)-ay, (j>>1)-az): flush it if outside
+      const bool kx = ax == 0 || (ax == 1 && (h ^ px) == 1) || (ax == -1 && (h ^ px) == 0);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int nx = h - ax, ny = (j & 1) - ay, nz = (j >> 1) - az;
-        const bool keep = adj && nx >= 0 && nx <= 1 && ny >= 0 && ny <= 1 && nz >= 0 && nz <= 1;
+        const int dy = (j & 1) ^ py, dz = (j >> 1) ^ pz;
+        const bool ky = ay == 0 || (ay == 1 && dy == 1) || (ay == -1 && dy == 0);
+        const bool kz = az == 0 || (az == 1 && dz == 1) || (az == -1 && dz == 0);
+        const bool keep = kx && ky && kz;
         if (!keep && wsum[j] != 0.f) grid_add(grad + (size_t)rows[j] * NSLAM_C_DIM + ch, acc[j]);
-      }
-      // new corner (h, j&1, j>>1) takes old corner (h+ax, (j&1)+ay, (j>>1)+az) when that exists
-      float nacc[4], nws[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int sy = (j & 1) + ay, sz = (j >> 1) + az;  // wave-uniform source register
-        const bool in_yz = adj && sy >= 0 && sy <= 1 && sz >= 0 && sz <= 1;
-        const int js = in_yz ? sy + 2 * sz : 0;
-        float va = js == 0 ? acc[0] : js == 1 ? acc[1] : js == 2 ? acc[2] : acc[3];
-        float vw = js == 0 ? wsum[0] : js == 1 ? wsum[1] : js == 2 ? wsum[2] : wsum[3];
-        if (ax != 0) {  // x step: the source corner is held by the other half of the wave
-          va = xor32(va);
-          vw = xor32(vw);
-        }
-        const int sx = h + ax;
-        const bool in = in_yz && sx >= 0 && sx <= 1;
-        nacc[j] = in ? va : 0.f;
-        nws[j] = in ? vw : 0.f;
+        acc[j] = keep ? acc[j] : 0.f;
+        wsum[j] = keep ? wsum[j] : 0.f;
+        rows[j] = nr[j];
       }
       cur = cell;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {  // corner 2j+h lives in lane (j >> 1, t) at index 2(j & 1) + h
-        const int r0 = __builtin_amdgcn_readlane(rk[2 * (j & 1)], t + 32 * (j >> 1));
-        const int r1 = __builtin_amdgcn_readlane(rk[2 * (j & 1) + 1], t + 32 * (j >> 1));
-        rows[j] = h ? r1 : r0;
-        acc[j] = nacc[j];
-        wsum[j] = nws[j];
-      }
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float w0 = rdlane(wk[2 * (j & 1)], t + 32 * (j >> 1));
-      const float w1 = rdlane(wk[2 * (j & 1) + 1], t + 32 * (j >> 1));
-      const float w = h ? w1 : w0;
-      acc[j] += w * vcol[t];
-      wsum[j] += w;
+      acc[j] += w[j] * vcol[t];
+      wsum[j] += w[j];
     }
   }
 #pragma unroll
@@ -1406,7 +1410,8 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
     } else {
       // the tape kernel (256 VGPRs) resolves its corners here rather than across the backward
       if (WG) scn = resolve_corners(gr.slot, cr, q.valid, lane);
-      scatter_grid_grad_uniform(gr.grad, scn, cr.cell, dc, S, lane);
+      // walk table: the lean kernels' slot after the transpose image, the tape kernel's sX
+      scatter_grid_grad_uniform(gr.grad, scn, cr.cell, dc, S.sA, WG ? S.sX : S.sA + TILE_FLOATS, lane);
     }
   }
   PHASE(DEC, 13);
@@ -1426,8 +1431,8 @@ __global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd(QueryKArgs a, flo
                                                                  int acc_floats) {
   // per-wave scratch: the scatter needs sA + corner rows/weights; weight gradients add sX and
   // the per-point tables (sizing LDS per variant keeps the lean kernels at 5+ waves/SIMD)
-  // (the lean kernels' register-resident scatter walk needs only the sA transpose image)
-  constexpr int kScr = WG ? kScratchFloats + (SAVED ? TILE_FLOATS : 0) : TILE_FLOATS;
+  // (the lean kernels' scatter walk needs only the sA transpose image and its walk table)
+  constexpr int kScr = WG ? kScratchFloats + (SAVED ? TILE_FLOATS : 0) : TILE_FLOATS + kWalkFloats;
   __shared__ __attribute__((aligned(16))) float lds[kWavesBwd * kScr];
   const int lane = threadIdx.x & 63, wave = wave_id();
   float* sc = lds + wave * kScr;

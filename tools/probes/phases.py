@@ -47,6 +47,10 @@ def main():
         tot = tp[:, marks[-1]] - tp[:, marks[0]]
         print(f"== forward part {nm}: {len(tp)} waves, marks {marks}; wave total median {np.median(tot):.0f} "
               f"p10 {np.percentile(tot, 10):.0f} p90 {np.percentile(tot, 90):.0f}")
+        t0 = np.percentile(t[t[:, 0] != 0][:, 0], 0.5)  # robust to stale marks
+        st, en = tp[:, marks[0]] - t0, tp[:, marks[-1]] - t0
+        print("   start offsets p0/p50/p90/p99/max " + " ".join(f"{np.percentile(st, q):.0f}" for q in (0, 50, 90, 99, 100))
+              + " | end p50/p90/max " + " ".join(f"{np.percentile(en, q):.0f}" for q in (50, 90, 100)))
         for a_, b_ in zip(marks[:-1], marks[1:]):
             dt = tp[:, b_] - tp[:, a_]
             print(f"   {fwd_names[a_]:>12s} -> {fwd_names[b_]:<12s} median {np.median(dt):8.0f}  "
