@@ -106,13 +106,30 @@ __device__ __forceinline__ f32x16 zero16() {
 __device__ float g_hot_frag[1024];
 #endif
 
-// acc += Wblock * X   (frag: packed [lane][16])
+// Global-address-space view of a pointer into device memory.  A pointer read out of the kernel
+// argument struct by a runtime index, or laundered through an asm constraint, is generic to the
+// compiler, and a generic access is a flat_* instruction — which counts in LGKM_CNT as well as
+// VM_CNT, so every LDS wait (s_waitcnt lgkmcnt(0)) also drains the loads in flight (the weight
+// fragments, the activation tape), and every use of a flat-loaded value waits for all LDS traffic.
+// Through this view the same accesses are global_* (VM_CNT only).
+template <class T>
+using gptr_t = const __attribute__((address_space(1))) T*;
+template <class T>
+__device__ __forceinline__ gptr_t<T> as_global(const T* p) {
+  return (gptr_t<T>)p;
+}
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* as_global_w(T* p) {
+  return (__attribute__((address_space(1))) T*)p;
+}
+
+// acc += Wblock * X   (frag: packed [lane][16], global memory)
 __device__ __forceinline__ void gemm_acc(f32x16& acc, const float* __restrict__ frag, const f32x16& x,
                                          int lane) {
 #ifdef NSLAM_EXP_HOTFRAG
   frag = g_hot_frag;
 #endif
-  const f32x4* f = reinterpret_cast<const f32x4*>(frag) + lane * 4;
+  const gptr_t<f32x4> f = as_global(reinterpret_cast<const f32x4*>(frag)) + lane * 4;
   const f32x4 a0 = f[0], a1 = f[1], a2 = f[2], a3 = f[3];
   acc = mfma32(a0[0], x[0], acc);
   acc = mfma32(a0[1], x[1], acc);
@@ -139,6 +156,20 @@ __device__ __forceinline__ f32x16 vec_tile(const float* __restrict__ v, int lane
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const f32x4 q = *reinterpret_cast<const f32x4*>(v + 8 * i + 4 * h);
+    t[4 * i + 0] = q[0];
+    t[4 * i + 1] = q[1];
+    t[4 * i + 2] = q[2];
+    t[4 * i + 3] = q[3];
+  }
+  return t;
+}
+// vec_tile of a vector in global memory (global_load, not flat)
+__device__ __forceinline__ f32x16 vec_tile_g(const float* __restrict__ v, int lane) {
+  const int h = lane >> 5;
+  f32x16 t;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x4 q = *as_global(reinterpret_cast<const f32x4*>(v + 8 * i + 4 * h));
     t[4 * i + 0] = q[0];
     t[4 * i + 1] = q[1];
     t[4 * i + 2] = q[2];
@@ -264,7 +295,7 @@ __device__ __forceinline__ f32x16 gather_tile(const float* __restrict__ grid, co
   f32x16 acc = zero16();
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const f32x4* row = reinterpret_cast<const f32x4*>(grid + (size_t)c.row[k] * NSLAM_C_DIM + 4 * h);
+    const gptr_t<f32x4> row = as_global(reinterpret_cast<const f32x4*>(grid + (size_t)c.row[k] * NSLAM_C_DIM + 4 * h));
     const f32x4 v0 = row[0], v1 = row[2], v2 = row[4], v3 = row[6];
     const float w = c.w[k];
 #pragma unroll
@@ -287,7 +318,7 @@ __device__ __forceinline__ void coord_grad_partial(const float* __restrict__ gri
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     __builtin_amdgcn_sched_barrier(0);  // keep the 8 corner reads from being hoisted together
-    const f32x4* row = reinterpret_cast<const f32x4*>(grid + (size_t)c.row[k] * NSLAM_C_DIM + 4 * h);
+    const gptr_t<f32x4> row = as_global(reinterpret_cast<const f32x4*>(grid + (size_t)c.row[k] * NSLAM_C_DIM + 4 * h));
     const f32x4 v0 = row[0], v1 = row[2], v2 = row[4], v3 = row[6];
     float dot = 0.f;
 #pragma unroll

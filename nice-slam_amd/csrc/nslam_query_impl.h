@@ -74,16 +74,19 @@ __device__ __forceinline__ float fourier_arg(const float x[3], float b0, float b
   return fmaf(x[2], b2, fmaf(x[1], b1, x[0] * b0));
 }
 
-template <bool COS>
+// G: B is in global memory (else LDS or generic); see as_global
+template <bool COS, bool G = false>
 __device__ __forceinline__ f32x16 emb_tile(const float* __restrict__ B, const float x[3], int b, int lane) {
   const int h = lane >> 5;
   f32x16 e;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int k = 32 * b + 8 * i + 4 * h;
-    const f32x4 B0 = *reinterpret_cast<const f32x4*>(B + k);
-    const f32x4 B1 = *reinterpret_cast<const f32x4*>(B + 96 + k);
-    const f32x4 B2 = *reinterpret_cast<const f32x4*>(B + 192 + k);
+    const f32x4 B0 = G ? *as_global(reinterpret_cast<const f32x4*>(B + k)) : *reinterpret_cast<const f32x4*>(B + k);
+    const f32x4 B1 = G ? *as_global(reinterpret_cast<const f32x4*>(B + 96 + k))
+                       : *reinterpret_cast<const f32x4*>(B + 96 + k);
+    const f32x4 B2 = G ? *as_global(reinterpret_cast<const f32x4*>(B + 192 + k))
+                       : *reinterpret_cast<const f32x4*>(B + 192 + k);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float t = fourier_arg(x, B0[j], B1[j], B2[j]);
@@ -154,14 +157,14 @@ constexpr int kTapeFloats = 5 * 16 * 64;  // per tile
 // contiguous, and no 4-register grouping of the tile is needed (a float4 layout cost the forward
 // ~30 VGPRs of copies).
 __device__ __forceinline__ void tape_store(float* __restrict__ t, int i, const f32x16& v, int lane) {
-  float* p = t + i * 1024 + lane;
+  __attribute__((address_space(1))) float* p = as_global_w(t) + i * 1024 + lane;
 #pragma unroll
   for (int r = 0; r < 16; ++r) p[r * 64] = v[r];
 }
 __device__ __forceinline__ f32x16 tape_load(const float* __restrict__ t, int i, int lane) {
   // laundered base: keeps the scheduler from hoisting all five tile loads (80 VGPRs) to the top
   asm volatile("" : "+s"(t));
-  const float* p = t + i * 1024 + lane;
+  const gptr_t<float> p = as_global(t) + i * 1024 + lane;
   f32x16 v;
 #pragma unroll
   for (int r = 0; r < 16; ++r) v[r] = p[r * 64];
@@ -249,61 +252,69 @@ __device__ __forceinline__ void wg_end(const Slab& A, int base, const Scratch& S
 //   layer-3's embedding product is formed right after layer 0, so the 48-register embedding
 //   dies early (the MFMA work is unchanged).
 // ------------------------------------------------------------------------------------------
-template <int NC>
+// vector-section tile: LDS copy (vec_tile) or global (vec_tile_g)
+template <bool VLDS>
+__device__ __forceinline__ f32x16 vtile(const float* __restrict__ v, int lane) {
+  return VLDS ? vec_tile(v, lane) : vec_tile_g(v, lane);
+}
+
+template <int NC, bool VLDS>
 __device__ __forceinline__ f32x16 fc_branch(const float* __restrict__ pk, const XyzPack& L, int i,
-                                            const f32x16 (&cin)[NC], int lane, const float* vec = nullptr) {
+                                            const f32x16 (&cin)[NC], int lane, const float* vec) {
   // vec: the decoder's vector section (biases, output row, Fourier B) — an LDS copy in the
   // decoder-parallel forward, else pk + L.V()
-  f32x16 z = vec_tile((vec ? vec : pk + L.V()) + (L.BiasC(i) - L.V()), lane);
+  f32x16 z = vtile<VLDS>(vec + (L.BiasC(i) - L.V()), lane);
 #pragma unroll
   for (int c = 0; c < NC; ++c) gemm_acc(z, pk + L.FC(i, c) * NSLAM_FRAG, cin[c], lane);
   return z;
 }
 
-template <int NC, bool KEEP, bool PHF = false, bool TAPE = false>
+template <int NC, bool KEEP, bool PHF = false, bool TAPE = false, bool VLDS = false>
 __device__ __forceinline__ f32x16 xyz_forward(const float* __restrict__ pk, const f32x16 (&cin)[NC],
                                               const float x[3], int lane, uint32_t m[5], f32x16* hs,
                                               float* __restrict__ tape = nullptr, const float* vec = nullptr) {
   const XyzPack L{NC};
-  const float* vs = vec ? vec : pk + L.V();  // vector section (LDS copy or global)
+  // vector section: the workgroup's LDS copy (VLDS) or global.  A compile-time choice: a runtime
+  // select of an LDS and a global pointer is a generic pointer, i.e. flat loads.
+  const float* vs = VLDS ? vec : pk + L.V();
 #define PHF_(k) \
   if (PHF) PHASE(0, k)
-  f32x16 a = vec_tile(vs + (L.Bias(0) - L.V()), lane);
-  f32x16 a3 = vec_tile(vs + (L.Bias(3) - L.V()), lane);
+  f32x16 a = vtile<VLDS>(vs + (L.Bias(0) - L.V()), lane);
+  f32x16 a3 = vtile<VLDS>(vs + (L.Bias(3) - L.V()), lane);
 #pragma unroll
   for (int b = 0; b < 3; ++b) {
-    const f32x16 e = emb_tile<false>(vs + (L.FB() - L.V()), x, b, lane);
+    const f32x16 e = emb_tile<false, !VLDS>(vs + (L.FB() - L.V()), x, b, lane);
     gemm_acc(a, pk + (L.L0() + b) * NSLAM_FRAG, e, lane);
     gemm_acc(a3, pk + (L.L3() + b) * NSLAM_FRAG, e, lane);
   }
   PHF_(5);
   m[0] = mask16(a);
-  f32x16 h = relu16(a) + fc_branch<NC>(pk, L, 0, cin, lane, vs);
+  f32x16 h = relu16(a) + fc_branch<NC, VLDS>(pk, L, 0, cin, lane, vs);
   if (KEEP) hs[0] = h;
   if (TAPE) tape_store(tape, 0, h, lane);
-  a = vec_tile(vs + (L.Bias(1) - L.V()), lane);
+  a = vtile<VLDS>(vs + (L.Bias(1) - L.V()), lane);
   gemm_acc(a, pk + L.L1() * NSLAM_FRAG, h, lane);
   m[1] = mask16(a);
-  h = relu16(a) + fc_branch<NC>(pk, L, 1, cin, lane, vs);
+  h = relu16(a) + fc_branch<NC, VLDS>(pk, L, 1, cin, lane, vs);
   if (KEEP) hs[1] = h;
   if (TAPE) tape_store(tape, 1, h, lane);
   PHF_(6);
-  a = vec_tile(vs + (L.Bias(2) - L.V()), lane);
+  a = vtile<VLDS>(vs + (L.Bias(2) - L.V()), lane);
   gemm_acc(a, pk + L.L2() * NSLAM_FRAG, h, lane);
   m[2] = mask16(a);
-  h = relu16(a) + fc_branch<NC>(pk, L, 2, cin, lane, vs);
+  h = relu16(a) + fc_branch<NC, VLDS>(pk, L, 2, cin, lane, vs);
   if (KEEP) hs[2] = h;
   if (TAPE) tape_store(tape, 2, h, lane);
   gemm_acc(a3, pk + (L.L3() + 3) * NSLAM_FRAG, h, lane);
   m[3] = mask16(a3);
-  h = relu16(a3) + fc_branch<NC>(pk, L, 3, cin, lane, vs);
+  h = relu16(a3) + fc_branch<NC, VLDS>(pk, L, 3, cin, lane, vs);
   if (KEEP) hs[3] = h;
   if (TAPE) tape_store(tape, 3, h, lane);
   PHF_(7);
-  a = vec_tile(vs + (L.Bias(4) - L.V()), lane);
+  a = vtile<VLDS>(vs + (L.Bias(4) - L.V()), lane);
   gemm_acc(a, pk + L.L4() * NSLAM_FRAG, h, lane);
   m[4] = mask16(a);
-  h = relu16(a) + fc_branch<NC>(pk, L, 4, cin, lane, vs);
+  h = relu16(a) + fc_branch<NC, VLDS>(pk, L, 4, cin, lane, vs);
   if (TAPE) tape_store(tape, 4, h, lane);
   PHF_(8);
   return h;
@@ -356,7 +367,7 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
   f32x16 dh = zero16();
 #pragma unroll
   for (int j = 0; j < NOUT; ++j) {
-    const f32x16 w = vec_tile(pk + L.Wo() + 32 * j, lane);
+    const f32x16 w = vec_tile_g(pk + L.Wo() + 32 * j, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) dh[r] += w[r] * gall[GOFS + j];
   }
@@ -411,7 +422,7 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
     wg_begin(da3, S, lane);
 #pragma unroll
     for (int b = 0; b < 3; ++b)
-      wg_block<WG>(A, dg.w[3], 125, 32 * b, b < 2 ? 32 : 29, emb_tile<false>(FB, x, b, lane), S, lane);
+      wg_block<WG>(A, dg.w[3], 125, 32 * b, b < 2 ? 32 : 29, emb_tile<false, true>(FB, x, b, lane), S, lane);
     wg_block<WG>(A, dg.w[3], 125, 93, 32, hs[2], S, lane);
     wg_end<WG>(A, dg.b[3], S, lane);
   }
@@ -447,7 +458,7 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
     wg_begin(da, S, lane);
 #pragma unroll
     for (int b = 0; b < 3; ++b)
-      wg_block<WG>(A, dg.w[0], 93, 32 * b, b < 2 ? 32 : 29, emb_tile<false>(FB, x, b, lane), S, lane);
+      wg_block<WG>(A, dg.w[0], 93, 32 * b, b < 2 ? 32 : 29, emb_tile<false, true>(FB, x, b, lane), S, lane);
     wg_end<WG>(A, dg.b[0], S, lane);
   }
 
@@ -460,14 +471,14 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
       f32x16 de = zero16();
       gemm_acc(de, pk + (L.L3T() + b) * NSLAM_FRAG, da3, lane);
       gemm_acc(de, pk + (L.L0T() + b) * NSLAM_FRAG, da, lane);
-      const f32x16 cs = emb_tile<true>(FB, x, b, lane);
+      const f32x16 cs = emb_tile<true, true>(FB, x, b, lane);
       f32x16 G;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int k = 32 * b + 8 * i + 4 * h;
-        const f32x4 B0 = *reinterpret_cast<const f32x4*>(FB + k);
-        const f32x4 B1 = *reinterpret_cast<const f32x4*>(FB + 96 + k);
-        const f32x4 B2 = *reinterpret_cast<const f32x4*>(FB + 192 + k);
+        const f32x4 B0 = *as_global(reinterpret_cast<const f32x4*>(FB + k));
+        const f32x4 B1 = *as_global(reinterpret_cast<const f32x4*>(FB + 96 + k));
+        const f32x4 B2 = *as_global(reinterpret_cast<const f32x4*>(FB + 192 + k));
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float gk = de[4 * i + j] * cs[4 * i + j];
@@ -512,19 +523,19 @@ template <bool KEEP>
 __device__ __forceinline__ f32x16 noxyz_forward(const float* __restrict__ pk, const f32x16& c, int lane,
                                                 uint32_t m[5], f32x16* hs) {
   const NoXyzPack L;
-  f32x16 a = vec_tile(pk + L.Bias(0), lane);
+  f32x16 a = vec_tile_g(pk + L.Bias(0), lane);
   gemm_acc(a, pk + L.L0() * NSLAM_FRAG, c, lane);
-  f32x16 a3 = vec_tile(pk + L.Bias(3), lane);
+  f32x16 a3 = vec_tile_g(pk + L.Bias(3), lane);
   gemm_acc(a3, pk + L.L3() * NSLAM_FRAG, c, lane);
   m[0] = mask16(a);
   f32x16 h = relu16(a);
   if (KEEP) hs[0] = h;
-  a = vec_tile(pk + L.Bias(1), lane);
+  a = vec_tile_g(pk + L.Bias(1), lane);
   gemm_acc(a, pk + L.L1() * NSLAM_FRAG, h, lane);
   m[1] = mask16(a);
   h = relu16(a);
   if (KEEP) hs[1] = h;
-  a = vec_tile(pk + L.Bias(2), lane);
+  a = vec_tile_g(pk + L.Bias(2), lane);
   gemm_acc(a, pk + L.L2() * NSLAM_FRAG, h, lane);
   m[2] = mask16(a);
   h = relu16(a);
@@ -533,7 +544,7 @@ __device__ __forceinline__ f32x16 noxyz_forward(const float* __restrict__ pk, co
   m[3] = mask16(a3);
   h = relu16(a3);
   if (KEEP) hs[3] = h;
-  a = vec_tile(pk + L.Bias(4), lane);
+  a = vec_tile_g(pk + L.Bias(4), lane);
   gemm_acc(a, pk + L.L4() * NSLAM_FRAG, h, lane);
   m[4] = mask16(a);
   return relu16(a);
@@ -550,7 +561,7 @@ __device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, con
   const f32x16 h4 = noxyz_forward<WG != 0>(pk, c, lane, m, hs);
   f32x16 dh;
   {
-    const f32x16 w = vec_tile(pk + L.Wo(), lane);
+    const f32x16 w = vec_tile_g(pk + L.Wo(), lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) dh[r] = w[r] * g;
   }
@@ -637,7 +648,7 @@ __device__ __forceinline__ void xyz_backward_saved(const float* __restrict__ pk,
   f32x16 dh = zero16();
 #pragma unroll
   for (int j = 0; j < NOUT; ++j) {
-    const f32x16 w = vec_tile(pk + L.Wo() + 32 * j, lane);
+    const f32x16 w = vec_tile_g(pk + L.Wo() + 32 * j, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) dh[r] += w[r] * gall[GOFS + j];
   }
@@ -668,13 +679,13 @@ __device__ __forceinline__ void xyz_backward_saved(const float* __restrict__ pk,
       f32x16 de = zero16();
       gemm_acc(de, pk + (L.L3T() + b) * NSLAM_FRAG, da3, lane);
       gemm_acc(de, pk + (L.L0T() + b) * NSLAM_FRAG, da, lane);
-      const f32x16 cs = emb_tile<true>(FB, x, b, lane);
+      const f32x16 cs = emb_tile<true, true>(FB, x, b, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int k = 32 * b + 8 * i + 4 * h;
-        const f32x4 B0 = *reinterpret_cast<const f32x4*>(FB + k);
-        const f32x4 B1 = *reinterpret_cast<const f32x4*>(FB + 96 + k);
-        const f32x4 B2 = *reinterpret_cast<const f32x4*>(FB + 192 + k);
+        const f32x4 B0 = *as_global(reinterpret_cast<const f32x4*>(FB + k));
+        const f32x4 B1 = *as_global(reinterpret_cast<const f32x4*>(FB + 96 + k));
+        const f32x4 B2 = *as_global(reinterpret_cast<const f32x4*>(FB + 192 + k));
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float gk = de[4 * i + j] * cs[4 * i + j];
@@ -708,7 +719,7 @@ __device__ __forceinline__ void color_backward_tape(const float* __restrict__ pk
   f32x16 dh = zero16();
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    const f32x16 w = vec_tile(pk + L.Wo() + 32 * j, lane);
+    const f32x16 w = vec_tile_g(pk + L.Wo() + 32 * j, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) dh[r] += w[r] * gall[j];
   }
@@ -790,9 +801,9 @@ __device__ __forceinline__ void color_backward_tape(const float* __restrict__ pk
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int k = 32 * b + 8 * i + 4 * h;
-      const f32x4 B0 = *reinterpret_cast<const f32x4*>(FB + k);
-      const f32x4 B1 = *reinterpret_cast<const f32x4*>(FB + 96 + k);
-      const f32x4 B2 = *reinterpret_cast<const f32x4*>(FB + 192 + k);
+      const f32x4 B0 = *as_global(reinterpret_cast<const f32x4*>(FB + k));
+      const f32x4 B1 = *as_global(reinterpret_cast<const f32x4*>(FB + 96 + k));
+      const f32x4 B2 = *as_global(reinterpret_cast<const f32x4*>(FB + 192 + k));
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float sv, cv;
@@ -840,7 +851,7 @@ __device__ __forceinline__ void noxyz_backward_saved(const float* __restrict__ p
   const NoXyzPack L;
   f32x16 dh;
   {
-    const f32x16 w = vec_tile(pk + L.Wo(), lane);
+    const f32x16 w = vec_tile_g(pk + L.Wo(), lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) dh[r] = w[r] * g;
   }
@@ -1186,7 +1197,7 @@ __device__ __forceinline__ void fwd_part_middle(const QueryKArgs& a, const Pt& q
   const float* pk = a.c.packed[NSLAM_DEC_MIDDLE];
   const XyzPack L{1};
   const f32x16 cms[1] = {cm};
-  const f32x16 h4 = xyz_forward<1, false, true>(pk, cms, q.x, lane, m, nullptr, nullptr, vec);
+  const f32x16 h4 = xyz_forward<1, false, true, false, true>(pk, cms, q.x, lane, m, nullptr, nullptr, vec);
   save_masks(a, NSLAM_DEC_MIDDLE, tile, m, lane);
   float o = out_row(vec + (L.Wo() - L.V()), vec + (L.Bo() - L.V()), 0, h4, lane);
   if (!q.inside) o = 100.f;
@@ -1208,7 +1219,7 @@ __device__ __forceinline__ void fwd_part_fine(const QueryKArgs& a, const Pt& q, 
   PHASE(0, 3);
   const float* pk = a.c.packed[NSLAM_DEC_FINE];
   const XyzPack L{2};
-  const f32x16 h4 = xyz_forward<2, false, true>(pk, cf, q.x, lane, m, nullptr, nullptr, vec);
+  const f32x16 h4 = xyz_forward<2, false, true, false, true>(pk, cf, q.x, lane, m, nullptr, nullptr, vec);
   save_masks(a, NSLAM_DEC_FINE, tile, m, lane);
   float o = out_row(vec + (L.Wo() - L.V()), vec + (L.Bo() - L.V()), 0, h4, lane);
   if (!q.inside) o = 0.f;
@@ -1235,7 +1246,7 @@ __device__ __forceinline__ void fwd_part_color(const QueryKArgs& a, const Pt& q,
   const float* pk = a.c.packed[NSLAM_DEC_COLOR];
   const XyzPack L{1};
   float* tp = TAPE ? a.c.act_tape + tile * kTapeFloats : nullptr;
-  const f32x16 h4 = xyz_forward<1, false, true, TAPE>(pk, cc, q.x, lane, m, nullptr, tp, vec);
+  const f32x16 h4 = xyz_forward<1, false, true, TAPE, true>(pk, cc, q.x, lane, m, nullptr, tp, vec);
   save_masks(a, NSLAM_DEC_COLOR, tile, m, lane);
   float o[3];
 #pragma unroll
