@@ -156,18 +156,26 @@ constexpr int kTapeFloats = 5 * 16 * 64;  // per tile
 // Layout [tile][layer][register r][64 lanes] float: every store / load instruction moves 256 B
 // contiguous, and no 4-register grouping of the tile is needed (a float4 layout cost the forward
 // ~30 VGPRs of copies).
+// Point-major: layer i of a tile is [32 points][32 features], the layout of the weight-gradient
+// MFMA's B operand (K = points), so the backward streams it from global memory with no LDS
+// transpose.  The forward stores registers 4k..4k+3 of lane (p, h) — features 8k+4h..+3, i.e.
+// F(r, h) — as one 16-B store at [p][8k+4h].
 __device__ __forceinline__ void tape_store(float* __restrict__ t, int i, const f32x16& v, int lane) {
-  __attribute__((address_space(1))) float* p = as_global_w(t) + i * 1024 + lane;
+  const int p = lane & 31, h = lane >> 5;
+  __attribute__((address_space(1))) f32x4* q =
+      reinterpret_cast<__attribute__((address_space(1))) f32x4*>(as_global_w(t) + i * 1024 + p * 32 + 4 * h);
 #pragma unroll
-  for (int r = 0; r < 16; ++r) p[r * 64] = v[r];
+  for (int k = 0; k < 4; ++k) q[2 * k] = f32x4{v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]};
 }
-__device__ __forceinline__ f32x16 tape_load(const float* __restrict__ t, int i, int lane) {
+// Layer i of the tape as an MFMA B-operand stream over the points: element s of lane (j, h) is
+// h_i[point 2s+h][feature j] (each load instruction reads two 128-B point rows).
+__device__ __forceinline__ f32x16 tape_bop(const float* __restrict__ t, int i, int lane) {
   // laundered base: keeps the scheduler from hoisting all five tile loads (80 VGPRs) to the top
   asm volatile("" : "+s"(t));
-  const gptr_t<float> p = as_global(t) + i * 1024 + lane;
+  const gptr_t<float> p = as_global(t) + i * 1024 + (lane >> 5) * 32 + (lane & 31);
   f32x16 v;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] = p[r * 64];
+  for (int s = 0; s < 16; ++s) v[s] = p[s * 64];
   return v;
 }
 
@@ -205,6 +213,20 @@ __device__ __forceinline__ void dw_block_img(const Slab& A, int base, int ldk, i
   for (int s = 0; s < 16; ++s) acc = mfma32(sa[(2 * s + h) * TPITCH + j], sx[(2 * s + h) * TPITCH + j], acc);
   if (j < kvalid) {
     const int lo = 4 * h * ldk + j;  // fidx(r, h) = (r & 3) + 8 (r >> 2) + 4 h
+#pragma unroll
+    for (int r = 0; r < 16; ++r) put<WG>(A, lo, base + ((r & 3) + 8 * (r >> 2)) * ldk + kofs, acc[r]);
+  }
+}
+// the same with the input side as a B-operand stream in registers (tape_bop): no sx image
+template <int WG>
+__device__ __forceinline__ void dw_block_bop(const Slab& A, int base, int ldk, int kofs, int kvalid,
+                                             const float* __restrict__ sa, const f32x16& bx, int lane) {
+  const int h = lane >> 5, j = lane & 31;
+  f32x16 acc = zero16();
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc = mfma32(sa[(2 * s + h) * TPITCH + j], bx[s], acc);
+  if (j < kvalid) {
+    const int lo = 4 * h * ldk + j;
 #pragma unroll
     for (int r = 0; r < 16; ++r) put<WG>(A, lo, base + ((r & 3) + 8 * (r >> 2)) * ldk + kofs, acc[r]);
   }
@@ -714,7 +736,9 @@ __device__ __forceinline__ void color_backward_tape(const float* __restrict__ pk
                                                     const Slab& A, const Scratch& S, int lane, f32x16& dc) {
   const XyzPack L{1};
   const int h = lane >> 5, f = lane & 31;
-  const f32x16 c1[1] = {cin};
+  // sX holds the colour feature's image through layers 4..0: the input of every fc_c weight
+  // gradient (one transpose per tile); the hidden inputs come from the tape as B-operand streams
+  tstore(S.sX, cin, lane);
   // output layer (3 rows used; row 3 is overwritten by the stage combiner, decoder.py:331-334)
   f32x16 dh = zero16();
 #pragma unroll
@@ -723,72 +747,79 @@ __device__ __forceinline__ void color_backward_tape(const float* __restrict__ pk
 #pragma unroll
     for (int r = 0; r < 16; ++r) dh[r] += w[r] * gall[j];
   }
-  tstore(S.sX, tape_load(tape, 4, lane), lane);
-  lds_sync();
+  {
+    const f32x16 b4 = tape_bop(tape, 4, lane);  // h4[2t+h][f]
+    lds_sync();
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    float sw = 0.f;
+    for (int j = 0; j < 3; ++j) {
+      float sw = 0.f;
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const int p = 2 * t + h;
-      sw += S.gtab[p * 4 + j] * S.sX[p * TPITCH + f];
+      for (int t = 0; t < 16; ++t) sw += S.gtab[(2 * t + h) * 4 + j] * b4[t];
+      sw += xor32(sw);
+      if (h == 0) put<WG>(A, f, dg.wo + 32 * j, sw);
+      // dbo[j] = sum over the tile's points: butterfly over the 32 point lanes of half 0
+      float sb = gall[j];
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) sb += __shfl_xor(sb, o, 64);
+      if (lane == 0) put<WG>(A, 0, dg.bo + j, sb);
     }
-    sw += xor32(sw);
-    if (h == 0) put<WG>(A, f, dg.wo + 32 * j, sw);
-    // dbo[j] = sum over the tile's points: butterfly over the 32 point lanes of half 0
-    float sb = gall[j];
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) sb += __shfl_xor(sb, o, 64);
-    if (lane == 0) put<WG>(A, 0, dg.bo + j, sb);
   }
   if (WG == 1) {
     if (h == 0) put<1>(A, f, dg.wo + 96, 0.f);
     if (lane == 0) put<1>(A, 0, dg.bo + 3, 0.f);
   }
-  lds_sync();
   PHASE(3, 5);
   dc = zero16();
+  // fc_c branch i: dc += FC_i^T dh; dFC_i = dh (x) c (c image in sX); dbFC_i = sum dh
+  auto fc_step = [&](int i) {
+    gemm_acc(dc, pk + L.FCT(i) * NSLAM_FRAG, dh, lane);
+    tstore(S.sA, dh, lane);
+    lds_sync();
+    dw_block_img<WG>(A, dg.wc[i], 32, 0, 32, S.sA, S.sX, lane);
+    db_vec_img<WG>(A, dg.bc[i], S.sA, lane);
+    lds_sync();
+  };
+  // layer i's weight gradient: dW_i = da (x) h_{i-1} (tape B operand), db_i = sum da
+  auto w_step = [&](int i, const float* sa, int ldk, int kofs, const f32x16& bx) {
+    lds_sync();
+    dw_block_bop<WG>(A, dg.w[i], ldk, kofs, 32, sa, bx, lane);
+    db_vec_img<WG>(A, dg.b[i], sa, lane);
+    lds_sync();
+  };
   // layer 4 (input h3)
-  fc_bwd<1, WG>(pk, L, 4, c1, dh, dg, A, S, lane, dc);
+  fc_step(4);
   f32x16 da = apply_mask(dh, m[4]);
-  wg_begin(da, S, lane);
-  wg_block<WG>(A, dg.w[4], 32, 0, 32, tape_load(tape, 3, lane), S, lane);
-  wg_end<WG>(A, dg.b[4], S, lane);
+  tstore(S.sA, da, lane);
+  w_step(4, S.sA, 32, 0, tape_bop(tape, 3, lane));
   dh = zero16();
   gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
   PHASE(3, 6);
   // layer 3 (input [emb | h2]): the h2 columns now, the embedding columns at the end
-  fc_bwd<1, WG>(pk, L, 3, c1, dh, dg, A, S, lane, dc);
+  fc_step(3);
   const f32x16 da3 = apply_mask(dh, m[3]);
   tstore(S.sD3, da3, lane);
-  tstore(S.sX, tape_load(tape, 2, lane), lane);
-  lds_sync();
-  dw_block_img<WG>(A, dg.w[3], 125, 93, 32, S.sD3, S.sX, lane);
-  db_vec_img<WG>(A, dg.b[3], S.sD3, lane);
-  lds_sync();
+  w_step(3, S.sD3, 125, 93, tape_bop(tape, 2, lane));
   dh = zero16();
   gemm_acc(dh, pk + (L.L3T() + 3) * NSLAM_FRAG, da3, lane);
   PHASE(3, 7);
   // layer 2 (input h1)
-  fc_bwd<1, WG>(pk, L, 2, c1, dh, dg, A, S, lane, dc);
+  fc_step(2);
   da = apply_mask(dh, m[2]);
-  wg_begin(da, S, lane);
-  wg_block<WG>(A, dg.w[2], 32, 0, 32, tape_load(tape, 1, lane), S, lane);
-  wg_end<WG>(A, dg.b[2], S, lane);
+  tstore(S.sA, da, lane);
+  w_step(2, S.sA, 32, 0, tape_bop(tape, 1, lane));
   dh = zero16();
   gemm_acc(dh, pk + L.L2T() * NSLAM_FRAG, da, lane);
   PHASE(3, 8);
   // layer 1 (input h0)
-  fc_bwd<1, WG>(pk, L, 1, c1, dh, dg, A, S, lane, dc);
+  fc_step(1);
   da = apply_mask(dh, m[1]);
-  wg_begin(da, S, lane);
-  wg_block<WG>(A, dg.w[1], 32, 0, 32, tape_load(tape, 0, lane), S, lane);
-  wg_end<WG>(A, dg.b[1], S, lane);
+  tstore(S.sA, da, lane);
+  w_step(1, S.sA, 32, 0, tape_bop(tape, 0, lane));
   dh = zero16();
   gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
   PHASE(3, 9);
   // layer 0 (input emb): its cotangent stays in sA for the embedding blocks
-  fc_bwd<1, WG>(pk, L, 0, c1, dh, dg, A, S, lane, dc);
+  fc_step(0);
   da = apply_mask(dh, m[0]);
   wg_begin(da, S, lane);
   wg_end<WG>(A, dg.b[0], S, lane);

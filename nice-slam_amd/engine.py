@@ -99,6 +99,8 @@ class MappingEngine:
         self._side = []     # side streams of the concurrent decoder backward
         self.concurrent = True
         self.priority = False  # concurrent: run the weight-gradient branch on a high-priority stream
+        self.all_side = False  # concurrent: every branch on a side stream (main only forks / joins)
+        self.lean_first = False  # concurrent: enqueue the frozen decoders' branches before the weight-gradient one
         self._hi = None
         for k, v in c.items():
             if not v.is_contiguous(memory_format=torch.channels_last_3d):
@@ -203,12 +205,14 @@ class MappingEngine:
         main = torch.cuda.current_stream(z.device)
         streams = [main]
         if concurrent:
-            while len(self._side) < len(decs) - 1:
+            while len(self._side) < len(decs):
                 self._side.append(torch.cuda.Stream(z.device))
             if self.priority:  # the critical (MFMA-heavy) branch gets its waves dispatched first
                 if self._hi is None:
                     self._hi = torch.cuda.Stream(z.device, priority=-1)
                 streams = [self._hi]
+            elif self.all_side:
+                streams = [self._side[len(decs) - 1]]
             streams += self._side[:len(decs) - 1]
         used = [st for st in streams if st is not main]
         gp = [torch.empty(n, 3, dtype=torch.float64, device=z.device) for _ in decs] if pts_grad else None
@@ -218,7 +222,10 @@ class MappingEngine:
                 for t in (ro, rd, z, g_raw, self._saved, self._tape):
                     if t is not None:
                         t.record_stream(st)
-            for i, name in enumerate(decs):
+            order = list(enumerate(decs))
+            if concurrent and self.lean_first:
+                order = order[1:] + order[:1]
+            for i, name in order:
                 st = streams[i] if concurrent else main
                 d = ops._DEC_ID[name]
                 with torch.cuda.stream(st):

@@ -36,9 +36,12 @@ def timed(scene, steps=200):
 def main():
     dev = torch.device("cuda:0")
     scene = bench.Room0Scene(dev, 0, path="fused")
-    tag = os.environ.get("NSLAM_FWD_PARTS", "3")
+    tag = os.environ.get("NSLAM_FWD_PARTS", "auto")
+    base = {"priority": False, "concurrent": True, "all_side": False, "lean_first": False}
     for name, knobs in (("default", {}), ("priority", {"priority": True}), ("sequential", {"concurrent": False}),
-                        ("default", {"priority": False, "concurrent": True})):
+                        ("all_side", {"all_side": True}), ("lean_first", {"lean_first": True}),
+                        ("side+lean", {"all_side": True, "lean_first": True}), ("default", {})):
+        knobs = {**base, **knobs}
         for k, v in knobs.items():
             setattr(scene.engine, k, v)
         ms, rate = timed(scene)
