@@ -100,8 +100,8 @@ typedef struct nslam_query_cfg {
   int32_t defer_occ;
   int32_t pad2_;
   /* ABI v9: activation tape of the colour decoder (NULL = none).  nslam_query_fwd[_ws] writes the
-   * post-ReLU hidden tiles h0..h4 of every 32-point tile ([tile][layer][4][64] float4,
-   * nslam_query_tape_size(M) bytes); with it and saved_masks the colour decoder's weight-gradient
+   * post-ReLU hidden tiles h0..h4 of every 32-point tile ([tile][layer][32 points][32 features]
+   * float, nslam_query_tape_size(M) bytes; layout private to the library); with it and saved_masks the colour decoder's weight-gradient
    * backward reads them instead of recomputing its forward (Mapper.py:503). */
   float* act_tape;
 } nslam_query_cfg;
