@@ -1468,8 +1468,11 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
   PHASE(DEC, 14);
 }
 
+#ifndef NSLAM_LEAN_LB
+#define NSLAM_LEAN_LB 2  // min waves per SIMD of the mask-only kernels (experiments: 3..5)
+#endif
 template <int DEC, int WG, bool PG, bool FIRST, bool SAVED>
-__global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd(QueryKArgs a, float* __restrict__ slab,
+__global__ __launch_bounds__(64 * kWavesBwd, (WG || PG || !SAVED) ? 2 : NSLAM_LEAN_LB) void k_dec_bwd(QueryKArgs a, float* __restrict__ slab,
                                                                  int acc_floats) {
   // per-wave scratch: the scatter needs sA + corner rows/weights; weight gradients add sX and
   // the per-point tables (sizing LDS per variant keeps the lean kernels at 5+ waves/SIMD)

@@ -1,6 +1,6 @@
 """Mapping-iteration time under engine knobs (one process, hipGraph-replayed like bench.py).
 
-python tools/probes/knobs.py            (NSLAM_FWD_PARTS etc. are per-process: run it again)
+python tools/probes/knobs.py [knob names]   (NSLAM_FWD_PARTS, NSLAM_LIB are per-process)
 Prints ms/iteration and M ray-samples/s for: the default engine, the weight-gradient branch on a
 high-priority stream, and sequential (non-concurrent) decoder backward launches.
 """
@@ -36,11 +36,13 @@ def timed(scene, steps=200):
 def main():
     dev = torch.device("cuda:0")
     scene = bench.Room0Scene(dev, 0, path="fused")
-    tag = os.environ.get("NSLAM_FWD_PARTS", "auto")
+    tag = os.environ.get("NSLAM_FWD_PARTS", "auto") + " " + os.path.basename(os.environ.get("NSLAM_LIB", "libnslam.so"))
     base = {"priority": False, "concurrent": True, "all_side": False, "lean_first": False}
     for name, knobs in (("default", {}), ("priority", {"priority": True}), ("sequential", {"concurrent": False}),
                         ("all_side", {"all_side": True}), ("lean_first", {"lean_first": True}),
                         ("side+lean", {"all_side": True, "lean_first": True}), ("default", {})):
+        if len(sys.argv) > 1 and name not in sys.argv[1:]:
+            continue
         knobs = {**base, **knobs}
         for k, v in knobs.items():
             setattr(scene.engine, k, v)
