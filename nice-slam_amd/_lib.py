@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NSLAM_LIB") or os.path.join(_HERE, "libnslam.so")  # NSLAM_LIB: instrumented builds
 
 NSLAM_OK = 0
-ABI_VERSION = 9
+ABI_VERSION = 10
 STAGES = {"coarse": 0, "middle": 1, "fine": 2, "color": 3}
 DEC_COARSE, DEC_MIDDLE, DEC_FINE, DEC_COLOR = 0, 1, 2, 3
 
@@ -109,6 +109,7 @@ class NslamAdamSeg(ctypes.Structure):
 EXPORTS = (
     "nslam_pack_layout", "nslam_sample_rays", "nslam_query_fwd", "nslam_query_bwd", "nslam_query_bwd_workspace_size",
     "nslam_query_saved_size", "nslam_query_bwd_decoder", "nslam_query_bwd_decoder_workspace_size",
+    "nslam_query_bwd_decoders",
     "nslam_composite_fwd", "nslam_composite_bwd", "nslam_grid_sample_fwd", "nslam_grid_sample_bwd",
     "nslam_workspace_size", "nslam_strerror", "nslam_abi_version", "nslam_gather_rays", "nslam_render_loss",
     "nslam_render_loss_workspace_size", "nslam_adam_step", "nslam_rows_pack", "nslam_rows_unpack",
@@ -145,6 +146,7 @@ def lib():
         L.nslam_query_bwd_workspace_size.argtypes = [ctypes.POINTER(NslamQueryCfg), i64]
         L.nslam_query_bwd_workspace_size.restype = sz
         L.nslam_query_bwd_decoder.argtypes = [ctypes.POINTER(NslamQueryCfg), i32, i32, vp, i64, vp, vp, vp, sz, vp]
+        L.nslam_query_bwd_decoders.argtypes = [ctypes.POINTER(NslamQueryCfg), i32, vp, i64, vp, ctypes.POINTER(vp), vp]
         L.nslam_query_bwd_decoder_workspace_size.argtypes = [ctypes.POINTER(NslamQueryCfg), i32, i64]
         L.nslam_query_bwd_decoder_workspace_size.restype = sz
         L.nslam_query_saved_size.argtypes = [i64]

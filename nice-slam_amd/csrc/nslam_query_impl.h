@@ -1367,7 +1367,7 @@ constexpr int kMaxSlabs = 4096;  // WG == 2 above this many tiles
 
 template <int DEC, int WG, bool PG, bool FIRST, bool SAVED>
 __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, const Slab& A, const Scratch& S,
-                                             int lane) {
+                                             int lane, double* __restrict__ gpts) {
   // Every scratch / slab address is a function of the lane only, i.e. invariant across the tile
   // loop; letting LICM hoist the ~300 of them pins (and spills) the register file.  Re-derive
   // them per tile.
@@ -1462,7 +1462,7 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
     coord_grad(gr, cr, dc, lane, gp);
     if (h == 0 && q.valid) {
 #pragma unroll
-      for (int k = 0; k < 3; ++k) a.g_pts[idx * 3 + k] = FIRST ? gp[k] : a.g_pts[idx * 3 + k] + gp[k];
+      for (int k = 0; k < 3; ++k) gpts[idx * 3 + k] = FIRST ? gp[k] : gpts[idx * 3 + k] + gp[k];
     }
   }
   PHASE(DEC, 14);
@@ -1500,11 +1500,11 @@ __global__ __launch_bounds__(64 * kWavesBwd, (WG || PG || !SAVED) ? 2 : NSLAM_LE
   const int64_t w = (int64_t)blockIdx.x * kWavesBwd + wave;
   const Slab A = make_slab(WG ? slab + (size_t)w * acc_floats : slab, WG ? acc_floats : 0);
   if (WG == 0) {  // one tile per wave (grid covers all tiles)
-    if (w < ntiles) dec_bwd_tile<DEC, WG, PG, FIRST, SAVED>(a, w, A, S, lane);
+    if (w < ntiles) dec_bwd_tile<DEC, WG, PG, FIRST, SAVED>(a, w, A, S, lane, a.g_pts);
     return;
   }
   if (WG == 1) {  // one tile per wave, then the workgroup folds its waves' slabs into its first one
-    if (w < ntiles) dec_bwd_tile<DEC, WG, PG, FIRST, SAVED>(a, w, A, S, lane);
+    if (w < ntiles) dec_bwd_tile<DEC, WG, PG, FIRST, SAVED>(a, w, A, S, lane, a.g_pts);
     // the slabs were just written by this CU (L2-resident): summing them here in wave order (a
     // fixed order: deterministic) leaves k_slab_reduce a quarter of the bytes to read
     __syncthreads();
@@ -1521,7 +1521,39 @@ __global__ __launch_bounds__(64 * kWavesBwd, (WG || PG || !SAVED) ? 2 : NSLAM_LE
   }
 #pragma nounroll
   for (int64_t tile = w; tile < ntiles; tile += (int64_t)gridDim.x * kWavesBwd)
-    dec_bwd_tile<DEC, WG, PG, FIRST, SAVED>(a, tile, A, S, lane);
+    dec_bwd_tile<DEC, WG, PG, FIRST, SAVED>(a, tile, A, S, lane, a.g_pts);
+}
+
+// Mask-only backward of several decoders in ONE launch (ABI v10 nslam_query_bwd_decoders): the
+// decoders' workgroups are interleaved over blockIdx (part = blockIdx % ndec), so frozen decoders
+// that would otherwise run as concurrent launches on separate streams (tracking: middle, fine and
+// colour; mapping: middle and fine) need no fork / join between streams.  Each part writes its own
+// d/dpts buffer gp[part] (no cross-decoder accumulation, no atomics on points).
+struct MultiDecArgs {
+  int ndec;
+  int dec[4];
+  double* gp[4];
+};
+template <bool PG>
+__global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd_multi(QueryKArgs a, MultiDecArgs m) {
+  constexpr int kScr = TILE_FLOATS + kWalkFloats;
+  __shared__ __attribute__((aligned(16))) float lds[kWavesBwd * kScr];
+  const int lane = threadIdx.x & 63, wave = wave_id();
+  Scratch S;
+  S.sA = lds + wave * kScr;
+  S.sX = S.sD3 = S.gtab = S.xtab = S.cw = nullptr;
+  S.crow = S.ccell = nullptr;
+  const int part = (int)(blockIdx.x % (unsigned)m.ndec);
+  const int64_t w = (int64_t)(blockIdx.x / (unsigned)m.ndec) * kWavesBwd + wave;
+  if (w >= (a.n + 31) / 32) return;
+  const Slab A = make_slab(nullptr, 0);
+  double* gp = m.gp[part];
+  switch (m.dec[part]) {
+    case NSLAM_DEC_COARSE: dec_bwd_tile<NSLAM_DEC_COARSE, 0, PG, true, true>(a, w, A, S, lane, gp); break;
+    case NSLAM_DEC_MIDDLE: dec_bwd_tile<NSLAM_DEC_MIDDLE, 0, PG, true, true>(a, w, A, S, lane, gp); break;
+    case NSLAM_DEC_FINE: dec_bwd_tile<NSLAM_DEC_FINE, 0, PG, true, true>(a, w, A, S, lane, gp); break;
+    default: dec_bwd_tile<NSLAM_DEC_COLOR, 0, PG, true, true>(a, w, A, S, lane, gp); break;
+  }
 }
 
 // base[j] += sum_b slab[b][j].  A workgroup owns 64 parameters; lane (r, c) of a wave reads the

@@ -9,3 +9,5 @@ template int dispatch_dec_bwd<NSLAM_DEC_MIDDLE>(const QueryKArgs&, bool, float*,
 template int dispatch_dec_bwd<NSLAM_DEC_FINE>(const QueryKArgs&, bool, float*, hipStream_t);
 template int dispatch_dec_bwd<NSLAM_DEC_COLOR>(const QueryKArgs&, bool, float*, hipStream_t);
 }  // namespace nslamq
+
+#include "nslam_query_multi.hip"

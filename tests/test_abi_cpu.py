@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_strerror(pkg):
     L = pkg._lib.lib()
-    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 9
+    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 10
     assert L.nslam_strerror(0) == b"ok"
     assert b"invalid" in L.nslam_strerror(-1)
 
@@ -138,3 +138,15 @@ def test_v8_cam_pose_validates_without_gpu(pkg):
     L = pkg._lib.lib()
     assert L.nslam_cam_pose(None, 64, None) == -1
     assert L.nslam_cam_pose(64, None, None) == -1
+
+
+def test_v10_bwd_decoders_validates_without_gpu(pkg):
+    """nslam_query_bwd_decoders rejects bad configs, masks and missing buffers before any launch."""
+    L = pkg._lib.lib()
+    cfg = pkg._lib.NslamQueryCfg()
+    cfg.stage = 7
+    gps = (ctypes.c_void_p * 4)()
+    assert L.nslam_query_bwd_decoders(ctypes.byref(cfg), 0b0110, None, 10, None, gps, None) == -1  # bad stage
+    ok = pkg._lib.NslamQueryCfg()
+    rc = L.nslam_query_bwd_decoders(ctypes.byref(ok), 0, None, 0, None, gps, None)
+    assert rc < 0  # an empty decoder mask (or an otherwise incomplete config) is never launched

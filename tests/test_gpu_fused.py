@@ -591,3 +591,52 @@ def test_cam_pose_kernel_matches_get_camera_from_tensor():
         worst = max(worst, float((out - ref).abs().max() / ref.abs().max()))
     print(f"cam_pose: {exact}/200 bit-identical, worst rel {worst:.2e}")
     assert worst < 1e-6
+
+
+@pytest.mark.gpu
+def test_merged_frozen_backward_matches_per_decoder_launches(tiny):
+    """ABI v10 nslam_query_bwd_decoders (the frozen decoders' mask-only backward as ONE launch) ==
+    one nslam_query_bwd_decoder launch per decoder: mapping grid gradients (float atomics: up to
+    summation order) and the tracking camera gradient (per-decoder d/dpts buffers: bit-exact)."""
+    import copy
+
+    sc, frames = _frames(tiny)
+    keys = ("grid_middle", "grid_fine", "grid_color")
+    pix = torch.randint(96 * 128, (3 * 150,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(21))
+    out = {}
+    for merge in (False, True):
+        nice, c = _nice(sc)
+        eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV)
+        eng.merge_frozen = merge
+        opt = P.ops.FusedAdam([{"params": [eng.decs["color"].param], "lr": 0.0}] +
+                              [{"params": [c[k]], "lr": 0.0} for k in keys])
+        gr = {}
+
+        def snapshot(ks, dn):
+            for k in keys:
+                gr[k] = eng.ggrad[k].clone()
+            gr["dec"] = eng.decs["color"].grad.clone()
+
+        eng.iteration("color", frames, pix, 150, (96, 128), (sc.fx, sc.fy, sc.cx, sc.cy), opt, exchange=snapshot)
+        out[merge] = gr
+    for k in keys:
+        assert float(out[False][k].abs().sum()) > 0, k
+        assert rel_l2(out[True][k], out[False][k]) < 1e-6, k
+    assert torch.equal(out[True]["dec"], out[False]["dec"])
+    # tracking: middle, fine and colour frozen, d/dpts per decoder
+    scn = Scene(tiny)
+    slam = scn.slam(base_cfg())
+    cam0 = P.common.get_tensor_from_camera(scn.c2w).cuda()
+    pixs = torch.randint(400, (200,), generator=torch.Generator().manual_seed(5))
+    grads = {}
+    for merge in (False, True):
+        te = P.engine.TrackingEngine(copy.deepcopy(slam.shared_decoders), slam.shared_c, scn.bound, 32, 16,
+                                     (scn.H, scn.W), (scn.fx, scn.fy, scn.cx, scn.cy), ignore_edge=(20, 20),
+                                     w_color=0.5, handle_dynamic=True, use_color=True, device=DEV)
+        te.eng.merge_frozen = merge  # (the default, None, merges here: every tracking decoder is frozen)
+        cam = cam0.clone().requires_grad_(True)
+        opt = P.ops.FusedAdam([{"params": [cam], "lr": 0.0}])
+        te.iteration(cam, scn.depth.cuda(), scn.color.cuda(), (pixs % te.n_window()).cuda(), opt)
+        grads[merge] = cam.grad.detach().clone()
+    assert float(grads[False].abs().sum()) > 0
+    assert torch.equal(grads[True], grads[False])

@@ -37,10 +37,11 @@ def main():
     dev = torch.device("cuda:0")
     scene = bench.Room0Scene(dev, 0, path="fused")
     tag = os.environ.get("NSLAM_FWD_PARTS", "auto") + " " + os.path.basename(os.environ.get("NSLAM_LIB", "libnslam.so"))
-    base = {"priority": False, "concurrent": True, "all_side": False, "lean_first": False}
+    base = {"priority": False, "concurrent": True, "all_side": False, "lean_first": False, "merge_frozen": None}
     for name, knobs in (("default", {}), ("priority", {"priority": True}), ("sequential", {"concurrent": False}),
                         ("all_side", {"all_side": True}), ("lean_first", {"lean_first": True}),
-                        ("side+lean", {"all_side": True, "lean_first": True}), ("default", {})):
+                        ("side+lean", {"all_side": True, "lean_first": True}), ("merged", {"merge_frozen": True}),
+                        ("default", {})):
         if len(sys.argv) > 1 and name not in sys.argv[1:]:
             continue
         knobs = {**base, **knobs}
