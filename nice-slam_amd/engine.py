@@ -198,8 +198,8 @@ class MappingEngine:
         pts_grad: also return d loss / d pts [N*S, 3] float64 (tracking, bundle adjustment): every
         decoder writes its share into its own buffer (so the branches stay independent) and the
         shares are summed afterwards.
-        on_branch(name): called on each decoder's stream right after its backward (the per-branch
-        Adam of the mapping iteration: its grid's rows depend on that branch alone)."""
+        on_branch(names): called on each launch's stream right after it, with the decoders it covered
+        (the per-branch Adam of the mapping iteration: a grid's rows depend on its branch alone)."""
         n = z.numel()
         self._clean = False
         concurrent = self.concurrent if concurrent is None else concurrent
@@ -263,8 +263,7 @@ class MappingEngine:
                                                                ptr(ws), wsb, st.cuda_stream)
                         check(rc, "nslam_query_bwd_decoder")
                     if on_branch is not None:
-                        for name in names:
-                            on_branch(name)
+                        on_branch(names)
                 if pts_grad and st is not main:
                     for name in names:
                         gp[decs.index(name)].record_stream(st)
@@ -378,10 +377,13 @@ class MappingEngine:
             # one rank: each decoder branch updates its own grid's rows (+ the trainable decoder's
             # parameters, after its slab reduction) on its own stream — the update of a grid needs
             # that branch's gradients alone, so no branch waits for the others before its Adam
-            def on_branch(name):
-                sub = {self.c[_GRID_OF[name]]: grads[self.c[_GRID_OF[name]]]} if _GRID_OF[name] in keys else {}
-                if name in dnames:
-                    sub[self.decs[name].param] = grads[self.decs[name].param]
+            def on_branch(names):  # the decoders of one launch: one Adam call for their grids
+                sub = {}
+                for name in names:
+                    if _GRID_OF[name] in keys:
+                        sub[self.c[_GRID_OF[name]]] = grads[self.c[_GRID_OF[name]]]
+                    if name in dnames:
+                        sub[self.decs[name].param] = grads[self.decs[name].param]
                 if sub:
                     optimizer.step(grads=sub, zero_grad=clean)
         self.query_bwd(stage, ro, rd, z, g_raw, keys, dnames, on_branch=on_branch)
