@@ -55,6 +55,7 @@ KERNEL_WORK = {
     "query_bwd.middle": (2 * 15479, 2048),
     # the frozen decoders' mask-only backward as one launch (ABI v10 nslam_query_bwd_decoders)
     "query_bwd.middle+fine": (2 * 15479 + 2 * 20599, 2 * 2048),
+    "query_bwd.color+middle+fine": (2 * 15479 + 2 * 20599 + 2 * 2 * 15575, 3 * 2048),
 }
 # rocprofv3 kernel names behind each span (for the PMC traffic of profiles/*traffic*.json)
 SPAN_KERNELS = {
@@ -62,7 +63,8 @@ SPAN_KERNELS = {
     "query_bwd.color": ("k_dec_bwd<3,", "k_slab_reduce"),
     "query_bwd.fine": ("k_dec_bwd<2,",),
     "query_bwd.middle": ("k_dec_bwd<1,",),
-    "query_bwd.middle+fine": ("k_dec_bwd_multi<false>",),
+    "query_bwd.middle+fine": ("k_dec_bwd_multi<false, false>",),
+    "query_bwd.color+middle+fine": ("k_dec_bwd_multi<false, true>", "k_slab_reduce"),
 }
 TRAFFIC_FILE = os.path.join(REPO, "profiles", "r02_traffic.json")
 

@@ -157,18 +157,18 @@ int nslam_query_bwd_decoder(const nslam_query_cfg* cfg, int32_t dec, int32_t acc
 size_t nslam_query_bwd_decoder_workspace_size(const nslam_query_cfg* cfg, int32_t dec, int64_t n_pts);
 size_t nslam_query_saved_size(int64_t n_pts);
 size_t nslam_query_tape_size(int64_t n_pts); /* ABI v9 */
-/* ABI v10: the mask-only backward of several frozen decoders in ONE launch — the share of
- * nslam_query_bwd_decoder of every decoder d in dec_mask (bit d), with their workgroups
- * interleaved over the grid, so decoders that would run as concurrent launches on separate
- * streams (tracking: middle, fine, colour; mapping: middle, fine) need no cross-stream fork / join.
- * Requires cfg->saved_masks (the forward's ReLU masks) and no parameter gradients for those
- * decoders (dgrad[d].base == NULL, else NSLAM_EUNSUPPORTED).  Grid gradients as
- * nslam_query_bwd_decoder; with cfg->need_pts_grad, g_pts[d] (a host array of 4 device pointers)
- * receives decoder d's d/dpts [M][3] float64 (written, not accumulated).  Replaces the per-decoder
- * loop of Tracker.optimize_cam_in_batch's backward (Tracker.py:125) / the frozen decoders' share of
- * Mapper.optimize_map's (Mapper.py:503). */
+/* ABI v10: the backward of several decoders in ONE launch — the share of nslam_query_bwd_decoder of
+ * every decoder d in dec_mask (bit d), their workgroups interleaved over the grid, so decoders
+ * that would run as concurrent launches on separate streams need no cross-stream fork / join.
+ * Requires cfg->saved_masks (the forward's ReLU masks).  Frozen decoders (dgrad[d].base == NULL):
+ * mask-only backward; with cfg->need_pts_grad, g_pts[d] (a host array of 4 device pointers)
+ * receives decoder d's d/dpts [M][3] float64 (written, not accumulated).  The colour decoder may
+ * also carry weight gradients (dgrad[COLOR].base, cfg->act_tape, no need_pts_grad,
+ * ws >= nslam_query_bwd_decoder_workspace_size(cfg, COLOR, M)); any other decoder with weight
+ * gradients is NSLAM_EUNSUPPORTED.  Replaces the per-decoder loop of Tracker.optimize_cam_in_batch's
+ * backward (Tracker.py:125) / Mapper.optimize_map's (Mapper.py:503). */
 int nslam_query_bwd_decoders(const nslam_query_cfg* cfg, int32_t dec_mask, const double* pts, int64_t n_pts,
-                             const float* g_raw, double* const* g_pts, void* stream);
+                             const float* g_raw, double* const* g_pts, void* ws, size_t ws_bytes, void* stream);
 
 /* ---- compositing: raw2outputs_nerf_color, src/common.py:204-245 (occupancy mode) ------------ */
 int nslam_composite_fwd(const float* raw, const double* z_vals, int64_t n_rays, int32_t n_samples,

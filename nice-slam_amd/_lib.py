@@ -146,7 +146,8 @@ def lib():
         L.nslam_query_bwd_workspace_size.argtypes = [ctypes.POINTER(NslamQueryCfg), i64]
         L.nslam_query_bwd_workspace_size.restype = sz
         L.nslam_query_bwd_decoder.argtypes = [ctypes.POINTER(NslamQueryCfg), i32, i32, vp, i64, vp, vp, vp, sz, vp]
-        L.nslam_query_bwd_decoders.argtypes = [ctypes.POINTER(NslamQueryCfg), i32, vp, i64, vp, ctypes.POINTER(vp), vp]
+        L.nslam_query_bwd_decoders.argtypes = [ctypes.POINTER(NslamQueryCfg), i32, vp, i64, vp, ctypes.POINTER(vp), vp,
+                                               sz, vp]
         L.nslam_query_bwd_decoder_workspace_size.argtypes = [ctypes.POINTER(NslamQueryCfg), i32, i64]
         L.nslam_query_bwd_decoder_workspace_size.restype = sz
         L.nslam_query_saved_size.argtypes = [i64]

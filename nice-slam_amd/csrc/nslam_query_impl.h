@@ -1534,9 +1534,13 @@ struct MultiDecArgs {
   int dec[4];
   double* gp[4];
 };
-template <bool PG>
-__global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd_multi(QueryKArgs a, MultiDecArgs m) {
-  constexpr int kScr = TILE_FLOATS + kWalkFloats;
+// CW: one of the parts is the colour decoder WITH its weight gradients (activation-tape backward,
+// one slab per wave folded per workgroup exactly as k_dec_bwd<COLOR, 1, .., SAVED>); the launch
+// then takes that kernel's registers and LDS for every part.
+template <bool PG, bool CW>
+__global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd_multi(QueryKArgs a, MultiDecArgs m,
+                                                                       float* __restrict__ slab, int acc_floats) {
+  constexpr int kScr = CW ? kScratchFloats + TILE_FLOATS : TILE_FLOATS + kWalkFloats;
   __shared__ __attribute__((aligned(16))) float lds[kWavesBwd * kScr];
   const int lane = threadIdx.x & 63, wave = wave_id();
   Scratch S;
@@ -1544,11 +1548,36 @@ __global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd_multi(QueryKArgs 
   S.sX = S.sD3 = S.gtab = S.xtab = S.cw = nullptr;
   S.crow = S.ccell = nullptr;
   const int part = (int)(blockIdx.x % (unsigned)m.ndec);
-  const int64_t w = (int64_t)(blockIdx.x / (unsigned)m.ndec) * kWavesBwd + wave;
-  if (w >= (a.n + 31) / 32) return;
+  // selects, not a dynamic index into the by-value argument (that would copy it to scratch)
+  const int dec = part == 0 ? m.dec[0] : part == 1 ? m.dec[1] : part == 2 ? m.dec[2] : m.dec[3];
+  double* gp = part == 0 ? m.gp[0] : part == 1 ? m.gp[1] : part == 2 ? m.gp[2] : m.gp[3];
+  const int64_t w0 = (int64_t)(blockIdx.x / (unsigned)m.ndec) * kWavesBwd;
+  const int64_t w = w0 + wave;
+  const int64_t ntiles = (a.n + 31) / 32;
+  if (CW && dec == NSLAM_DEC_COLOR && a.c.dgrad[NSLAM_DEC_COLOR].base) {
+    S.sX = S.sA + TILE_FLOATS;
+    S.gtab = S.sA + 2 * TILE_FLOATS;
+    S.xtab = S.gtab + 32 * 4;
+    S.crow = reinterpret_cast<int*>(S.xtab + 32 * 3);
+    S.cw = reinterpret_cast<float*>(S.crow + 32 * 8);
+    S.ccell = reinterpret_cast<int*>(S.cw + 32 * 8);
+    S.sD3 = reinterpret_cast<float*>(S.ccell + 32);
+    const Slab A = make_slab(slab + (size_t)w * acc_floats, acc_floats);
+    if (w < ntiles) dec_bwd_tile<NSLAM_DEC_COLOR, 1, false, true, true>(a, w, A, S, lane, nullptr);
+    __syncthreads();  // fold the workgroup's slabs into its first one (k_dec_bwd, WG == 1)
+    const int nv = (int)(ntiles - w0 < kWavesBwd ? ntiles - w0 : kWavesBwd);
+    f32x4* s0 = reinterpret_cast<f32x4*>(slab + (size_t)w0 * acc_floats);
+    const int q = acc_floats / 4;
+    for (int i = threadIdx.x; i < q; i += blockDim.x) {
+      f32x4 t = s0[i];
+      for (int v = 1; v < nv; ++v) t += s0[(size_t)v * q + i];
+      s0[i] = t;
+    }
+    return;
+  }
+  if (w >= ntiles) return;
   const Slab A = make_slab(nullptr, 0);
-  double* gp = m.gp[part];
-  switch (m.dec[part]) {
+  switch (dec) {
     case NSLAM_DEC_COARSE: dec_bwd_tile<NSLAM_DEC_COARSE, 0, PG, true, true>(a, w, A, S, lane, gp); break;
     case NSLAM_DEC_MIDDLE: dec_bwd_tile<NSLAM_DEC_MIDDLE, 0, PG, true, true>(a, w, A, S, lane, gp); break;
     case NSLAM_DEC_FINE: dec_bwd_tile<NSLAM_DEC_FINE, 0, PG, true, true>(a, w, A, S, lane, gp); break;

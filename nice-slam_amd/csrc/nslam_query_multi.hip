@@ -1,12 +1,13 @@
-// nslam_query_multi.hip — ABI v10 nslam_query_bwd_decoders: the mask-only backward of several
-// frozen decoders in one launch (k_dec_bwd_multi, nslam_query_impl.h).  Its own translation unit:
-// the kernel instantiates every decoder's backward tile.
+// nslam_query_multi.hip — ABI v10 nslam_query_bwd_decoders: the backward of several decoders in one
+// launch (k_dec_bwd_multi, nslam_query_impl.h).  Its own translation unit: the kernel instantiates
+// every decoder's backward tile.
 #include "nslam_query_impl.h"
 
 using namespace nslamq;
 
 extern "C" int nslam_query_bwd_decoders(const nslam_query_cfg* cfg, int32_t dec_mask, const double* pts,
-                                        int64_t n_pts, const float* g_raw, double* const* g_pts, void* stream) {
+                                        int64_t n_pts, const float* g_raw, double* const* g_pts, void* ws,
+                                        size_t ws_bytes, void* stream) {
   const int rc = check_cfg(cfg, true);
   if (rc) return rc;
   if (dec_mask <= 0 || dec_mask > 15) return NSLAM_EINVAL;
@@ -14,10 +15,16 @@ extern "C" int nslam_query_bwd_decoders(const nslam_query_cfg* cfg, int32_t dec_
   if (cfg->rays_o && (n_pts >= (int64_t(1) << 31) || n_pts % cfg->n_samples)) return NSLAM_EINVAL;
   if (cfg->need_pts_grad && n_pts > 0 && !g_pts) return NSLAM_EINVAL;
   MultiDecArgs m{};
+  bool cw = false;  // the colour decoder's weight gradients are part of the launch
   for (int d = 0; d < 4; ++d) {
     if (!((dec_mask >> d) & 1)) continue;
     if (!stage_uses(cfg->stage, d)) return NSLAM_EINVAL;
-    if (cfg->dgrad[d].base) return NSLAM_EUNSUPPORTED;  // weight gradients: nslam_query_bwd_decoder
+    if (cfg->dgrad[d].base) {
+      // only the colour decoder's activation-tape backward joins a merged launch
+      if (d != NSLAM_DEC_COLOR || cfg->need_pts_grad || !cfg->act_tape || cfg->dgrad[d].count <= 0)
+        return NSLAM_EUNSUPPORTED;
+      cw = true;
+    }
     if (cfg->need_pts_grad && n_pts > 0 && !g_pts[d]) return NSLAM_EINVAL;
     m.dec[m.ndec] = d;
     m.gp[m.ndec] = cfg->need_pts_grad ? g_pts[d] : nullptr;
@@ -25,13 +32,26 @@ extern "C" int nslam_query_bwd_decoders(const nslam_query_cfg* cfg, int32_t dec_
   }
   if (n_pts > 0 && !cfg->saved_masks) return NSLAM_EUNSUPPORTED;
   if (n_pts == 0) return NSLAM_OK;
+  const int64_t tiles = (n_pts + 31) / 32;
+  const int64_t groups = (tiles + kWavesBwd - 1) / kWavesBwd;
+  const nslam_dec_grad& dg = cfg->dgrad[NSLAM_DEC_COLOR];
+  const int acc = cw ? acc_floats_of(dg) : 0;
+  if (cw) {
+    if (tiles > max_slabs()) return NSLAM_EUNSUPPORTED;  // one slab per tile only
+    const size_t need = dec_ws_bytes(cfg, NSLAM_DEC_COLOR, n_pts);
+    if (!ws || ws_bytes < need) return NSLAM_EWORKSPACE;
+  }
   QueryKArgs a{*cfg, pts, n_pts, nullptr, g_raw, nullptr};
-  const int64_t groups = ((n_pts + 31) / 32 + kWavesBwd - 1) / kWavesBwd;
   const dim3 grid((unsigned)(groups * m.ndec)), block(64 * kWavesBwd);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (cfg->need_pts_grad)
-    hipLaunchKernelGGL(k_dec_bwd_multi<true>, grid, block, 0, s, a, m);
+  float* slab = reinterpret_cast<float*>(ws);
+  if (cw)
+    hipLaunchKernelGGL((k_dec_bwd_multi<false, true>), grid, block, 0, s, a, m, slab, acc);
+  else if (cfg->need_pts_grad)
+    hipLaunchKernelGGL((k_dec_bwd_multi<true, false>), grid, block, 0, s, a, m, nullptr, 0);
   else
-    hipLaunchKernelGGL(k_dec_bwd_multi<false>, grid, block, 0, s, a, m);
-  return hip_status();
+    hipLaunchKernelGGL((k_dec_bwd_multi<false, false>), grid, block, 0, s, a, m, nullptr, 0);
+  const int lrc = hip_status();
+  if (lrc || !cw) return lrc;
+  return slab_reduce(dg, slab, true, tiles, groups, acc, s);  // one folded slab per colour workgroup
 }

@@ -103,7 +103,8 @@ class MappingEngine:
         self.lean_first = False  # concurrent: enqueue the frozen decoders' branches before the weight-gradient one
         # frozen decoders' mask-only backward as one launch (ABI v10): None = when every decoder of
         # the stage is frozen (tracking: 0.199 -> 0.117 ms per iteration); with a weight-gradient
-        # branch beside them (mapping) two concurrent launches measured faster (200 vs 193 M/s)
+        # branch beside them (mapping) two concurrent launches measured faster (200 vs 193 M/s);
+        # "all": every decoder, the colour weight gradients included, in one launch (experiment)
         self.merge_frozen = None
         self._hi = None
         for k, v in c.items():
@@ -211,8 +212,12 @@ class MappingEngine:
         # launch (ABI v10 nslam_query_bwd_decoders) — no fork / join between their streams
         frozen = [d for d in decs if d not in dec_grads]
         merge = self.merge_frozen if self.merge_frozen is not None else len(frozen) == len(decs)
-        if merge and len(frozen) > 1 and self._saved is not None:
-            units = [[d] for d in decs if d in dec_grads] + [frozen]
+        wgt = [d for d in decs if d in dec_grads]
+        if (merge == "all" and self._saved is not None and not pts_grad and wgt == ["color"]
+                and self._tape is not None):
+            units = [list(decs)]  # every decoder, the colour weight gradients included: one launch
+        elif merge and len(frozen) > 1 and self._saved is not None:
+            units = [[d] for d in wgt] + [frozen]
         else:
             units = [[d] for d in decs]
         main = torch.cuda.current_stream(z.device)
@@ -248,9 +253,13 @@ class MappingEngine:
                             mask |= 1 << d
                             if pts_grad:
                                 gps[d] = ptr(gp[decs.index(name)])
+                        wsb = 0
+                        if "color" in names and "color" in dec_grads:
+                            wsb = lib().nslam_query_bwd_decoder_workspace_size(ctypes.byref(cfg), ops._DEC_ID["color"], n)
+                        ws = torch.empty(wsb, dtype=torch.uint8, device=z.device) if wsb else None
                         with ops._span("query_bwd." + "+".join(names)):
                             rc = lib().nslam_query_bwd_decoders(ctypes.byref(cfg), mask, None, n, ptr(g_raw), gps,
-                                                                st.cuda_stream)
+                                                                ptr(ws), wsb, st.cuda_stream)
                         check(rc, "nslam_query_bwd_decoders")
                     else:
                         name = names[0]
@@ -471,9 +480,11 @@ class TrackingEngine:
         ro, rd, gd, gc, keep = ops.gather_rays([(depth, color, c2w)], pix, n, self.H, self.W, self.window,
                                                fx, fy, cx, cy, self.bound)
         z = ops.sample_z(ro, rd, gd, self.bound, self.n_strat, self.n_surf)
-        raw = self.eng.query_fwd("color", ro, rd, z)
+        # the fine + middle occupancy sum is formed by the loss kernel as it reads raw (no combine pass)
+        raw = self.eng.query_fwd("color", ro, rd, z, defer_occ=True)
         _, _, _, ray_loss, g_raw = ops.render_loss(raw, z, gd, gc, keep, mode="tracker", use_color=self.use_color,
-                                                   handle_dynamic=self.handle_dynamic, w_color=self.w_color)
+                                                   handle_dynamic=self.handle_dynamic, w_color=self.w_color,
+                                                   occ_add=self.eng.occ_add)
         g_pts = self.eng.query_bwd("color", ro, rd, z, g_raw, (), (), pts_grad=True)
         if cam.grad is None:
             cam.grad = torch.empty_like(cam)

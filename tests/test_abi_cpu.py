@@ -146,7 +146,7 @@ def test_v10_bwd_decoders_validates_without_gpu(pkg):
     cfg = pkg._lib.NslamQueryCfg()
     cfg.stage = 7
     gps = (ctypes.c_void_p * 4)()
-    assert L.nslam_query_bwd_decoders(ctypes.byref(cfg), 0b0110, None, 10, None, gps, None) == -1  # bad stage
+    assert L.nslam_query_bwd_decoders(ctypes.byref(cfg), 0b0110, None, 10, None, gps, None, 0, None) == -1  # stage
     ok = pkg._lib.NslamQueryCfg()
-    rc = L.nslam_query_bwd_decoders(ctypes.byref(ok), 0, None, 0, None, gps, None)
+    rc = L.nslam_query_bwd_decoders(ctypes.byref(ok), 0, None, 0, None, gps, None, 0, None)
     assert rc < 0  # an empty decoder mask (or an otherwise incomplete config) is never launched

@@ -604,7 +604,7 @@ def test_merged_frozen_backward_matches_per_decoder_launches(tiny):
     keys = ("grid_middle", "grid_fine", "grid_color")
     pix = torch.randint(96 * 128, (3 * 150,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(21))
     out = {}
-    for merge in (False, True):
+    for merge in (False, True, "all"):  # "all": the colour weight-gradient backward joins the launch
         nice, c = _nice(sc)
         eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV)
         eng.merge_frozen = merge
@@ -619,10 +619,11 @@ def test_merged_frozen_backward_matches_per_decoder_launches(tiny):
 
         eng.iteration("color", frames, pix, 150, (96, 128), (sc.fx, sc.fy, sc.cx, sc.cy), opt, exchange=snapshot)
         out[merge] = gr
-    for k in keys:
-        assert float(out[False][k].abs().sum()) > 0, k
-        assert rel_l2(out[True][k], out[False][k]) < 1e-6, k
-    assert torch.equal(out[True]["dec"], out[False]["dec"])
+    for merge in (True, "all"):
+        for k in keys:
+            assert float(out[False][k].abs().sum()) > 0, k
+            assert rel_l2(out[merge][k], out[False][k]) < 1e-6, (merge, k)
+        assert torch.equal(out[merge]["dec"], out[False]["dec"]), merge
     # tracking: middle, fine and colour frozen, d/dpts per decoder
     scn = Scene(tiny)
     slam = scn.slam(base_cfg())

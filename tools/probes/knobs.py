@@ -40,7 +40,7 @@ def main():
     base = {"priority": False, "concurrent": True, "all_side": False, "lean_first": False, "merge_frozen": None}
     for name, knobs in (("default", {}), ("priority", {"priority": True}), ("sequential", {"concurrent": False}),
                         ("all_side", {"all_side": True}), ("lean_first", {"lean_first": True}),
-                        ("side+lean", {"all_side": True, "lean_first": True}), ("merged", {"merge_frozen": True}),
+                        ("side+lean", {"all_side": True, "lean_first": True}), ("merged", {"merge_frozen": True}), ("merged_all", {"merge_frozen": "all"}),
                         ("default", {})):
         if len(sys.argv) > 1 and name not in sys.argv[1:]:
             continue
