@@ -314,23 +314,45 @@ __global__ __launch_bounds__(256) void k_render_loss(LossArgs a) {
 }
 
 // Tracker handle_dynamic: thr = 10 * median(r over kept rays) (torch.median: lower median).
-// One workgroup: kept residuals into LDS (padded with +inf to a power of two), bitonic sort.
+// One workgroup: kept residuals into LDS; up to one per thread (tracking: 200 rays) the median is
+// selected by rank, else (or with a NaN) padded with +inf to a power of two and bitonic-sorted.
 constexpr int kMedianMax = 16384;
 
 __global__ __launch_bounds__(1024) void k_median_thr(const double* __restrict__ r, const uint8_t* __restrict__ keep,
                                                      int n, double* __restrict__ thr) {
   extern __shared__ double sv[];
-  __shared__ int cnt;
-  if (threadIdx.x == 0) cnt = 0;
+  __shared__ int cnt, nan_seen;
+  if (threadIdx.x == 0) cnt = nan_seen = 0;
   __syncthreads();
   int np2 = 1;
   while (np2 < n) np2 <<= 1;
   for (int i = threadIdx.x; i < np2; i += blockDim.x) sv[i] = INFINITY;
   __syncthreads();
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    if (!keep || keep[i]) sv[atomicAdd(&cnt, 1)] = r[i];
+    if (!keep || keep[i]) {
+      const double v = r[i];
+      if (v != v) nan_seen = 1;
+      sv[atomicAdd(&cnt, 1)] = v;
+    }
   }
   __syncthreads();
+  const int c = cnt;
+  if (c <= (int)blockDim.x && !nan_seen) {
+    // selection by rank (one value per thread, ties broken by slot): the value of rank (c-1)/2 is
+    // the lower median — the element the sort below would put there, without its log^2 passes
+    const int i = threadIdx.x;
+    if (i < c) {
+      const double x = sv[i];
+      int rank = 0;
+      for (int j = 0; j < c; ++j) {
+        const double y = sv[j];
+        rank += (y < x) || (y == x && j < i);
+      }
+      if (rank == (c - 1) / 2) *thr = 10.0 * x;
+    }
+    if (c == 0 && i == 0) *thr = INFINITY;
+    return;
+  }
   for (int k = 2; k <= np2; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
       for (int i = threadIdx.x; i < np2; i += blockDim.x) {

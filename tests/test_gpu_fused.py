@@ -128,15 +128,16 @@ def _autograd_loss(raw, z, gd, gc, keep, mode, use_color, handle_dynamic, w):
     return depth, var, color, loss.detach(), raw.grad
 
 
-@pytest.mark.parametrize("mode,use_color,hd", [("mapper", True, False), ("mapper", False, False),
-                                               ("tracker", True, True), ("tracker", False, True),
-                                               ("tracker", True, False)])
-def test_render_loss_matches_autograd(tiny, mode, use_color, hd):
+# n_per 100 (300 rays): the median by rank selection; 400 (1200 rays > 1024 threads): the bitonic sort
+@pytest.mark.parametrize("mode,use_color,hd,n_per", [("mapper", True, False, 100), ("mapper", False, False, 100),
+                                                     ("tracker", True, True, 100), ("tracker", False, True, 100),
+                                                     ("tracker", True, False, 100), ("tracker", True, True, 400)])
+def test_render_loss_matches_autograd(tiny, mode, use_color, hd, n_per):
     sc, frames = _frames(tiny)
     nice, c = _nice(sc)
-    pix = torch.randint(96 * 128, (3 * 100,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(4))
-    ro, rd, gd, gc, keep = P.ops.gather_rays(frames, pix, 100, 96, 128, (0, 96, 0, 128), sc.fx, sc.fy, sc.cx, sc.cy,
-                                             sc.bound)
+    pix = torch.randint(96 * 128, (3 * n_per,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(4))
+    ro, rd, gd, gc, keep = P.ops.gather_rays(frames, pix, n_per, 96, 128, (0, 96, 0, 128), sc.fx, sc.fy, sc.cx,
+                                             sc.cy, sc.bound)
     z = P.ops.sample_z(ro, rd, gd, sc.bound, 32, 16)
     pts = ro[:, None, :] + rd[:, None, :] * z[:, :, None]
     with torch.no_grad():
