@@ -165,8 +165,11 @@ size_t nslam_query_tape_size(int64_t n_pts); /* ABI v9 */
  * receives decoder d's d/dpts [M][3] float64 (written, not accumulated).  The colour decoder may
  * also carry weight gradients (dgrad[COLOR].base, cfg->act_tape, no need_pts_grad,
  * ws >= nslam_query_bwd_decoder_workspace_size(cfg, COLOR, M)); any other decoder with weight
- * gradients is NSLAM_EUNSUPPORTED.  Replaces the per-decoder loop of Tracker.optimize_cam_in_batch's
- * backward (Tracker.py:125) / Mapper.optimize_map's (Mapper.py:503). */
+ * gradients is NSLAM_EUNSUPPORTED.  dec_mask | NSLAM_BWD_SUM_PTS (frozen decoders, need_pts_grad):
+ * g_pts[0] receives the SUM of the decoders' d/dpts, added in decoder order ((middle + fine) +
+ * colour: the order of summing the per-decoder buffers).  Replaces the per-decoder loop of
+ * Tracker.optimize_cam_in_batch's backward (Tracker.py:125) / Mapper.optimize_map's (Mapper.py:503). */
+#define NSLAM_BWD_SUM_PTS 0x100
 int nslam_query_bwd_decoders(const nslam_query_cfg* cfg, int32_t dec_mask, const double* pts, int64_t n_pts,
                              const float* g_raw, double* const* g_pts, void* ws, size_t ws_bytes, void* stream);
 

@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("NSLAM_LIB") or os.path.join(_HERE, "libnslam.so")  # 
 
 NSLAM_OK = 0
 ABI_VERSION = 10
+BWD_SUM_PTS = 0x100  # nslam.h NSLAM_BWD_SUM_PTS (nslam_query_bwd_decoders)
 STAGES = {"coarse": 0, "middle": 1, "fine": 2, "color": 3}
 DEC_COARSE, DEC_MIDDLE, DEC_FINE, DEC_COLOR = 0, 1, 2, 3
 

@@ -1367,7 +1367,8 @@ constexpr int kMaxSlabs = 4096;  // WG == 2 above this many tiles
 
 template <int DEC, int WG, bool PG, bool FIRST, bool SAVED>
 __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, const Slab& A, const Scratch& S,
-                                             int lane, double* __restrict__ gpts) {
+                                             int lane, double* __restrict__ gpts, int64_t gbase = 0) {
+  // gpts: d/dpts of point idx at gpts[(idx - gbase) * 3 + k] (gbase: a tile's LDS staging rows)
   // Every scratch / slab address is a function of the lane only, i.e. invariant across the tile
   // loop; letting LICM hoist the ~300 of them pins (and spills) the register file.  Re-derive
   // them per tile.
@@ -1462,7 +1463,8 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
     coord_grad(gr, cr, dc, lane, gp);
     if (h == 0 && q.valid) {
 #pragma unroll
-      for (int k = 0; k < 3; ++k) gpts[idx * 3 + k] = FIRST ? gp[k] : gpts[idx * 3 + k] + gp[k];
+      for (int k = 0; k < 3; ++k)
+        gpts[(idx - gbase) * 3 + k] = FIRST ? gp[k] : gpts[(idx - gbase) * 3 + k] + gp[k];
     }
   }
   PHASE(DEC, 14);
@@ -1582,6 +1584,46 @@ __global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd_multi(QueryKArgs 
     case NSLAM_DEC_MIDDLE: dec_bwd_tile<NSLAM_DEC_MIDDLE, 0, PG, true, true>(a, w, A, S, lane, gp); break;
     case NSLAM_DEC_FINE: dec_bwd_tile<NSLAM_DEC_FINE, 0, PG, true, true>(a, w, A, S, lane, gp); break;
     default: dec_bwd_tile<NSLAM_DEC_COLOR, 0, PG, true, true>(a, w, A, S, lane, gp); break;
+  }
+}
+
+// Mask-only backward of several frozen decoders with their d/dpts SUMMED (ABI v10,
+// NSLAM_BWD_SUM_PTS): one workgroup per tile, wave i evaluates decoder part i and stages its
+// d/dpts in LDS; after a barrier the parts are added in decoder order ((middle + fine) + colour,
+// the order of the per-decoder buffers' sum) and written once — no separate add kernels.
+template <bool PG_UNUSED = true>
+__global__ __launch_bounds__(256, 2) void k_dec_bwd_multi_sum(QueryKArgs a, MultiDecArgs m, double* __restrict__ out) {
+  constexpr int kScr = TILE_FLOATS + kWalkFloats;
+  __shared__ __attribute__((aligned(16))) float lds[4 * kScr];
+  __shared__ double stage[4][32 * 3];
+  const int lane = threadIdx.x & 63, part = wave_id();
+  const int64_t tile = blockIdx.x;
+  Scratch S;
+  S.sA = lds + part * kScr;
+  S.sX = S.sD3 = S.gtab = S.xtab = S.cw = nullptr;
+  S.crow = S.ccell = nullptr;
+  for (int i = lane; i < 96; i += 64) stage[part][i] = 0.0;
+  __syncthreads();
+  const int dec = part == 0 ? m.dec[0] : part == 1 ? m.dec[1] : part == 2 ? m.dec[2] : m.dec[3];
+  const Slab A = make_slab(nullptr, 0);
+  double* st = &stage[part][0];
+  const int64_t gb = tile * 32;
+  switch (dec) {
+    case NSLAM_DEC_COARSE: dec_bwd_tile<NSLAM_DEC_COARSE, 0, true, true, true>(a, tile, A, S, lane, st, gb); break;
+    case NSLAM_DEC_MIDDLE: dec_bwd_tile<NSLAM_DEC_MIDDLE, 0, true, true, true>(a, tile, A, S, lane, st, gb); break;
+    case NSLAM_DEC_FINE: dec_bwd_tile<NSLAM_DEC_FINE, 0, true, true, true>(a, tile, A, S, lane, st, gb); break;
+    default: dec_bwd_tile<NSLAM_DEC_COLOR, 0, true, true, true>(a, tile, A, S, lane, st, gb); break;
+  }
+  __syncthreads();
+  if (part == 0) {
+    for (int i = lane; i < 96; i += 64) {
+      const int64_t idx = gb + i / 3;
+      if (idx < a.n) {
+        double v = stage[0][i];
+        for (int d = 1; d < m.ndec; ++d) v = v + stage[d][i];
+        out[gb * 3 + i] = v;
+      }
+    }
   }
 }
 

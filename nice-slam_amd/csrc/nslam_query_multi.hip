@@ -10,7 +10,10 @@ extern "C" int nslam_query_bwd_decoders(const nslam_query_cfg* cfg, int32_t dec_
                                         size_t ws_bytes, void* stream) {
   const int rc = check_cfg(cfg, true);
   if (rc) return rc;
+  const bool sum_pts = (dec_mask & NSLAM_BWD_SUM_PTS) != 0;
+  dec_mask &= ~NSLAM_BWD_SUM_PTS;
   if (dec_mask <= 0 || dec_mask > 15) return NSLAM_EINVAL;
+  if (sum_pts && (!cfg->need_pts_grad || (n_pts > 0 && (!g_pts || !g_pts[0])))) return NSLAM_EINVAL;
   if (n_pts < 0 || (n_pts > 0 && ((!pts && !cfg->rays_o) || !g_raw))) return NSLAM_EINVAL;
   if (cfg->rays_o && (n_pts >= (int64_t(1) << 31) || n_pts % cfg->n_samples)) return NSLAM_EINVAL;
   if (cfg->need_pts_grad && n_pts > 0 && !g_pts) return NSLAM_EINVAL;
@@ -25,9 +28,9 @@ extern "C" int nslam_query_bwd_decoders(const nslam_query_cfg* cfg, int32_t dec_
         return NSLAM_EUNSUPPORTED;
       cw = true;
     }
-    if (cfg->need_pts_grad && n_pts > 0 && !g_pts[d]) return NSLAM_EINVAL;
+    if (cfg->need_pts_grad && n_pts > 0 && !sum_pts && !g_pts[d]) return NSLAM_EINVAL;
     m.dec[m.ndec] = d;
-    m.gp[m.ndec] = cfg->need_pts_grad ? g_pts[d] : nullptr;
+    m.gp[m.ndec] = cfg->need_pts_grad && !sum_pts ? g_pts[d] : nullptr;
     ++m.ndec;
   }
   if (n_pts > 0 && !cfg->saved_masks) return NSLAM_EUNSUPPORTED;
@@ -42,8 +45,13 @@ extern "C" int nslam_query_bwd_decoders(const nslam_query_cfg* cfg, int32_t dec_
     if (!ws || ws_bytes < need) return NSLAM_EWORKSPACE;
   }
   QueryKArgs a{*cfg, pts, n_pts, nullptr, g_raw, nullptr};
-  const dim3 grid((unsigned)(groups * m.ndec)), block(64 * kWavesBwd);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (sum_pts) {  // one workgroup per tile, one wave per decoder, d/dpts summed in decoder order
+    if (cw) return NSLAM_EUNSUPPORTED;
+    hipLaunchKernelGGL(k_dec_bwd_multi_sum<>, dim3((unsigned)tiles), dim3(64 * m.ndec), 0, s, a, m, g_pts[0]);
+    return hip_status();
+  }
+  const dim3 grid((unsigned)(groups * m.ndec)), block(64 * kWavesBwd);
   float* slab = reinterpret_cast<float*>(ws);
   if (cw)
     hipLaunchKernelGGL((k_dec_bwd_multi<false, true>), grid, block, 0, s, a, m, slab, acc);

@@ -106,6 +106,7 @@ class MappingEngine:
         # branch beside them (mapping) two concurrent launches measured faster (200 vs 193 M/s);
         # "all": every decoder, the colour weight gradients included, in one launch (experiment)
         self.merge_frozen = None
+        self.sum_pts = True  # merged d/dpts: summed inside the launch (NSLAM_BWD_SUM_PTS)
         self._hi = None
         for k, v in c.items():
             if not v.is_contiguous(memory_format=torch.channels_last_3d):
@@ -233,6 +234,7 @@ class MappingEngine:
                 streams = [self._side[len(units) - 1]]
             streams += self._side[:len(units) - 1]
         used = [st for st in streams if st is not main]
+        summed = False
         with ops._span("query_bwd"):
             for st in used:  # fork: every branch starts from the same point of the main stream
                 st.wait_stream(main)
@@ -253,6 +255,12 @@ class MappingEngine:
                             mask |= 1 << d
                             if pts_grad:
                                 gps[d] = ptr(gp[decs.index(name)])
+                        if pts_grad and names == decs and self.sum_pts:
+                            # every decoder in this launch: their d/dpts summed in the kernel, in decoder
+                            # order (what the loop below would add), into the first buffer
+                            mask |= _lib.BWD_SUM_PTS
+                            gps[0] = ptr(gp[0])
+                            summed = True
                         wsb = 0
                         if "color" in names and "color" in dec_grads:
                             wsb = lib().nslam_query_bwd_decoder_workspace_size(ctypes.byref(cfg), ops._DEC_ID["color"], n)
@@ -278,6 +286,8 @@ class MappingEngine:
                         gp[decs.index(name)].record_stream(st)
             for st in used:
                 main.wait_stream(st)
+        if pts_grad and summed:
+            return gp[0]
         if pts_grad:
             out = gp[0]
             for g in gp[1:]:

@@ -631,14 +631,16 @@ def test_merged_frozen_backward_matches_per_decoder_launches(tiny):
     cam0 = P.common.get_tensor_from_camera(scn.c2w).cuda()
     pixs = torch.randint(400, (200,), generator=torch.Generator().manual_seed(5))
     grads = {}
-    for merge in (False, True):
+    for merge in (False, True, "nosum"):  # "nosum": merged launch, per-decoder d/dpts buffers added in torch
         te = P.engine.TrackingEngine(copy.deepcopy(slam.shared_decoders), slam.shared_c, scn.bound, 32, 16,
                                      (scn.H, scn.W), (scn.fx, scn.fy, scn.cx, scn.cy), ignore_edge=(20, 20),
                                      w_color=0.5, handle_dynamic=True, use_color=True, device=DEV)
-        te.eng.merge_frozen = merge  # (the default, None, merges here: every tracking decoder is frozen)
+        te.eng.merge_frozen = bool(merge)  # (the default, None, merges here: every tracking decoder is frozen)
+        te.eng.sum_pts = merge is True  # in-kernel sum of the decoders' d/dpts (NSLAM_BWD_SUM_PTS)
         cam = cam0.clone().requires_grad_(True)
         opt = P.ops.FusedAdam([{"params": [cam], "lr": 0.0}])
         te.iteration(cam, scn.depth.cuda(), scn.color.cuda(), (pixs % te.n_window()).cuda(), opt)
         grads[merge] = cam.grad.detach().clone()
     assert float(grads[False].abs().sum()) > 0
     assert torch.equal(grads[True], grads[False])
+    assert torch.equal(grads["nosum"], grads[False])
