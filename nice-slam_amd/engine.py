@@ -106,7 +106,9 @@ class MappingEngine:
         # branch beside them (mapping) two concurrent launches measured faster (200 vs 193 M/s);
         # "all": every decoder, the colour weight gradients included, in one launch (experiment)
         self.merge_frozen = None
-        self.sum_pts = True  # merged d/dpts: summed inside the launch (NSLAM_BWD_SUM_PTS)
+        # merged d/dpts summed inside the launch (NSLAM_BWD_SUM_PTS, one workgroup per tile): measured
+        # 0.109 vs 0.102 ms per tracking iteration for per-decoder buffers + two adds — kept off
+        self.sum_pts = False
         self._hi = None
         for k, v in c.items():
             if not v.is_contiguous(memory_format=torch.channels_last_3d):
