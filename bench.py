@@ -532,7 +532,7 @@ def kernel_roofline(name, avg_ms, pts):
                             "profiles/r02_traffic.json"}
 
 
-def room0_frame_rate(scene, reps=20):
+def room0_frame_rate(scene, reps=100):
     """frames/s on Replica room0 (BASELINE metric) from measured iteration times:
     per frame 10 tracking iterations × 200 pixels (replica.yaml tracking, edges 100 px) and 12
     mapping iterations × 1000 pixels (60 iterations every 5 frames, stage split middle 25 / fine 12
