@@ -114,19 +114,23 @@ class Mapper(object):
         return frustum_mask(c2w, key, val_shape, depth, self.bound, self.H, self.W, self.fx, self.fy, self.cx,
                             self.cy)
 
-    def keyframe_selection_overlap(self, gt_color, gt_depth, c2w, keyframe_dict, k, N_samples=16, pixels=100):
-        """Mapper.py:166-228: keyframes whose frustum sees the current frame's surface samples."""
+    def keyframe_overlap_scores(self, gt_color, gt_depth, c2w, keyframe_dict, N_samples=16, pixels=100):
+        """Mapper.py:185-221: per keyframe, the fraction of the current frame's near-surface samples
+        (100 pixels × 16 depths in [0.8·d, d + 0.5]) that project inside it (20-px margin, in front
+        of the camera).  One host sync for all keyframes (the reference's loop is host numpy)."""
         dev = self.device
         H, W, fx, fy, cx, cy = self.H, self.W, self.fx, self.fy, self.cx, self.cy
         rays_o, rays_d, gd, _ = get_samples(0, H, 0, W, pixels, H, W, fx, fy, cx, cy, c2w, gt_depth, gt_color, dev,
                                             generator=self.generator)
+        if not keyframe_dict:
+            return []
         gd = gd.reshape(-1, 1).repeat(1, N_samples)
         t = torch.linspace(0.0, 1.0, N_samples, device=dev)
         z = gd * 0.8 * (1.0 - t) + (gd + 0.5) * t
         verts = (rays_o[..., None, :] + rays_d[..., None, :] * z[..., :, None]).reshape(-1, 3)
         K = torch.tensor([[fx, 0.0, cx], [0.0, fy, cy], [0.0, 0.0, 1.0]], dtype=torch.float64, device=dev)
-        scores = []
-        for kid, kf in enumerate(keyframe_dict):
+        counts = []
+        for kf in keyframe_dict:
             w2c = torch.linalg.inv(kf["est_c2w"].to(dev).float())
             cam = (verts @ w2c[:3, :3].T + w2c[:3, 3]).double()
             cam[:, 0] *= -1
@@ -135,9 +139,18 @@ class Mapper(object):
             uv = (uvz[:, :2] / zz[:, None]).float()
             edge = 20
             m = (uv[:, 0] < W - edge) & (uv[:, 0] > edge) & (uv[:, 1] < H - edge) & (uv[:, 1] > edge) & (zz < 0)
-            scores.append((kid, float(m.float().mean())))
-        scores.sort(key=lambda s: s[1], reverse=True)
-        sel = [kid for kid, s in scores if s > 0.0]
+            counts.append(m.sum())
+        n = verts.shape[0]
+        # mask.sum() / uv.shape[0] as the reference divides: an integer count over the sample count
+        return [int(cnt) / n for cnt in torch.stack(counts).cpu()]
+
+    def keyframe_selection_overlap(self, gt_color, gt_depth, c2w, keyframe_dict, k, N_samples=16, pixels=100):
+        """Mapper.py:166-228: keyframes whose frustum sees the current frame's surface samples,
+        ranked by overlap (stable sort, as `sorted`), then a random permutation (numpy RNG) of the
+        ones with any overlap, truncated to k."""
+        scores = self.keyframe_overlap_scores(gt_color, gt_depth, c2w, keyframe_dict, N_samples, pixels)
+        ranked = sorted(enumerate(scores), key=lambda s: s[1], reverse=True)
+        sel = [kid for kid, s in ranked if s > 0.0]
         return list(np.random.permutation(np.array(sel))[:k])
 
     # ------------------------------------------------------------------------------------------

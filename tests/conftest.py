@@ -32,6 +32,35 @@ def tiny():
 
 
 @pytest.fixture(scope="session")
+def loop():
+    """tests/golden/loop_fixtures.npz: loop-level vectors from the reference's own Tracker / Mapper
+    code (tests/golden/make_golden_loop.py)."""
+    with np.load(os.path.join(GOLDEN, "loop_fixtures.npz")) as z:
+        return {k: z[k] for k in z.files}
+
+
+class FixedPixels:
+    """Replaces common.select_uv (src/common.py:92-107): pre-drawn flat pixel indices from a seeded
+    CPU generator, in call order — the draws tests/golden/make_golden_loop.py's FixedDraws made."""
+
+    def __init__(self, seed=11):
+        import torch
+        self.g = torch.Generator().manual_seed(seed)
+        self.log = []
+
+    def draw(self, n_total, n):
+        import torch
+        idx = torch.randint(n_total, (n,), generator=self.g)
+        self.log.append(idx)
+        return idx
+
+    def __call__(self, i, j, n, depth, color, device="cuda:0", generator=None):
+        i, j = i.reshape(-1), j.reshape(-1)
+        idx = self.draw(i.shape[0], n).to(i.device)
+        return i[idx], j[idx], depth.reshape(-1)[idx], color.reshape(-1, 3)[idx]
+
+
+@pytest.fixture(scope="session")
 def room0():
     with np.load(os.path.join(GOLDEN, "room0_color.npz")) as z:
         return {k: z[k] for k in z.files}

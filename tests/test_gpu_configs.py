@@ -1,0 +1,328 @@
+"""The BASELINE.json configurations run through the FUSED mapping engine (the bench's path) and
+compared elementwise with the oracle on the same inputs:
+
+  configs[2] ScanNet scene0000: 5000 pixels × 48 samples over a 5-frame window, colour stage,
+             frustum-compacted grid gradients (MappingEngine.iteration) — and bundle adjustment
+             with a 5-frame window through the Mapper drop-in (4 cameras optimised, the oldest
+             fixed, Mapper.py:346-363,420-421,521-540).
+  configs[3] Apartment: the coarse mapper's iteration (Mapper.py:403-404,482-484: stage 'coarse',
+             no gt depth in the sampler, 32 samples, coarse grid gradients).
+  configs[4] synthetic stress: fine / colour grids 512³×32 (16 GiB each), middle 256³, 65536
+             pixels × 64 samples (48 stratified + 16 surface), colour stage.  The oracle runs on
+             the DEVICE here (the same torch ops; 34 GiB of grids do not belong in host RAM), as
+             the checker only.
+
+Tolerances are the reference's fp32 noise floor (tests/test_gpu_parity.py):
+forward max-abs 2e-4; gradients rel-L2 5e-3 middle grid, 1e-3 fine grid, 2e-4 colour / coarse
+grid and decoder weights.  The losses are L1: a ray whose depth residual is within fp32 noise of
+zero may flip its sign, which the rel-L2 bound absorbs.
+"""
+import importlib
+import json
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, FixedPixels, rel_l2
+from oracle import nslam_oracle as orc
+
+sys.path.insert(0, GOLDEN)
+import scenes  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+P = importlib.import_module("nice-slam_amd")
+DEV = torch.device("cuda:0")
+LENS = {"coarse": 2.0, "middle": 0.32, "fine": 0.16, "color": 0.16}   # configs/nice_slam.yaml:7-12
+# configs/ScanNet/scannet.yaml cam after crop_edge 10 (NICE_SLAM.update_cam)
+SCANNET_CAM = dict(H=460, W=620, fx=577.590698, fy=578.729797, cx=308.905426, cy=232.683609)
+APARTMENT_CAM = dict(H=720, W=1280, fx=607.4694213867188, fy=607.4534912109375, cx=636.9967041015625,
+                     cy=369.2689514160156)
+TOL = {"grid_coarse": 2e-4, "grid_middle": 5e-3, "grid_fine": 1e-3, "grid_color": 2e-4, "decoder": 2e-4}
+
+
+def build_scene(bound_cfg, cam, n_frames, seed, coarse=False, lens=LENS, div=0.32, device_grids=False):
+    bound = orc.enlarge_bound(bound_cfg, div)
+    gen = torch.Generator().manual_seed(seed)
+    if device_grids:
+        gd = torch.Generator(device=DEV).manual_seed(seed)
+        grids = {}
+        for k, std in (("middle", 0.01), ("fine", 1e-4), ("color", 0.01)):
+            shp = orc.grid_shape(bound, lens[k])
+            t = torch.empty(1, shp[2], shp[3], shp[4], 32, device=DEV).normal_(0.0, std, generator=gd)
+            grids["grid_" + k] = t.permute(0, 4, 1, 2, 3)
+    else:
+        grids = orc.make_grids(bound, lens, coarse=coarse, gen=gen)
+    sd = orc.init_decoders(gen, coarse=coarse)
+    b = bound.numpy()
+    ctr = b.mean(1)
+    frames = []
+    for f in range(n_frames):
+        c2w = scenes.look_pose(ctr, 0.4 * f + 0.2, 0.25 * ((f % 3) - 1), (0.3 * (f - 1), -0.2 * (f % 2), 0.1))
+        depth = scenes.box_depth(c2w, cam, b, seed=seed * 10 + f)
+        color = scenes.color_image(cam, seed=seed * 10 + 5 + f)
+        frames.append((torch.from_numpy(depth), torch.from_numpy(color), torch.from_numpy(c2w)))
+    return bound, grids, sd, frames
+
+
+def product_nice(sd, bound, coarse=False):
+    nice = P.NICE(c_dim=32, coarse=coarse, coarse_grid_len=2.0, middle_grid_len=0.32, fine_grid_len=0.16,
+                  color_grid_len=0.16)
+    nice.load_state_dict({k: v.clone() for k, v in sd.items()})
+    nice.set_bound(bound)
+    return nice.to(DEV)
+
+
+def oracle_batch(frames, pix, n_per, cam, bound, dev="cpu"):
+    """get_samples over the window with the given select_uv indices + the inside-mask (oracle)."""
+    ro_l, rd_l, gd_l, gc_l = [], [], [], []
+    W = cam["W"]
+    for f, (d, c, m) in enumerate(frames):
+        idx = pix[f * n_per:(f + 1) * n_per].to(dev)
+        i, j = (idx % W).float(), (idx // W).float()
+        ro, rd = orc.rays_from_uv(i, j, m.to(dev), cam["fx"], cam["fy"], cam["cx"], cam["cy"])
+        ro_l.append(ro)
+        rd_l.append(rd)
+        gd_l.append(d.to(dev).reshape(-1)[idx])
+        gc_l.append(c.to(dev).reshape(-1, 3)[idx])
+    ro, rd, gd, gc = (torch.cat(x) for x in (ro_l, rd_l, gd_l, gc_l))
+    keep = orc.inside_mask(ro, rd, gd, bound.to(dev))
+    return ro[keep].contiguous(), rd[keep].contiguous(), gd[keep], gc[keep], keep
+
+
+def run_engine(nice, grids_dev, bound, frames_dev, pix, n_per, cam, stage, rows, n_strat, n_surf, trainable):
+    eng = P.engine.MappingEngine(nice, grids_dev, bound, n_strat, n_surf, device=DEV, rows=rows)
+    keys, dn = eng.grads_for(stage, trainable)
+    groups = [{"params": [eng.decs[n].param], "lr": 0.0} for n in dn]
+    groups += [{"params": [grids_dev[k]], "lr": 0.0, **({"rows": rows[k]} if rows and k in rows else {})} for k in keys]
+    opt = P.ops.FusedAdam(groups)
+    snap = {}
+
+    def exchange(ks, dns):  # after the backward, before Adam (where the ray-sharded exchange runs)
+        for k in ks:
+            snap[k] = eng.ggrad[k].detach().clone()
+        for n in dns:
+            snap["dec." + n] = eng.decs[n].grad.detach().clone()
+
+    ray_loss, keep = eng.iteration(stage, frames_dev, pix.to(DEV), n_per, (cam["H"], cam["W"]),
+                                   (cam["fx"], cam["fy"], cam["cx"], cam["cy"]), opt, trainable_decoders=trainable,
+                                   use_gt_in_sampler=stage != "coarse", exchange=exchange)
+    torch.cuda.synchronize()
+    return eng, snap, ray_loss, keep
+
+
+def oracle_step(sd, grids, ro, rd, gd, gc, stage, bound, n_strat, n_surf, trainable, coarse_bound=None):
+    sdg = {k: (v.clone().requires_grad_(True) if any(k.startswith(t + "_decoder.") for t in trainable) else v)
+           for k, v in sd.items()}
+    keys = {"coarse": ["grid_coarse"], "middle": ["grid_middle"], "fine": ["grid_middle", "grid_fine"],
+            "color": ["grid_middle", "grid_fine", "grid_color"]}[stage]
+    gl = {k: (v.detach().requires_grad_(True) if k in keys else v) for k, v in grids.items()}
+    z_gt = None if stage == "coarse" else gd
+    d, v, c = orc.render_batch_ray(sdg, gl, rd, ro, stage, bound.to(ro.device), z_gt, n_strat=n_strat, n_surf=n_surf,
+                                   coarse_bound=coarse_bound)
+    loss = orc.mapper_loss(d, c, gd, gc, stage)
+    loss.backward()
+    grads = {k: gl[k].grad for k in keys}
+    dec = {k: sdg[k].grad for k in sdg if sdg[k].requires_grad}
+    return float(loss), grads, dec, (d.detach(), c.detach())
+
+
+def compact(g_dense, rows):
+    return g_dense.permute(0, 2, 3, 4, 1).reshape(-1, 32)[rows.long().to(g_dense.device)]
+
+
+def decoder_flat(nice, name, dec_grads):
+    """Oracle decoder gradients in the product's flat (named_parameters) order."""
+    pre = name + "_decoder."
+    return torch.cat([dec_grads[pre + n].reshape(-1).to(DEV) for n, _ in nice.decoder(name).named_parameters()])
+
+
+def frustum_rows(frames, grids, bound, cam):
+    depth, _, c2w = frames[-1]   # the current frame selects the optimised voxels (Mapper.py:314-333)
+    rows = {}
+    for k, v in grids.items():
+        m = P.mapper.frustum_mask(c2w.to(DEV), k, v.shape[2:], depth.to(DEV), bound, cam["H"], cam["W"], cam["fx"],
+                                  cam["fy"], cam["cx"], cam["cy"])
+        rows[k] = P.engine.frustum_rows(m)
+    return rows
+
+
+def check(report, name, got, ref, tol):
+    report[name] = rel_l2(got, ref)
+    return report[name] <= tol
+
+
+# ------------------------------------------------------------------------------------------------
+def test_scene0000_color_iteration_5000_rays():
+    """configs[2] shapes: one colour-stage engine iteration, 5 frames × 1000 pixels × 48 samples."""
+    cam = SCANNET_CAM
+    bound, grids, sd, frames = build_scene([[-2.0, 11.0], [-2.0, 11.5], [-2.0, 5.5]], cam, 5, seed=61)
+    assert [list(grids[k].shape) for k in ("grid_middle", "grid_fine")] == [[1, 32, 23, 42, 40], [1, 32, 47, 85, 81]]
+    n_per = 1000
+    pix = torch.randint(cam["H"] * cam["W"], (5 * n_per,), generator=torch.Generator().manual_seed(62))
+    nice = product_nice(sd, bound)
+    gdev = {k: v.to(DEV).contiguous(memory_format=torch.channels_last_3d) for k, v in grids.items()}
+    fdev = [(d.to(DEV), c.to(DEV), m.to(DEV)) for d, c, m in frames]
+    rows = frustum_rows(frames, gdev, bound, cam)
+    eng, snap, ray_loss, keep = run_engine(nice, gdev, bound, fdev, pix, n_per, cam, "color", rows, 32, 16, ("color",))
+    ro, rd, gd, gc, k_ref = oracle_batch(frames, pix, n_per, cam, bound)
+    assert torch.equal(keep.bool().cpu(), k_ref)
+    assert ro.shape[0] > 4000
+    loss, g, dec, _ = oracle_step(sd, grids, ro, rd, gd, gc, "color", bound, 32, 16, ("color",))
+    report = {"loss_rel": abs(float(ray_loss.sum()) - loss) / loss, "rays": int(ro.shape[0])}
+    ok = report["loss_rel"] < 1e-5
+    for k in ("grid_middle", "grid_fine", "grid_color"):
+        assert snap[k].shape[0] == rows[k].numel()
+        ok &= check(report, k, snap[k], compact(g[k], rows[k]), TOL[k])
+    ok &= check(report, "color_decoder", snap["dec.color"], decoder_flat(nice, "color", dec), TOL["decoder"])
+    print(json.dumps(report, indent=1))
+    assert ok, report
+
+
+def test_apartment_coarse_iteration():
+    """configs[3]: the coarse mapper's iteration on the fused engine (stage 'coarse', gt_depth=None
+    in the sampler so 32 stratified samples, loss on depth only, coarse grid gradients; the
+    coarse decoder reads the grid over the ×2 bound, NICE_SLAM.py:152-157)."""
+    cam = APARTMENT_CAM
+    bound, grids, sd, frames = build_scene([[-5.8, 11.3], [-4.0, 4.5], [-7.9, 4.9]], cam, 3, seed=71, coarse=True)
+    assert list(grids["grid_coarse"].shape) == [1, 32, 13, 8, 17]
+    n_per = 1000
+    pix = torch.randint(cam["H"] * cam["W"], (3 * n_per,), generator=torch.Generator().manual_seed(72))
+    nice = product_nice(sd, bound, coarse=True)
+    gdev = {k: v.to(DEV).contiguous(memory_format=torch.channels_last_3d) for k, v in grids.items()}
+    fdev = [(d.to(DEV), c.to(DEV), m.to(DEV)) for d, c, m in frames]
+    # the coarse grid is not frustum-masked (Mapper.py:113-115 returns an all-true mask): dense gradients
+    eng, snap, ray_loss, keep = run_engine(nice, gdev, bound, fdev, pix, n_per, cam, "coarse", None, 32, 16, ())
+    ro, rd, gd, gc, _ = oracle_batch(frames, pix, n_per, cam, bound)
+    loss, g, _, _ = oracle_step(sd, grids, ro, rd, gd, gc, "coarse", bound, 32, 16, (), coarse_bound=bound * 2)
+    report = {"loss_rel": abs(float(ray_loss.sum()) - loss) / loss, "rays": int(ro.shape[0])}
+    ok = report["loss_rel"] < 1e-5
+    ok &= check(report, "grid_coarse", snap["grid_coarse"], g["grid_coarse"], TOL["grid_coarse"])
+    print(json.dumps(report, indent=1))
+    assert ok, report
+
+
+def test_stress_color_iteration_65536x64():
+    """configs[4]: 512³×32 fine / colour grids (16 GiB each) + 256³ middle, 65536 pixels × 64
+    samples, one colour-stage engine iteration with frustum-compacted gradients, vs the oracle
+    evaluated on the device on the same (channels-last) grids."""
+    cam = dict(scenes.ROOM0_CAM)
+    lens = {"coarse": 2.0, "middle": 1 / 32, "fine": 1 / 64, "color": 1 / 64}
+    bound, grids, sd, frames = build_scene([[0.0, 7.9]] * 3, cam, 4, seed=81, lens=lens, div=0.5, device_grids=True)
+    assert [list(grids[k].shape) for k in ("grid_middle", "grid_fine", "grid_color")] == \
+        [[1, 32, 256, 256, 256], [1, 32, 512, 512, 512], [1, 32, 512, 512, 512]]
+    n_per = 16384
+    pix = torch.randint(cam["H"] * cam["W"], (4 * n_per,), generator=torch.Generator().manual_seed(82))
+    nice = product_nice(sd, bound)
+    fdev = [(d.to(DEV), c.to(DEV), m.to(DEV)) for d, c, m in frames]
+    rows = frustum_rows(frames, grids, bound, cam)
+    eng, snap, ray_loss, keep = run_engine(nice, grids, bound, fdev, pix, n_per, cam, "color", rows, 48, 16,
+                                           ("color",))
+    n_keep = int(keep.sum())
+    assert bool(torch.isfinite(ray_loss).all()) and n_keep > 60000
+    del eng
+    torch.cuda.empty_cache()
+    ro, rd, gd, gc, k_ref = oracle_batch([(d, c, m) for d, c, m in fdev], pix, n_per, cam, bound, dev=DEV)
+    assert torch.equal(keep.bool(), k_ref) and ro.shape[0] == n_keep
+    sd_dev = {k: v.to(DEV) for k, v in sd.items()}
+    loss, g, dec, _ = oracle_step(sd_dev, grids, ro, rd, gd, gc, "color", bound, 48, 16, ("color",))
+    report = {"loss_rel": abs(float(ray_loss.sum()) - loss) / loss, "rays": n_keep,
+              "rows": {k: int(r.numel()) for k, r in rows.items()}}
+    ok = report["loss_rel"] < 1e-5
+    for k in ("grid_middle", "grid_fine", "grid_color"):
+        ok &= check(report, k, snap[k], compact(g[k], rows[k]), TOL[k])
+        g[k] = None
+    ok &= check(report, "color_decoder", snap["dec.color"], decoder_flat(nice, "color", dec), TOL["decoder"])
+    print(json.dumps(report, indent=1))
+    del grids, g
+    torch.cuda.empty_cache()
+    assert ok, report
+
+
+def test_scene0000_bundle_adjustment_window5(monkeypatch):
+    """configs[2]: Mapper.optimize_map with BA over a 5-frame window at scene0000 shapes and 5000
+    pixels: 4 keyframes + the current frame, window [0, 1, 2] (overlap selection stubbed: it is
+    pinned separately) + the last keyframe (3) + the current frame; frame 0 (oldest) stays fixed,
+    4 cameras get Adam steps at BA_cam_lr in the colour stage.  3 iterations: middle, middle,
+    colour (Mapper.py:403-421).  Oracle replica: the same draws, frustum-masked grid updates
+    (Adam with the gradient outside the mask zeroed ≡ Adam on the masked vector)."""
+    from test_gpu_dropins import base_cfg
+    cam = SCANNET_CAM
+    bound, grids, sd, frames = build_scene([[-2.0, 11.0], [-2.0, 11.5], [-2.0, 5.5]], cam, 5, seed=91)
+    grids = {k: v for k, v in grids.items() if k != "grid_coarse"}
+    cfg = base_cfg()
+    cfg["mapping"].update(pixels=5000, mapping_window_size=5, frustum_feature_selection=True)
+    cfg["rendering"].update(N_samples=32, N_surface=16)
+    nice = product_nice(sd, bound)
+    from types import SimpleNamespace
+    slam = SimpleNamespace(nice=True, bound=bound, H=cam["H"], W=cam["W"], fx=cam["fx"], fy=cam["fy"], cx=cam["cx"],
+                           cy=cam["cy"], shared_decoders=nice,
+                           shared_c={k: v.to(DEV).contiguous(memory_format=torch.channels_last_3d)
+                                     for k, v in grids.items()},
+                           estimate_c2w_list=torch.zeros(4, 4, 4), gt_c2w_list=torch.zeros(4, 4, 4),
+                           mapping_idx=torch.zeros(1).int())
+    slam.renderer = P.Renderer(cfg, None, slam)
+    mp = P.Mapper(cfg, None, slam)
+    mp.BA = True
+    mp.loss_history = []
+    monkeypatch.setattr(mp, "keyframe_selection_overlap", lambda *a, **k: [0, 1, 2])
+    fp = FixedPixels(seed=93)
+    monkeypatch.setattr(P.common, "select_uv", fp)
+    kf = [{"gt_c2w": m, "idx": 10 * i, "depth": d, "color": c, "est_c2w": m.clone()}
+          for i, (d, c, m) in enumerate(frames[:4])]
+    cur_d, cur_c, cur_m = frames[4]
+    n = 3
+    out = mp.optimize_map(n, 1.0, 40, cur_c, cur_d, cur_m, kf, [0, 10, 20, 30], cur_m.clone())
+    torch.cuda.synchronize()
+    losses = [float(x) for x in mp.loss_history]
+
+    # oracle replica (Mapper.py:230-540 with BA, frustum selection; window order [0, 1, 2, 3, -1])
+    masks = {}
+    for k, v in grids.items():
+        m = P.mapper.frustum_mask(cur_m.to(DEV), k, v.shape[2:], cur_d.to(DEV), bound, cam["H"], cam["W"], cam["fx"],
+                                  cam["fy"], cam["cx"], cam["cy"])
+        masks[k] = m.permute(2, 1, 0)[None, None].expand(1, 32, -1, -1, -1).cpu()
+    sdo = {k: v.clone().requires_grad_(k.startswith("color_decoder.")) for k, v in sd.items()}
+    go = {k: v.clone().requires_grad_(True) for k, v in grids.items()}
+    poses0 = [m for _, _, m in frames]
+    cams = [P.common.get_tensor_from_camera(poses0[f]).float().requires_grad_(True) for f in (1, 2, 3, 4)]
+    st = cfg["mapping"]["stage"]
+    opt = torch.optim.Adam([{"params": [v for k, v in sdo.items() if v.requires_grad], "lr": 0},
+                            {"params": [], "lr": 0}, {"params": [go["grid_middle"]], "lr": 0},
+                            {"params": [go["grid_fine"]], "lr": 0}, {"params": [go["grid_color"]], "lr": 0},
+                            {"params": cams, "lr": 0}])
+    ref = []
+    n_per = 1000
+    for it in range(n):
+        stage = "middle" if it <= int(n * 0.4) else ("fine" if it <= int(n * 0.6) else "color")
+        for gi, name in enumerate(("decoders", "coarse", "middle", "fine", "color")):
+            opt.param_groups[gi]["lr"] = st[stage][name + "_lr"]
+        if stage == "color":
+            opt.param_groups[5]["lr"] = cfg["mapping"]["BA_cam_lr"]
+        opt.zero_grad()
+        fr = [(frames[0][0], frames[0][1], poses0[0])] + \
+             [(frames[f][0], frames[f][1], orc.camera_from_tensor(cams[f - 1])) for f in (1, 2, 3, 4)]
+        pix = torch.cat([fp.log[5 * it + f] for f in range(5)])
+        ro, rd, gd, gc, _ = oracle_batch(fr, pix, n_per, cam, bound)
+        d, v, c = orc.render_batch_ray(sdo, go, rd, ro, stage, bound, gd)
+        loss = orc.mapper_loss(d, c, gd, gc, stage)
+        loss.backward()
+        for k in go:
+            if go[k].grad is not None:
+                go[k].grad *= masks[k]
+        opt.step()
+        ref.append(float(loss))
+    np.testing.assert_allclose(losses, ref, rtol=2e-3)
+    report = {}
+    for f, (got, start) in enumerate(((kf[1]["est_c2w"], poses0[1]), (kf[2]["est_c2w"], poses0[2]),
+                                      (kf[3]["est_c2w"], poses0[3]), (out, poses0[4]))):
+        r = orc.camera_from_tensor(cams[f].detach())
+        d_ref = r - start[:3]
+        assert float(d_ref.abs().max()) > 1e-6
+        report[f"pose{f + 1}"] = rel_l2(got[:3].detach().cpu() - start[:3], d_ref)
+    assert torch.equal(kf[0]["est_c2w"], poses0[0])
+    for k in go:
+        report[k] = rel_l2(slam.shared_c[k].detach().cpu() - grids[k], go[k].detach() - grids[k])
+    print(json.dumps(report, indent=1))
+    assert all(v < 5e-2 for v in report.values()), report

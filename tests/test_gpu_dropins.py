@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import grids_from, rel_l2, sd_from
+from conftest import FixedPixels, grids_from, rel_l2, sd_from
 from oracle import nslam_oracle as orc
 
 pytestmark = pytest.mark.gpu
@@ -72,24 +72,6 @@ class Scene:
                             mapping_idx=torch.zeros(1).int())
         s.renderer = P.Renderer(cfg, None, s)
         return s
-
-
-class FixedPixels:
-    """Replaces common.select_uv: hands out pre-drawn flat pixel indices in call order."""
-
-    def __init__(self, seed=11):
-        self.g = torch.Generator().manual_seed(seed)
-        self.log = []
-
-    def draw(self, n_total, n):
-        idx = torch.randint(n_total, (n,), generator=self.g)
-        self.log.append(idx)
-        return idx
-
-    def __call__(self, i, j, n, depth, color, device="cuda:0", generator=None):
-        i, j = i.reshape(-1), j.reshape(-1)
-        idx = self.draw(i.shape[0], n).to(i.device)
-        return i[idx], j[idx], depth.reshape(-1)[idx], color.reshape(-1, 3)[idx]
 
 
 def oracle_samples(scene, idx, H0, H1, W0, W1, c2w, depth, color):

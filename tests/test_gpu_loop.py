@@ -1,0 +1,250 @@
+"""GPU parity of the loop-level pieces against vectors the REFERENCE's own code produced
+(tests/golden/loop_fixtures.npz, tests/golden/make_golden_loop.py):
+
+  nslam_cam_pose / nslam_cam_grad      vs get_camera_from_tensor + get_rays_from_uv + pts (a2, a3)
+  nslam_render_loss TRACKER / MAPPER   vs Tracker.py:110-125 / Mapper.py:487-503 (a13, a14)
+  Tracker.optimize_cam_in_batch        vs Tracker.py:71-128, 3 iterations (drop-in and TrackingEngine)
+  Mapper.optimize_map                  vs Mapper.py:230-540: frustum selection, overlap keyframe
+                                       selection, BA over a 5-frame window (a16, a17, f3)
+  mapper.frustum_mask / overlap scores vs Mapper.py:93-228 at room0 shapes, on the device
+
+Tolerances: forward quantities as tests/test_gpu_parity.py; multi-iteration loops (Adam
+normalises every gradient, so fp32-level differences in tiny gradient entries become lr-sized
+steps) as tests/test_gpu_dropins.py: losses rtol 2e-3 (mapper) / 2e-4 (tracker), parameter
+updates rel-L2 5e-2 / 1e-2.
+"""
+import importlib
+import json
+import sys
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, FixedPixels, rel_l2
+
+sys.path.insert(0, GOLDEN)
+import scenes  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+P = importlib.import_module("nice-slam_amd")
+DEV = torch.device("cuda:0")
+
+
+def test_cam_pose_matches_reference(loop):
+    cams = torch.from_numpy(loop["camera.cam"]).to(DEV)
+    ref = torch.from_numpy(loop["camera.c2w"])
+    out = torch.empty(3, 4, device=DEV)
+    exact, worst = 0, 0.0
+    for b in range(cams.shape[0]):
+        P.ops.cam_pose(cams[b].contiguous(), out)
+        got = out.cpu()
+        exact += bool(torch.equal(got, ref[b]))
+        worst = max(worst, float((got - ref[b]).abs().max() / ref[b].abs().max()))
+    print(f"cam_pose vs reference: {exact}/{cams.shape[0]} bit-identical, worst rel {worst:.2e}")
+    assert worst < 1e-6
+
+
+def test_cam_grad_matches_reference(loop):
+    """d loss/d cam for fixed d loss/d pts through the reference's rays + pts chain."""
+    B = loop["camera.cam"].shape[0]
+    out = torch.empty(7, device=DEV)
+    c2w = torch.empty(3, 4, device=DEV)
+    worst = 0.0
+    for b in range(B):
+        cam = torch.from_numpy(loop["camera.cam"][b]).to(DEV)
+        P.ops.cam_pose(cam, c2w)
+        z = torch.from_numpy(loop["camera.z"][b]).to(DEV).contiguous()
+        gp = torch.from_numpy(loop["camera.g_pts"][b]).to(DEV).reshape(-1, 3).contiguous()
+        rd = torch.from_numpy(loop["camera.rays_d"][b]).to(DEV).contiguous()
+        P.ops.cam_grad(cam, c2w, gp, z, rd, out)
+        worst = max(worst, rel_l2(out, loop["camera.grad_cam"][b]))
+    print(f"cam_grad vs reference: worst rel-L2 {worst:.2e}")
+    assert worst < 1e-5
+
+
+@pytest.mark.parametrize("case,mode,hd,use_color,w", [("tloss_hd", "tracker", True, True, 0.5),
+                                                       ("tloss_nohd", "tracker", False, True, 0.5),
+                                                       ("mloss_color", "mapper", False, True, 0.2),
+                                                       ("mloss_middle", "mapper", False, False, 0.2)])
+def test_render_loss_matches_reference(loop, case, mode, hd, use_color, w):
+    raw = torch.from_numpy(loop[case + ".raw"]).to(DEV)
+    z = torch.from_numpy(loop[case + ".z"]).to(DEV)
+    gd = torch.from_numpy(loop[case + ".gt_depth"]).to(DEV)
+    gc = torch.from_numpy(loop[case + ".gt_color"]).to(DEV)
+    _, _, _, ray_loss, g_raw = P.ops.render_loss(raw, z, gd, gc, None, mode=mode, use_color=use_color,
+                                                 handle_dynamic=hd, w_color=w)
+    ref = float(loop[case + ".loss"])
+    got = float(ray_loss.sum())
+    assert abs(got - ref) <= 1e-6 * abs(ref), (got, ref)
+    gref = torch.from_numpy(loop[case + ".g_raw"])
+    assert float((g_raw.cpu() - gref).abs().max()) <= 1e-6 * max(1.0, float(gref.abs().max()))
+
+
+# ------------------------------------------------------------------------------------------------
+# drop-in loops on the tiny scene
+# ------------------------------------------------------------------------------------------------
+def tiny_slam(tiny, cfg, cam):
+    bound = torch.from_numpy(tiny["bound"])
+    sd = {k[3:]: torch.from_numpy(v) for k, v in tiny.items() if k.startswith("sd.") and not k.startswith("sd.coarse")}
+    nice = P.NICE(c_dim=32, coarse=False, middle_grid_len=0.64, fine_grid_len=0.32, color_grid_len=0.32)
+    nice.load_state_dict(sd)
+    nice.set_bound(bound)
+    grids = {k: torch.from_numpy(tiny[k]).to(DEV).contiguous(memory_format=torch.channels_last_3d)
+             for k in ("grid_middle", "grid_fine", "grid_color")}
+    s = SimpleNamespace(nice=True, bound=bound, H=cam["H"], W=cam["W"], fx=cam["fx"], fy=cam["fy"], cx=cam["cx"],
+                        cy=cam["cy"], shared_decoders=nice.to(DEV), shared_c=grids,
+                        estimate_c2w_list=torch.zeros(4, 4, 4), gt_c2w_list=torch.zeros(4, 4, 4),
+                        mapping_idx=torch.zeros(1).int())
+    s.renderer = P.Renderer(cfg, None, s)
+    return s
+
+
+def loop_cfg(frustum=True, pixels=1000, window=5):
+    from test_gpu_dropins import base_cfg
+    cfg = base_cfg()
+    m = cfg["mapping"]
+    m.update(pixels=pixels, mapping_window_size=window, frustum_feature_selection=frustum)
+    return cfg
+
+
+def test_tracker_loop_matches_reference(tiny, loop, monkeypatch):
+    cam = scenes.TINY_CAM
+    b, _, cur = scenes.tiny_window()
+    depth = torch.from_numpy(scenes.box_depth(cur, cam, b, seed=int(loop["track.depth_seed"]))).to(DEV)
+    color = torch.from_numpy(scenes.color_image(cam, seed=int(loop["track.color_seed"]))).to(DEV)
+    cfg = loop_cfg()
+    cam0 = torch.from_numpy(loop["track.cam0"])
+    # (1) the autograd drop-in, Tracker.optimize_cam_in_batch
+    monkeypatch.setattr(P.common, "select_uv", FixedPixels(int(loop["track.draw_seed"])))
+    tr = P.Tracker(cfg, None, tiny_slam(tiny, cfg, cam))
+    tr.update_para_from_mapping()
+    camt = cam0.to(DEV).clone().requires_grad_(True)
+    opt = torch.optim.Adam([camt], lr=0.001)
+    grads, cams, losses = [], [], []
+    step = opt.step
+
+    def step_rec(*a, **k):
+        grads.append(camt.grad.detach().cpu().clone())
+        return step(*a, **k)
+
+    opt.step = step_rec
+    for _ in range(3):
+        losses.append(tr.optimize_cam_in_batch(camt, color, depth, 200, opt))
+        cams.append(camt.detach().cpu().clone())
+    ref_l, ref_g, ref_c = loop["track.losses"], loop["track.grads"], loop["track.cams"]
+    np.testing.assert_allclose(losses, ref_l, rtol=2e-4)
+    assert rel_l2(grads[0], ref_g[0]) < 1e-3
+    for k in range(3):
+        assert rel_l2(cams[k] - cam0, ref_c[k] - cam0.numpy()) < 1e-2, k
+    # (2) the fused TrackingEngine on the same draws (select_uv indices into the cropped window)
+    fp = FixedPixels(int(loop["track.draw_seed"]))
+    eng = P.engine.TrackingEngine(tr.decoders, {k: v for k, v in tr.c.items()}, tr.bound, 32, 16,
+                                  (cam["H"], cam["W"]), (cam["fx"], cam["fy"], cam["cx"], cam["cy"]),
+                                  ignore_edge=(20, 20), w_color=0.5, handle_dynamic=True, use_color=True, device=DEV)
+    camf = cam0.to(DEV).clone().requires_grad_(True)
+    fopt = P.ops.FusedAdam([{"params": [camf], "lr": 0.001}])
+    flosses = []
+    for k in range(3):
+        pix = fp.draw(eng.n_window(), 200).to(DEV)
+        flosses.append(float(eng.iteration(camf, depth, color, pix, fopt)))
+        assert rel_l2(camf.detach().cpu() - cam0, ref_c[k] - cam0.numpy()) < 1e-2, k
+    np.testing.assert_allclose(flosses, ref_l, rtol=2e-4)
+
+
+def test_mapper_loop_matches_reference(tiny, loop, monkeypatch):
+    """optimize_map with frustum feature selection, overlap keyframe selection and BA over a
+    5-frame window (4 cameras optimised, the oldest fixed): losses of all 8 iterations (middle →
+    fine → colour), the selected keyframes, the updated grids / colour decoder / poses."""
+    cam = scenes.TINY_CAM
+    b, poses, cur = scenes.tiny_window()
+    cfg = loop_cfg(frustum=True, pixels=1000, window=5)
+    slam = tiny_slam(tiny, cfg, cam)
+    g0 = {k: v.detach().cpu().clone() for k, v in slam.shared_c.items()}
+    mp = P.Mapper(cfg, None, slam)
+    mp.BA = True
+    mp.loss_history = []
+    sel = []
+    orig_sel = mp.keyframe_selection_overlap
+
+    def sel_rec(*a, **k):
+        out = orig_sel(*a, **k)
+        sel.append([int(x) for x in out])
+        return out
+
+    mp.keyframe_selection_overlap = sel_rec
+    kf = []
+    for k, p in enumerate(poses):
+        kf.append({"gt_c2w": torch.from_numpy(p), "idx": 5 * k, "est_c2w": torch.from_numpy(p).clone(),
+                   "depth": torch.from_numpy(scenes.box_depth(p, cam, b, seed=100 + k)),
+                   "color": torch.from_numpy(scenes.color_image(cam, seed=200 + k))})
+    cur_depth = torch.from_numpy(scenes.box_depth(cur, cam, b, seed=150))
+    cur_color = torch.from_numpy(scenes.color_image(cam, seed=250))
+    monkeypatch.setattr(P.common, "select_uv", FixedPixels(int(loop["map.draw_seed"])))
+    np.random.seed(int(loop["map.np_seed"]))
+    n = int(loop["map.n_iters"])
+    out = mp.optimize_map(n, 1.0, 30, cur_color, cur_depth, torch.from_numpy(cur), kf, [5 * k for k in range(5)],
+                          torch.from_numpy(cur).clone())
+    torch.cuda.synchronize()
+    assert sel[0] == [int(x) for x in loop["map.selected"]]
+    losses = [float(x) for x in mp.loss_history]
+    np.testing.assert_allclose(losses, loop["map.losses"], rtol=2e-3)
+    report = {}
+    for k in ("grid_middle", "grid_fine", "grid_color"):
+        d_got = slam.shared_c[k].detach().cpu() - g0[k]
+        d_ref = torch.from_numpy(loop["map.grid_out." + k]) - g0[k]
+        report[k] = rel_l2(d_got, d_ref)
+        # frustum selection: voxels outside the reference's mask are untouched
+        mask = torch.from_numpy(loop["map.mask." + k]).permute(2, 1, 0)[None, None].expand_as(d_got)
+        assert float(d_got[~mask].abs().max()) == 0.0, k
+    sd = mp.decoders.color_decoder.state_dict()
+    d_got = torch.cat([sd[k].detach().cpu().reshape(-1) for k in sd])
+    d_ref = torch.cat([torch.from_numpy(loop["map.color_decoder_out." + k]).reshape(-1) for k in sd])
+    d0 = torch.cat([torch.from_numpy(tiny["sd.color_decoder." + k]).reshape(-1) for k in sd])
+    report["color_decoder"] = rel_l2(d_got - d0, d_ref - d0)
+    # poses: the 4 optimised cameras moved as the reference's did, the oldest did not move
+    oldest = min(int(x) for x in loop["map.selected"])
+    for k in range(5):
+        got = kf[k]["est_c2w"].detach().cpu()
+        ref = torch.from_numpy(loop[f"map.est_c2w_out.{k}"])
+        start = torch.from_numpy(poses[k])
+        if k == oldest or (k not in [int(x) for x in loop["map.selected"]] and k != 4):
+            assert torch.equal(got, start), k
+            continue
+        report[f"pose{k}"] = rel_l2(got - start, ref - start)
+    report["cur"] = rel_l2(out.detach().cpu() - torch.from_numpy(cur), loop["map.cur_c2w_out"] - cur)
+    print(json.dumps(report, indent=1))
+    assert all(v < 5e-2 for v in report.values()), report
+
+
+def test_frustum_mask_device_matches_reference(loop):
+    b, _, cur = scenes.room0_window()
+    cam = scenes.ROOM0_CAM
+    depth = torch.from_numpy(scenes.box_depth(cur, cam, b, seed=int(loop["frustum.depth_seed"]))).to(DEV)
+    for key in ("grid_middle", "grid_fine", "grid_color"):
+        shp = tuple(int(v) for v in loop["frustum.shape." + key])
+        m = P.mapper.frustum_mask(torch.from_numpy(cur).to(DEV), key, shp, depth, torch.from_numpy(b), cam["H"],
+                                  cam["W"], cam["fx"], cam["fy"], cam["cx"], cam["cy"])
+        ref = loop["frustum.mask." + key]
+        bad = int((m.cpu().numpy() != ref).sum())
+        print(f"frustum {key}: {bad} of {ref.size} voxels differ ({int(ref.sum())} selected)")
+        assert bad == 0, key
+
+
+def test_keyframe_overlap_device_matches_reference(loop, monkeypatch):
+    b, poses, cur = scenes.room0_window()
+    cam = scenes.ROOM0_CAM
+    depth = torch.from_numpy(scenes.box_depth(cur, cam, b, seed=int(loop["overlap.depth_seed"]))).to(DEV)
+    color = torch.from_numpy(scenes.color_image(cam, seed=int(loop["overlap.color_seed"]))).to(DEV)
+    kf = [{"est_c2w": torch.from_numpy(p).to(DEV)} for p in poses]
+    from test_loop_golden import overlap_mapper
+    mp = overlap_mapper(P, DEV)
+    monkeypatch.setattr(P.common, "select_uv", FixedPixels(int(loop["overlap.draw_seed"])))
+    scores = mp.keyframe_overlap_scores(color, depth, torch.from_numpy(cur).to(DEV), kf)
+    # 1600 samples per keyframe: one sample flipping across an image edge moves a score by 1/1600
+    np.testing.assert_allclose(scores, loop["overlap.scores"], atol=1.5 / 1600)
+    monkeypatch.setattr(P.common, "select_uv", FixedPixels(int(loop["overlap.draw_seed"])))
+    np.random.seed(int(loop["overlap.np_seed"]))
+    sel = mp.keyframe_selection_overlap(color, depth, torch.from_numpy(cur).to(DEV), kf, int(loop["overlap.k"]))
+    assert [int(s) for s in sel] == [int(s) for s in loop["overlap.selected"]]

@@ -227,4 +227,20 @@ def test_room0_color_stage_matches_golden(pkg, dev, room0):
             rel = abs(nrm - ref) / max(ref, 1e-30)
             REPORT["room0"][name + ".norm"] = {"got": nrm, "ref": ref, "rel": rel}
             ok &= rel <= max(tol_for(name), 1e-4)
-    assert ok, json.dumps(REPORT["room0"], indent=1)
+    # elementwise: the pinned oracle (its room0 norms / sums equal the reference's, test_oracle_golden)
+    # on the same inputs and cotangents — every grid-gradient and decoder-gradient entry
+    gl = {k: v.clone().requires_grad_(True) for k, v in grids.items()}
+    sdo = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    ro_c = torch.from_numpy(room0["rays_o"]).requires_grad_(True)
+    rd_c = torch.from_numpy(room0["rays_d"]).requires_grad_(True)
+    d_o, v_o, c_o = orc.render_batch_ray(sdo, gl, rd_c, ro_c, "color", bound, torch.from_numpy(room0["gt_depth"]))
+    cots_c = tuple(torch.from_numpy(room0[k]) for k in ("cot_depth", "cot_var", "cot_color"))
+    onames = [k for k in gl] + [k for k in sdo]
+    og = torch.autograd.grad((d_o, v_o, c_o), [gl[k] for k in gl] + [sdo[k] for k in sdo], cots_c, allow_unused=True)
+    oref = dict(zip(onames, og))
+    for name, gg in zip(names, grads):
+        ref = oref.get(name)
+        if ref is None or gg is None or name in ("rays_o", "rays_d"):
+            continue
+        ok &= record("room0_elementwise", name, gg, ref)["rel_l2"] <= tol_for(name)
+    assert ok, json.dumps({k: REPORT.get(k) for k in ("room0", "room0_elementwise")}, indent=1)
