@@ -296,7 +296,8 @@ typedef struct nslam_adam_seg {
 } nslam_adam_seg;
 /* ticket: NULL = the step counts advance in a second single-wave launch; else a device uint32
  * (zero-initialised, re-armed by the call itself) with which the update kernel's last workgroup
- * advances them — one launch per step (ABI v9). */
+ * advances them — one launch per step (ABI v9).  A ticket belongs to one call at a time: calls that
+ * may run concurrently (other streams, other processes) each pass their own. */
 int nslam_adam_step(const nslam_adam_seg* segs, int32_t n_segs, float beta1, float beta2, float eps,
                     int32_t zero_grad, uint32_t* ticket, void* stream);
 

@@ -268,9 +268,10 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam(AdamArgs a) {
   }
 }
 
-// Every segment's step advances after the update kernel, in its own single-wave launch (stream
-// order makes it see all reads of the old count).  The previous last-workgroup ticket needed a
-// device-scope release fence (an L2 writeback on gfx950's per-XCD L2s) in every workgroup.
+// Without a ticket, every segment's step advances after the update kernel in its own single-wave
+// launch (stream order makes it see all reads of the old count).  The ticket path above needs no
+// release fence: the last workgroup reads nothing the other workgroups wrote (only the ticket, an
+// atomic), and the counts it stores are read by later kernels only, across the kernel boundary.
 __global__ __launch_bounds__(64) void k_adam_steps(AdamArgs a) {
   if (threadIdx.x < (unsigned)a.nseg) *a.seg[threadIdx.x].step += 1.f;
 }

@@ -24,6 +24,9 @@ struct QueryKArgs {
   float* raw;          // fwd output [n][4]
   const float* g_raw;  // bwd input  [n][4]
   double* g_pts;       // bwd output [n][3]
+  // colour-decoder cotangent tape (workspace of a colour weight-gradient backward, NULL = none):
+  // the lean backward stores dh_0..dh_4 of every tile here for k_color_wgrad
+  float* cot = nullptr;
 };
 
 // ------------------------------------------------------------------------------------------
@@ -102,7 +105,6 @@ __device__ __forceinline__ f32x16 emb_tile(const float* __restrict__ B, const fl
 struct Scratch {
   float* sA;    // [32][33] transposed cotangent tile
   float* sX;    // [32][33] transposed input tile
-  float* sD3;   // [32][33] layer-3 cotangent (tape backward: kept for the embedding blocks)
   float* gtab;  // [32][4]  per-point output cotangents
   float* xtab;  // [32][3]  per-point x (float)
   int* crow;    // [32][8]  corner rows (grad slots when the grid gradient is frustum-compacted)
@@ -152,7 +154,14 @@ __device__ __forceinline__ void load_masks(const QueryKArgs& a, int dec, int64_t
 // Activation tape of the colour decoder (ABI v9 nslam_query_cfg.act_tape): the forward stores the
 // post-ReLU hidden tiles h0..h4 of every tile (C layout) and the weight-gradient backward reads them
 // instead of recomputing the decoder (it needs them as the inputs of dW; Mapper.py:503).
-constexpr int kTapeFloats = 5 * 16 * 64;  // per tile
+constexpr int kTapeFloats = 6 * 16 * 64;  // per tile: h0..h4 and (slot 5) the colour feature c
+constexpr int kTapeFeat = 5;
+// Cotangent tape of the colour decoder's weight-gradient backward: dh_0..dh_4 (the cotangents of
+// the five hidden layers before their ReLU masks) of every tile, in the activation tape's layout,
+// then a [32 points][8] block of x (float, 3 + pad) and the colour cotangent g (3 + pad): every
+// tile is 21 KiB of whole 1-KiB pieces (k_color_wgrad stages them by LDS-DMA).
+constexpr int kCotXg = 5 * 16 * 64;
+constexpr int kCotFloats = kCotXg + 32 * 8;
 // Layout [tile][layer][register r][64 lanes] float: every store / load instruction moves 256 B
 // contiguous, and no 4-register grouping of the tile is needed (a float4 layout cost the forward
 // ~30 VGPRs of copies).
@@ -176,6 +185,23 @@ __device__ __forceinline__ f32x16 tape_bop(const float* __restrict__ t, int i, i
   f32x16 v;
 #pragma unroll
   for (int s = 0; s < 16; ++s) v[s] = p[s * 64];
+  return v;
+}
+
+// Layer i of a point-major tape back in the C layout (inverse of tape_store): lane (p, h) gets
+// features F(r, h) of point p.
+__device__ __forceinline__ f32x16 tape_cload(const float* __restrict__ t, int i, int lane) {
+  const int p = lane & 31, h = lane >> 5;
+  const gptr_t<f32x4> q = as_global(reinterpret_cast<const f32x4*>(t + i * 1024 + p * 32 + 4 * h));
+  f32x16 v;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const f32x4 w = q[2 * k];
+    v[4 * k] = w[0];
+    v[4 * k + 1] = w[1];
+    v[4 * k + 2] = w[2];
+    v[4 * k + 3] = w[3];
+  }
   return v;
 }
 
@@ -661,10 +687,12 @@ __device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, con
 // dh_{i-1} = L_iT mask_i(dh_i) (layer 3 through its hidden block); EMBG adds d/dx through the
 // Fourier features from mask_3(dh_3) and mask_0(dh_0).
 // ------------------------------------------------------------------------------------------
+// cot (colour weight-gradient backward, else NULL): the tile's cotangent tape — dh_4..dh_0 are
+// stored there as they are formed, for k_color_wgrad.
 template <int NC, int NOUT, int GOFS, bool EMBG>
 __device__ __forceinline__ void xyz_backward_saved(const float* __restrict__ pk, const uint32_t m[5],
                                                    const float x[3], const float (&gall)[4], int lane, f32x16& dc,
-                                                   float gx[3]) {
+                                                   float gx[3], float* __restrict__ cot = nullptr) {
   const XyzPack L{NC};
   const int h = lane >> 5;
   f32x16 dh = zero16();
@@ -674,23 +702,28 @@ __device__ __forceinline__ void xyz_backward_saved(const float* __restrict__ pk,
 #pragma unroll
     for (int r = 0; r < 16; ++r) dh[r] += w[r] * gall[GOFS + j];
   }
+  if (cot) tape_store(cot, 4, dh, lane);
   dc = zero16();
   gemm_acc(dc, pk + L.FCT(4) * NSLAM_FRAG, dh, lane);
   f32x16 da = apply_mask(dh, m[4]);
   dh = zero16();
   gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
+  if (cot) tape_store(cot, 3, dh, lane);
   gemm_acc(dc, pk + L.FCT(3) * NSLAM_FRAG, dh, lane);
   const f32x16 da3 = apply_mask(dh, m[3]);
   dh = zero16();
   gemm_acc(dh, pk + (L.L3T() + 3) * NSLAM_FRAG, da3, lane);
+  if (cot) tape_store(cot, 2, dh, lane);
   gemm_acc(dc, pk + L.FCT(2) * NSLAM_FRAG, dh, lane);
   da = apply_mask(dh, m[2]);
   dh = zero16();
   gemm_acc(dh, pk + L.L2T() * NSLAM_FRAG, da, lane);
+  if (cot) tape_store(cot, 1, dh, lane);
   gemm_acc(dc, pk + L.FCT(1) * NSLAM_FRAG, dh, lane);
   da = apply_mask(dh, m[1]);
   dh = zero16();
   gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
+  if (cot) tape_store(cot, 0, dh, lane);
   gemm_acc(dc, pk + L.FCT(0) * NSLAM_FRAG, dh, lane);
   gx[0] = gx[1] = gx[2] = 0.f;
   if (EMBG) {
@@ -719,161 +752,6 @@ __device__ __forceinline__ void xyz_backward_saved(const float* __restrict__ pk,
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) gx[k] += xor32(gx[k]);
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// Colour decoder backward from the forward's masks + activation tape (no forward recompute):
-// the dh chain is the mask-only one; every weight gradient takes its input tile from the tape
-// (h0..h4) or from the colour feature `cin`; the embedding is evaluated ONCE at the end, per
-// block b: sin_b feeds both dW3's and dW0's embedding columns (the layer-3 and layer-0
-// cotangents wait in LDS images sD3 / sA), cos_b the Fourier backward G_b = de_b * cos_b -> dB.
-// ------------------------------------------------------------------------------------------
-template <int WG>
-__device__ __forceinline__ void color_backward_tape(const float* __restrict__ pk, const f32x16& cin, const float x[3],
-                                                    const float (&gall)[4], const uint32_t m[5],
-                                                    const float* __restrict__ tape, const nslam_dec_grad& dg,
-                                                    const Slab& A, const Scratch& S, int lane, f32x16& dc) {
-  const XyzPack L{1};
-  const int h = lane >> 5, f = lane & 31;
-  // sX holds the colour feature's image through layers 4..0: the input of every fc_c weight
-  // gradient (one transpose per tile); the hidden inputs come from the tape as B-operand streams
-  tstore(S.sX, cin, lane);
-  // output layer (3 rows used; row 3 is overwritten by the stage combiner, decoder.py:331-334)
-  f32x16 dh = zero16();
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const f32x16 w = vec_tile_g(pk + L.Wo() + 32 * j, lane);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dh[r] += w[r] * gall[j];
-  }
-  {
-    const f32x16 b4 = tape_bop(tape, 4, lane);  // h4[2t+h][f]
-    lds_sync();
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      float sw = 0.f;
-#pragma unroll
-      for (int t = 0; t < 16; ++t) sw += S.gtab[(2 * t + h) * 4 + j] * b4[t];
-      sw += xor32(sw);
-      if (h == 0) put<WG>(A, f, dg.wo + 32 * j, sw);
-      // dbo[j] = sum over the tile's points: butterfly over the 32 point lanes of half 0
-      float sb = gall[j];
-#pragma unroll
-      for (int o = 16; o > 0; o >>= 1) sb += __shfl_xor(sb, o, 64);
-      if (lane == 0) put<WG>(A, 0, dg.bo + j, sb);
-    }
-  }
-  if (WG == 1) {
-    if (h == 0) put<1>(A, f, dg.wo + 96, 0.f);
-    if (lane == 0) put<1>(A, 0, dg.bo + 3, 0.f);
-  }
-  PHASE(3, 5);
-  dc = zero16();
-  // fc_c branch i: dc += FC_i^T dh; dFC_i = dh (x) c (c image in sX); dbFC_i = sum dh
-  auto fc_step = [&](int i) {
-    gemm_acc(dc, pk + L.FCT(i) * NSLAM_FRAG, dh, lane);
-    tstore(S.sA, dh, lane);
-    lds_sync();
-    dw_block_img<WG>(A, dg.wc[i], 32, 0, 32, S.sA, S.sX, lane);
-    db_vec_img<WG>(A, dg.bc[i], S.sA, lane);
-    lds_sync();
-  };
-  // layer i's weight gradient: dW_i = da (x) h_{i-1} (tape B operand), db_i = sum da
-  auto w_step = [&](int i, const float* sa, int ldk, int kofs, const f32x16& bx) {
-    lds_sync();
-    dw_block_bop<WG>(A, dg.w[i], ldk, kofs, 32, sa, bx, lane);
-    db_vec_img<WG>(A, dg.b[i], sa, lane);
-    lds_sync();
-  };
-  // layer 4 (input h3)
-  fc_step(4);
-  f32x16 da = apply_mask(dh, m[4]);
-  tstore(S.sA, da, lane);
-  w_step(4, S.sA, 32, 0, tape_bop(tape, 3, lane));
-  dh = zero16();
-  gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
-  PHASE(3, 6);
-  // layer 3 (input [emb | h2]): the h2 columns now, the embedding columns at the end
-  fc_step(3);
-  const f32x16 da3 = apply_mask(dh, m[3]);
-  tstore(S.sD3, da3, lane);
-  w_step(3, S.sD3, 125, 93, tape_bop(tape, 2, lane));
-  dh = zero16();
-  gemm_acc(dh, pk + (L.L3T() + 3) * NSLAM_FRAG, da3, lane);
-  PHASE(3, 7);
-  // layer 2 (input h1)
-  fc_step(2);
-  da = apply_mask(dh, m[2]);
-  tstore(S.sA, da, lane);
-  w_step(2, S.sA, 32, 0, tape_bop(tape, 1, lane));
-  dh = zero16();
-  gemm_acc(dh, pk + L.L2T() * NSLAM_FRAG, da, lane);
-  PHASE(3, 8);
-  // layer 1 (input h0)
-  fc_step(1);
-  da = apply_mask(dh, m[1]);
-  tstore(S.sA, da, lane);
-  w_step(1, S.sA, 32, 0, tape_bop(tape, 0, lane));
-  dh = zero16();
-  gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
-  PHASE(3, 9);
-  // layer 0 (input emb): its cotangent stays in sA for the embedding blocks
-  fc_step(0);
-  da = apply_mask(dh, m[0]);
-  wg_begin(da, S, lane);
-  wg_end<WG>(A, dg.b[0], S, lane);
-  PHASE(3, 10);
-  // embedding blocks: sin_b -> dW3 / dW0 columns; cos_b -> G_b = (L3T_b da3 + L0T_b da0) cos_b -> dB
-  const float* FB = pk + L.FB();
-#pragma nounroll
-  for (int b = 0; b < 3; ++b) {
-    f32x16 sn, cs;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = 32 * b + 8 * i + 4 * h;
-      const f32x4 B0 = *as_global(reinterpret_cast<const f32x4*>(FB + k));
-      const f32x4 B1 = *as_global(reinterpret_cast<const f32x4*>(FB + 96 + k));
-      const f32x4 B2 = *as_global(reinterpret_cast<const f32x4*>(FB + 192 + k));
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float sv, cv;
-        fsincos(fourier_arg(x, B0[j], B1[j], B2[j]), sv, cv);
-        sn[4 * i + j] = sv;
-        cs[4 * i + j] = cv;
-      }
-    }
-    const int kv = b < 2 ? 32 : 29;
-    tstore(S.sX, sn, lane);
-    lds_sync();
-    dw_block_img<WG>(A, dg.w[3], 125, 32 * b, kv, S.sD3, S.sX, lane);
-    dw_block_img<WG>(A, dg.w[0], 93, 32 * b, kv, S.sA, S.sX, lane);
-    lds_sync();
-    f32x16 de = zero16();
-    gemm_acc(de, pk + (L.L3T() + b) * NSLAM_FRAG, da3, lane);
-    gemm_acc(de, pk + (L.L0T() + b) * NSLAM_FRAG, da, lane);
-    f32x16 G;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) G[r] = de[r] * cs[r];
-    tstore(S.sX, G, lane);
-    lds_sync();
-    // dB[j][k] += sum_p x_j[p] G[k][p]
-    const int jc = f < 3 ? f : 0;
-    f32x16 acc = zero16();
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const int p = 2 * t + h;
-      const float xv = f < 3 ? S.xtab[p * 3 + jc] : 0.f;
-      acc = mfma32(S.sX[p * TPITCH + f], xv, acc);
-    }
-    if (f < 3) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int k = 32 * b + fidx(r, h);
-        if (k < NSLAM_EMB) put<WG>(A, f * NSLAM_EMB + 4 * h, dg.B + 32 * b + (r & 3) + 8 * (r >> 2), acc[r]);
-      }
-    }
-    lds_sync();
   }
 }
 
@@ -1186,8 +1064,10 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd(QueryKArgs a) {
       const float* pk = a.c.packed[NSLAM_DEC_COLOR];
       const XyzPack L{1};
       f32x16 h4;
-      if (a.c.act_tape)
+      if (a.c.act_tape) {
+        tape_store(a.c.act_tape + tile * kTapeFloats, kTapeFeat, cc[0], lane);
         h4 = xyz_forward<1, false, false, true>(pk, cc, q.x, lane, m, nullptr, a.c.act_tape + tile * kTapeFloats);
+      }
       else
         h4 = xyz_forward<1, false>(pk, cc, q.x, lane, m, nullptr);
       save_masks(a, NSLAM_DEC_COLOR, tile, m, lane);
@@ -1277,6 +1157,7 @@ __device__ __forceinline__ void fwd_part_color(const QueryKArgs& a, const Pt& q,
   const float* pk = a.c.packed[NSLAM_DEC_COLOR];
   const XyzPack L{1};
   float* tp = TAPE ? a.c.act_tape + tile * kTapeFloats : nullptr;
+  if (TAPE) tape_store(tp, kTapeFeat, cc[0], lane);  // the fc_c weight gradients' input
   const f32x16 h4 = xyz_forward<1, false, true, TAPE, true>(pk, cc, q.x, lane, m, nullptr, tp, vec);
   save_masks(a, NSLAM_DEC_COLOR, tile, m, lane);
   float o[3];
@@ -1408,23 +1289,24 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
   PHASE(DEC, 2);
   f32x16 dc;
   float gx[3] = {0.f, 0.f, 0.f};
-  if constexpr (SAVED && WG != 0) {  // colour weight gradients from the masks + activation tape
+  static_assert(!(SAVED && WG), "weight gradients from saved masks run as k_color_wgrad");
+  if (SAVED) {  // masks from the forward: no recompute (the mask-only chain)
     uint32_t m[5];
     load_masks(a, DEC, tile, m, lane);
-    const f32x16 c = gather_tile(gr.data, cr, lane);
-    PHASE(DEC, 3);
-    color_backward_tape<WG>(pk, c, q.x, g, m, a.c.act_tape + tile * kTapeFloats, dg, A, S, lane, dc);
-  } else if (SAVED) {  // masks from the forward: no recompute (decoders without parameter gradients)
-    uint32_t m[5];
-    load_masks(a, DEC, tile, m, lane);
-    if (DEC == NSLAM_DEC_COARSE)
+    if (DEC == NSLAM_DEC_COARSE) {
       noxyz_backward_saved(pk, m, g[3], lane, dc);
-    else if (DEC == NSLAM_DEC_FINE)
+    } else if (DEC == NSLAM_DEC_FINE) {
       xyz_backward_saved<2, 1, 3, PG>(pk, m, q.x, g, lane, dc, gx);
-    else if (DEC == NSLAM_DEC_COLOR)
-      xyz_backward_saved<1, 3, 0, PG>(pk, m, q.x, g, lane, dc, gx);
-    else
+    } else if (DEC == NSLAM_DEC_COLOR) {  // + the cotangent tape of a colour weight-gradient backward
+      xyz_backward_saved<1, 3, 0, PG>(pk, m, q.x, g, lane, dc, gx, a.cot ? a.cot + tile * kCotFloats : nullptr);
+      if (a.cot) {  // x (half 0) and g (half 1) of point p; g is 0 past the end
+        const f32x4 v = h == 0 ? f32x4{q.x[0], q.x[1], q.x[2], 0.f} : f32x4{g[0], g[1], g[2], 0.f};
+        *reinterpret_cast<__attribute__((address_space(1))) f32x4*>(as_global_w(a.cot) + tile * kCotFloats + kCotXg +
+                                                                    p * 8 + 4 * h) = v;
+      }
+    } else {
       xyz_backward_saved<1, 1, 3, PG>(pk, m, q.x, g, lane, dc, gx);
+    }
   } else if (DEC == NSLAM_DEC_COARSE) {
     const f32x16 c = gather_tile(gr.data, cr, lane);
     noxyz_backward<WG>(pk, c, g[3], dg, A, S, lane, dc);
@@ -1448,13 +1330,10 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
 #else
   if (gr.grad) {
 #endif
-    if (WG && !SAVED) {
+    if (WG) {
       scatter_grid_grad_halves(gr.grad, gr.slot, cr, dc, q.valid, S, lane);
-    } else {
-      // the tape kernel (256 VGPRs) resolves its corners here rather than across the backward
-      if (WG) scn = resolve_corners(gr.slot, cr, q.valid, lane);
-      // walk table: the lean kernels' slot after the transpose image, the tape kernel's sX
-      scatter_grid_grad_uniform(gr.grad, scn, cr.cell, dc, S.sA, WG ? S.sX : S.sA + TILE_FLOATS, lane);
+    } else {  // walk table: the lean kernels' slot after the transpose image
+      scatter_grid_grad_uniform(gr.grad, scn, cr.cell, dc, S.sA, S.sA + TILE_FLOATS, lane);
     }
   }
   PHASE(DEC, 13);
@@ -1479,13 +1358,12 @@ __global__ __launch_bounds__(64 * kWavesBwd, (WG || PG || !SAVED) ? 2 : NSLAM_LE
   // per-wave scratch: the scatter needs sA + corner rows/weights; weight gradients add sX and
   // the per-point tables (sizing LDS per variant keeps the lean kernels at 5+ waves/SIMD)
   // (the lean kernels' scatter walk needs only the sA transpose image and its walk table)
-  constexpr int kScr = WG ? kScratchFloats + (SAVED ? TILE_FLOATS : 0) : TILE_FLOATS + kWalkFloats;
+  constexpr int kScr = WG ? kScratchFloats : TILE_FLOATS + kWalkFloats;
   __shared__ __attribute__((aligned(16))) float lds[kWavesBwd * kScr];
   const int lane = threadIdx.x & 63, wave = wave_id();
   float* sc = lds + wave * kScr;
   Scratch S;
   S.sA = sc;
-  S.sD3 = nullptr;
   if (WG) {
     S.sX = sc + TILE_FLOATS;
     S.gtab = sc + 2 * TILE_FLOATS;
@@ -1493,7 +1371,6 @@ __global__ __launch_bounds__(64 * kWavesBwd, (WG || PG || !SAVED) ? 2 : NSLAM_LE
     S.crow = reinterpret_cast<int*>(S.xtab + 32 * 3);
     S.cw = reinterpret_cast<float*>(S.crow + 32 * 8);
     S.ccell = reinterpret_cast<int*>(S.cw + 32 * 8);
-    if (SAVED) S.sD3 = reinterpret_cast<float*>(S.ccell + 32);
   } else {
     S.sX = S.gtab = S.xtab = S.cw = nullptr;
     S.crow = S.ccell = nullptr;
@@ -1536,47 +1413,24 @@ struct MultiDecArgs {
   int dec[4];
   double* gp[4];
 };
-// CW: one of the parts is the colour decoder WITH its weight gradients (activation-tape backward,
-// one slab per wave folded per workgroup exactly as k_dec_bwd<COLOR, 1, .., SAVED>); the launch
-// then takes that kernel's registers and LDS for every part.
-template <bool PG, bool CW>
-__global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd_multi(QueryKArgs a, MultiDecArgs m,
-                                                                       float* __restrict__ slab, int acc_floats) {
-  constexpr int kScr = CW ? kScratchFloats + TILE_FLOATS : TILE_FLOATS + kWalkFloats;
+// The colour decoder may be a part WITH weight gradients: its tiles run the same mask-only chain
+// and store their cotangents in a.cot (k_color_wgrad, launched after this kernel, forms the
+// weight gradients), so every part is lean and the launch keeps the lean kernels' occupancy.
+template <bool PG>
+__global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd_multi(QueryKArgs a, MultiDecArgs m) {
+  constexpr int kScr = TILE_FLOATS + kWalkFloats;
   __shared__ __attribute__((aligned(16))) float lds[kWavesBwd * kScr];
   const int lane = threadIdx.x & 63, wave = wave_id();
   Scratch S;
   S.sA = lds + wave * kScr;
-  S.sX = S.sD3 = S.gtab = S.xtab = S.cw = nullptr;
+  S.sX = S.gtab = S.xtab = S.cw = nullptr;
   S.crow = S.ccell = nullptr;
   const int part = (int)(blockIdx.x % (unsigned)m.ndec);
   // selects, not a dynamic index into the by-value argument (that would copy it to scratch)
   const int dec = part == 0 ? m.dec[0] : part == 1 ? m.dec[1] : part == 2 ? m.dec[2] : m.dec[3];
   double* gp = part == 0 ? m.gp[0] : part == 1 ? m.gp[1] : part == 2 ? m.gp[2] : m.gp[3];
-  const int64_t w0 = (int64_t)(blockIdx.x / (unsigned)m.ndec) * kWavesBwd;
-  const int64_t w = w0 + wave;
+  const int64_t w = (int64_t)(blockIdx.x / (unsigned)m.ndec) * kWavesBwd + wave;
   const int64_t ntiles = (a.n + 31) / 32;
-  if (CW && dec == NSLAM_DEC_COLOR && a.c.dgrad[NSLAM_DEC_COLOR].base) {
-    S.sX = S.sA + TILE_FLOATS;
-    S.gtab = S.sA + 2 * TILE_FLOATS;
-    S.xtab = S.gtab + 32 * 4;
-    S.crow = reinterpret_cast<int*>(S.xtab + 32 * 3);
-    S.cw = reinterpret_cast<float*>(S.crow + 32 * 8);
-    S.ccell = reinterpret_cast<int*>(S.cw + 32 * 8);
-    S.sD3 = reinterpret_cast<float*>(S.ccell + 32);
-    const Slab A = make_slab(slab + (size_t)w * acc_floats, acc_floats);
-    if (w < ntiles) dec_bwd_tile<NSLAM_DEC_COLOR, 1, false, true, true>(a, w, A, S, lane, nullptr);
-    __syncthreads();  // fold the workgroup's slabs into its first one (k_dec_bwd, WG == 1)
-    const int nv = (int)(ntiles - w0 < kWavesBwd ? ntiles - w0 : kWavesBwd);
-    f32x4* s0 = reinterpret_cast<f32x4*>(slab + (size_t)w0 * acc_floats);
-    const int q = acc_floats / 4;
-    for (int i = threadIdx.x; i < q; i += blockDim.x) {
-      f32x4 t = s0[i];
-      for (int v = 1; v < nv; ++v) t += s0[(size_t)v * q + i];
-      s0[i] = t;
-    }
-    return;
-  }
   if (w >= ntiles) return;
   const Slab A = make_slab(nullptr, 0);
   switch (dec) {
@@ -1600,7 +1454,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_bwd_multi_sum(QueryKArgs a, Mult
   const int64_t tile = blockIdx.x;
   Scratch S;
   S.sA = lds + part * kScr;
-  S.sX = S.sD3 = S.gtab = S.xtab = S.cw = nullptr;
+  S.sX = S.gtab = S.xtab = S.cw = nullptr;
   S.crow = S.ccell = nullptr;
   for (int i = lane; i < 96; i += 64) stage[part][i] = 0.0;
   __syncthreads();
@@ -1691,6 +1545,32 @@ inline int hip_status() {
 
 inline int acc_floats_of(const nslam_dec_grad& dg) { return (int)((dg.count + 3) & ~int64_t(3)); }
 
+// ---- the colour decoder's weight gradients from the tapes (k_color_wgrad, nslam_color_wgrad.hip) --
+// With the forward's activation tape and ReLU masks, the colour decoder's backward is two launches:
+// the lean mask-only chain (grid gradient; it also stores the cotangent tape) and k_color_wgrad, a
+// split-K reduction over tile chunks of every weight block (one 8-wave workgroup per chunk, the
+// tiles staged through LDS; each chunk's partial sums fill one slab), then k_slab_reduce over the
+// chunks.  Workspace: [cotangent tape | chunk slabs].
+constexpr int kCwTargetChunks = 256;  // one workgroup per CU (its LDS holds two staged tiles)
+struct CwPlan {
+  int64_t chunk_tiles;
+  int nchunks;
+  size_t cot_bytes, slab_bytes;
+};
+inline CwPlan cw_plan(const nslam_dec_grad& dg, int64_t n_pts) {
+  CwPlan p;
+  const int64_t tiles = (n_pts + 31) / 32;
+  p.chunk_tiles = (tiles + kCwTargetChunks - 1) / kCwTargetChunks;
+  p.nchunks = (int)((tiles + p.chunk_tiles - 1) / p.chunk_tiles);
+  p.cot_bytes = ((size_t)tiles * kCotFloats * sizeof(float) + 255) & ~(size_t)255;
+  p.slab_bytes = (size_t)p.nchunks * acc_floats_of(dg) * sizeof(float);
+  return p;
+}
+inline bool cw_tape_path(const nslam_query_cfg* c) { return c->act_tape != nullptr && c->saved_masks != nullptr; }
+// k_color_wgrad + k_slab_reduce into a.c.dgrad[COLOR] after the lean chain has filled the cotangent
+// tape at ws (a.cot is set from ws); nslam_color_wgrad.hip
+int launch_color_wgrad(const QueryKArgs& a, float* ws, hipStream_t s);
+
 // Slab cap: kMaxSlabs, or NSLAM_MAX_SLABS from the environment (tests use it to reach the
 // multi-tile read-modify-write mode at small sizes).
 inline int64_t max_slabs() {
@@ -1738,22 +1618,16 @@ int launch_dec_bwd(const QueryKArgs& a, bool first, float* slab, hipStream_t s) 
   const int acc = acc_floats_of(dg);
   const int64_t nslab = n_slabs(tiles);
   const int64_t blocks = (nslab + kWavesBwd - 1) / kWavesBwd;
-  // the colour decoder's weight gradients read the forward's activation tape when it is there
+  // the colour decoder's weight gradients read the forward's activation tape when it is there:
+  // the lean chain (+ cotangent tape) then k_color_wgrad
   constexpr bool kTapeable = DEC == NSLAM_DEC_COLOR && !PG;
-  const bool tape = kTapeable && a.c.act_tape && a.c.saved_masks;
   int rc;
   if constexpr (kTapeable) {
-    if (tape) {
-      if (tiles <= max_slabs())
-        rc = first ? launch_one<DEC, 1, PG, true, true>(a, slab, acc, blocks, s)
-                   : launch_one<DEC, 1, PG, false, true>(a, slab, acc, blocks, s);
-      else
-        rc = (hipMemsetAsync(slab, 0, (size_t)nslab * acc * sizeof(float), s) != hipSuccess)
-                 ? hip_status()
-                 : (first ? launch_one<DEC, 2, PG, true, true>(a, slab, acc, blocks, s)
-                          : launch_one<DEC, 2, PG, false, true>(a, slab, acc, blocks, s));
-      if (rc) return rc;
-      return slab_reduce(dg, slab, tiles <= max_slabs(), nslab, blocks, acc, s);
+    if (cw_tape_path(&a.c)) {
+      QueryKArgs b = a;
+      b.cot = slab;
+      rc = launch_one<DEC, 0, false, true, true>(b, nullptr, 0, (tiles + kWavesBwd - 1) / kWavesBwd, s);
+      return rc ? rc : launch_color_wgrad(a, slab, s);
     }
   }
   if (tiles > max_slabs() && hipMemsetAsync(slab, 0, (size_t)nslab * acc * sizeof(float), s) != hipSuccess)
@@ -1789,22 +1663,23 @@ int dispatch_dec_bwd(const QueryKArgs& a, bool first, float* slab, hipStream_t s
   return launch_dec_bwd<DEC, 0, false>(a, first, slab, s);
 }
 
-inline size_t bwd_ws_bytes(const nslam_query_cfg* cfg, int64_t n_pts) {
-  size_t need = 0;
-  const int64_t tiles = (n_pts + 31) / 32;
-  for (int d = 0; d < 4; ++d) {
-    const nslam_dec_grad& dg = cfg->dgrad[d];
-    if (!dg.base || dg.count <= 0) continue;
-    const size_t b = (size_t)n_slabs(tiles) * acc_floats_of(dg) * sizeof(float);
-    need = b > need ? b : need;  // decoders run one after the other on the stream: one region
-  }
-  return need;
-}
-
 inline size_t dec_ws_bytes(const nslam_query_cfg* cfg, int dec, int64_t n_pts) {
   const nslam_dec_grad& dg = cfg->dgrad[dec];
   if (!dg.base || dg.count <= 0) return 0;
+  if (dec == NSLAM_DEC_COLOR && cw_tape_path(cfg)) {
+    const CwPlan p = cw_plan(dg, n_pts);
+    return p.cot_bytes + p.slab_bytes;
+  }
   return (size_t)n_slabs((n_pts + 31) / 32) * acc_floats_of(dg) * sizeof(float);
+}
+
+inline size_t bwd_ws_bytes(const nslam_query_cfg* cfg, int64_t n_pts) {
+  size_t need = 0;
+  for (int d = 0; d < 4; ++d) {
+    const size_t b = dec_ws_bytes(cfg, d, n_pts);
+    need = b > need ? b : need;  // decoders run one after the other on the stream: one region
+  }
+  return need;
 }
 
 inline bool stage_uses(int stage, int dec) {

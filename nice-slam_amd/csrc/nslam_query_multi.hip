@@ -18,12 +18,12 @@ extern "C" int nslam_query_bwd_decoders(const nslam_query_cfg* cfg, int32_t dec_
   if (cfg->rays_o && (n_pts >= (int64_t(1) << 31) || n_pts % cfg->n_samples)) return NSLAM_EINVAL;
   if (cfg->need_pts_grad && n_pts > 0 && !g_pts) return NSLAM_EINVAL;
   MultiDecArgs m{};
-  bool cw = false;  // the colour decoder's weight gradients are part of the launch
+  bool cw = false;  // the colour decoder's weight gradients are part of the call
   for (int d = 0; d < 4; ++d) {
     if (!((dec_mask >> d) & 1)) continue;
     if (!stage_uses(cfg->stage, d)) return NSLAM_EINVAL;
     if (cfg->dgrad[d].base) {
-      // only the colour decoder's activation-tape backward joins a merged launch
+      // only the colour decoder's tape backward joins a merged launch (as its lean chain + k_color_wgrad)
       if (d != NSLAM_DEC_COLOR || cfg->need_pts_grad || !cfg->act_tape || cfg->dgrad[d].count <= 0)
         return NSLAM_EUNSUPPORTED;
       cw = true;
@@ -37,10 +37,7 @@ extern "C" int nslam_query_bwd_decoders(const nslam_query_cfg* cfg, int32_t dec_
   if (n_pts == 0) return NSLAM_OK;
   const int64_t tiles = (n_pts + 31) / 32;
   const int64_t groups = (tiles + kWavesBwd - 1) / kWavesBwd;
-  const nslam_dec_grad& dg = cfg->dgrad[NSLAM_DEC_COLOR];
-  const int acc = cw ? acc_floats_of(dg) : 0;
   if (cw) {
-    if (tiles > max_slabs()) return NSLAM_EUNSUPPORTED;  // one slab per tile only
     const size_t need = dec_ws_bytes(cfg, NSLAM_DEC_COLOR, n_pts);
     if (!ws || ws_bytes < need) return NSLAM_EWORKSPACE;
   }
@@ -52,14 +49,12 @@ extern "C" int nslam_query_bwd_decoders(const nslam_query_cfg* cfg, int32_t dec_
     return hip_status();
   }
   const dim3 grid((unsigned)(groups * m.ndec)), block(64 * kWavesBwd);
-  float* slab = reinterpret_cast<float*>(ws);
-  if (cw)
-    hipLaunchKernelGGL((k_dec_bwd_multi<false, true>), grid, block, 0, s, a, m, slab, acc);
-  else if (cfg->need_pts_grad)
-    hipLaunchKernelGGL((k_dec_bwd_multi<true, false>), grid, block, 0, s, a, m, nullptr, 0);
+  if (cw) a.cot = reinterpret_cast<float*>(ws);  // the colour part stores its cotangent tape
+  if (cfg->need_pts_grad)
+    hipLaunchKernelGGL((k_dec_bwd_multi<true>), grid, block, 0, s, a, m);
   else
-    hipLaunchKernelGGL((k_dec_bwd_multi<false, false>), grid, block, 0, s, a, m, nullptr, 0);
+    hipLaunchKernelGGL((k_dec_bwd_multi<false>), grid, block, 0, s, a, m);
   const int lrc = hip_status();
   if (lrc || !cw) return lrc;
-  return slab_reduce(dg, slab, true, tiles, groups, acc, s);  // one folded slab per colour workgroup
+  return launch_color_wgrad(a, reinterpret_cast<float*>(ws), s);
 }

@@ -11,3 +11,4 @@ template int dispatch_dec_bwd<NSLAM_DEC_COLOR>(const QueryKArgs&, bool, float*, 
 }  // namespace nslamq
 
 #include "nslam_query_multi.hip"
+#include "nslam_color_wgrad.hip"

@@ -331,7 +331,11 @@ class MappingEngine:
         device draw counter, not on the map.  Batches alternate between two persistent buffer sets
         (self._parity), so a hipGraph of an even and one of an odd iteration replay alternately
         with no copies.  Each call still draws, samples, renders and updates one batch; the first
-        call draws its own batch first.
+        call draws its own batch first.  The prefetched batch belongs to the frames of the call that
+        drew it: a call with other frames (another keyframe window, or poses changed in place, e.g.
+        by bundle adjustment — tracked by the tensors' identity and version counters) discards it
+        and draws its own batch.  With prefetch the returned `keep` is a persistent buffer, valid
+        until the next iteration() call (which overwrites it): clone it to keep it longer.
         """
         H, W = hw
         fx, fy, cx, cy = intrinsics
@@ -360,7 +364,10 @@ class MappingEngine:
         prefetch = prefetch and pix is None
         side = None
         if prefetch:
-            pkey = (stage, len(frames), n_per, hw, use_gt_in_sampler, seed, world, rank)
+            # the frames' identity and version counters: a prefetched batch is only valid for the very
+            # frames (images and poses, unmodified) it was gathered from
+            fkey = tuple((t.data_ptr(), t._version) for f in frames for t in f)
+            pkey = (stage, fkey, n_per, hw, use_gt_in_sampler, seed, world, rank)
             if self._pre is None or self._pre[0] != pkey:
                 first = rays()  # first call: this iteration's batch (set 0), then a same-shaped set 1
                 self._pre = (pkey, [first, [torch.empty_like(t) for t in first]])

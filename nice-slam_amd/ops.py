@@ -597,7 +597,6 @@ class FusedAdam:
             for p in g["params"]:
                 dev = p.device
         self.device = dev
-        self.ticket = torch.zeros(1, dtype=torch.int32, device=dev) if dev is not None else None
         self._tickets = {}  # one step ticket per parameter subset (subsets may step concurrently)
         self.mirrors = {}
 
@@ -666,7 +665,12 @@ class FusedAdam:
         b1, b2 = self.betas
         key = tuple(id(p) for _, p, _ in segs)
         ticket = self._tickets.get(key)
-        if ticket is None:  # first step of this subset (eager, before any graph capture)
+        if ticket is None:
+            # a ticket made during capture would come from the graph's private pool with its zero-fill
+            # baked into the graph: every subset must step once eagerly first
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("FusedAdam: first step of a parameter subset inside graph capture; "
+                                   "run one eager step of it before capturing")
             ticket = self._tickets[key] = torch.zeros(1, dtype=torch.int32, device=self.device)
         with _span("adam"):
             rc = lib().nslam_adam_step(arr, len(segs), b1, b2, self.eps, int(bool(zero_grad)), ptr(ticket),

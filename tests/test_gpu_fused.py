@@ -644,3 +644,27 @@ def test_merged_frozen_backward_matches_per_decoder_launches(tiny):
     assert float(grads[False].abs().sum()) > 0
     assert torch.equal(grads[True], grads[False])
     assert torch.equal(grads["nosum"], grads[False])
+
+
+def test_engine_prefetch_discards_batch_of_other_frames(tiny):
+    """A prefetched batch belongs to the frames it was gathered from: a call with another keyframe
+    window (or with poses changed in place) draws its own batch from its own frames."""
+    sc, frames = _frames(tiny)
+    nice, c = _nice(sc)
+    eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV)
+    opt = P.ops.FusedAdam([{"params": [eng.decs["color"].param], "lr": 0.005}] +
+                          [{"params": [c[k]], "lr": 0.005} for k in ("grid_middle", "grid_fine", "grid_color")])
+    args = (None, 150, (96, 128), (sc.fx, sc.fy, sc.cx, sc.cy), opt)
+    eng.iteration("color", frames, *args, seed=11, prefetch=True)
+    moved = [(d, col, m.clone()) for d, col, m in frames]
+    for f, (_, _, m) in enumerate(moved):
+        m[:3, 3] += 0.05 * (f + 1)
+    eng.iteration("color", moved, *args, seed=11, prefetch=True)   # another window: fresh batch (set 0)
+    ro = eng._pre[1][0][0].view(len(moved), 150, 3)
+    for f, (_, _, m) in enumerate(moved):
+        assert torch.equal(ro[f], m[:3, 3].expand(150, 3)), f
+    with torch.no_grad():
+        moved[0][2][:3, 3] += 0.01                                     # a pose updated in place
+    eng.iteration("color", moved, *args, seed=11, prefetch=True)
+    ro = eng._pre[1][0][0].view(len(moved), 150, 3)
+    assert torch.equal(ro[0], moved[0][2][:3, 3].expand(150, 3))
