@@ -37,6 +37,11 @@ ROOM0 = {
     "pixels": 1000, "window": 5, "n_strat": 32, "n_surf": 16, "w_color": 0.2,
     "lr": {"decoders": 0.005, "middle": 0.005, "fine": 0.005, "color": 0.005},
 }
+# configs[4] (BASELINE.json): synthetic 8 m cube, fine / colour grids 512^3 x 32 (16 GiB each), middle
+# 256^3, 65536 pixels (4 frames x 16384) x 64 samples (48 stratified + 16 surface), colour stage
+STRESS = dict(ROOM0, bound=[[0.0, 7.9]] * 3, bound_divisible=0.5,
+              grid_len={"coarse": 2.0, "middle": 1 / 32, "fine": 1 / 64, "color": 1 / 64},
+              pixels=65536, window=4, n_strat=48, n_surf=16)
 FLOP_FWD_PER_SAMPLE = 2 * (15479 + 20599 + 15575)   # SURVEY §8(a10) MACs, colour stage
 FLOP_FINE_STAGE_PER_POINT = 2 * (15479 + 20599)          # fine stage: middle + fine decoders
 BYTES_FWD_PER_SAMPLE = 3 * 1024                      # 3 trilinear lookups × 8 corners × 128 B
@@ -57,28 +62,35 @@ KERNEL_WORK = {
     "query_bwd.middle+fine": (2 * 15479 + 2 * 20599, 2 * 2048),
     "query_bwd.color+middle+fine": (2 * 15479 + 2 * 20599 + 2 * 2 * 15575, 3 * 2048),
 }
+# The frozen decoders' mask-only backward launches are bound by their grid-gradient float atomics,
+# not by HBM or MFMA: 8 corners x 32 channels x 4 B = 1024 added bytes per ray-sample against the
+# chip-wide float-atomic rate of ~1.3 TB/s of added bytes (MI355X_MICROARCH.md, atomics table: every
+# CU issuing, any footprint or contention).  Their roofline is stated against that ceiling.
+ATOMIC_SPANS = {"query_bwd.fine": 1024, "query_bwd.middle": 1024, "query_bwd.middle+fine": 2048}
+ATOMIC_PEAK_GBS = 1300.0
 # rocprofv3 kernel names behind each span (for the PMC traffic of profiles/*traffic*.json)
 SPAN_KERNELS = {
     "query_fwd": ("k_query_fwd", "k_occ_combine"),
-    "query_bwd.color": ("k_dec_bwd<3,", "k_slab_reduce"),
+    "query_bwd.color": ("k_dec_bwd<3,", "k_color_wgrad", "k_slab_reduce"),
     "query_bwd.fine": ("k_dec_bwd<2,",),
     "query_bwd.middle": ("k_dec_bwd<1,",),
     "query_bwd.middle+fine": ("k_dec_bwd_multi<false, false>",),
     "query_bwd.color+middle+fine": ("k_dec_bwd_multi<false, true>", "k_slab_reduce"),
 }
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r02_traffic.json")
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r03_traffic.json")
+STRESS_TRAFFIC_FILE = os.path.join(REPO, "profiles", "r03_traffic_stress.json")
 
 
-def pmc_traffic(span):
+def pmc_traffic(span, path=None):
     """HBM bytes per launch of `span` from the committed PMC summary (tools/traffic.py: separate
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this bench, FETCH_SIZE doubled per the
     MI355X guide's gfx950 correction), or None when absent."""
     try:
-        with open(TRAFFIC_FILE) as f:
+        with open(path or TRAFFIC_FILE) as f:
             kern = json.load(f)["kernels"]
     except (OSError, ValueError, KeyError):
         return None
-    pats = SPAN_KERNELS.get(span, ())
+    pats = SPAN_KERNELS.get(span, (span,))
     hits = [v["hbm_bytes_per_launch"] for k, v in kern.items() if any(k.startswith(p) for p in pats)]
     return sum(hits) if hits else None
 
@@ -161,7 +173,7 @@ def capture_step_graphs(fn, block=10, sync=None):
 class Room0Scene:
     """Synthetic room0-shaped mapping workload (grids, decoders, 5 keyframes in HBM)."""
 
-    def __init__(self, dev, rank=0, cfg=ROOM0, path="fused"):
+    def __init__(self, dev, rank=0, cfg=ROOM0, path="fused", device_init=False):
         P = pkg()
         self.cfg, self.dev = cfg, dev
         g = torch.Generator().manual_seed(2)
@@ -169,8 +181,14 @@ class Room0Scene:
         std = {"middle": 0.01, "fine": 1e-4, "color": 0.01}
         self.grids = {}
         for k in ("middle", "fine", "color"):
-            t = torch.randn(grid_shape(self.bound, cfg["grid_len"][k]), generator=g) * std[k]
-            self.grids["grid_" + k] = t.to(dev).contiguous(memory_format=torch.channels_last_3d).requires_grad_(True)
+            shp = grid_shape(self.bound, cfg["grid_len"][k])
+            if device_init:  # stress grids (16 GiB): drawn on the device, channels-last directly
+                gd = torch.Generator(device=dev).manual_seed(2 + len(self.grids))
+                t = torch.empty(shp[0], shp[2], shp[3], shp[4], shp[1], device=dev).normal_(0.0, std[k], generator=gd)
+                t = t.permute(0, 4, 1, 2, 3)
+            else:
+                t = (torch.randn(shp, generator=g) * std[k]).to(dev).contiguous(memory_format=torch.channels_last_3d)
+            self.grids["grid_" + k] = t.requires_grad_(True)
         torch.manual_seed(3)
         self.nice = P.NICE(c_dim=32, coarse_grid_len=2.0, middle_grid_len=0.32, fine_grid_len=0.16,
                            color_grid_len=0.16, hidden_size=32, coarse=False)
@@ -319,8 +337,22 @@ class _Slam:
         self.H, self.W, self.fx, self.fy, self.cx, self.cy = cfg["H"], cfg["W"], cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"]
 
 
-def cpu_baseline(scene, budget_s=20.0):
-    """The oracle (torch CPU restatement, oracle/nslam_oracle.py) on the same workload, host cores."""
+def cpu_model():
+    """The host CPU's model name (lscpu's 'Model name', from /proc/cpuinfo)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(scene, budget_s=20.0, reps=5):
+    """The oracle (torch CPU restatement, oracle/nslam_oracle.py) on the same workload, host cores:
+    one warm-up iteration, then `reps` timed samples of a few iterations each (about budget_s in
+    all); value = the median sample's ray-samples/s (BASELINE.md's warm-up + median-of-5 plan)."""
     from oracle import nslam_oracle as orc
     threads = torch.get_num_threads()
     bound = scene.bound
@@ -330,24 +362,35 @@ def cpu_baseline(scene, budget_s=20.0):
         if k.startswith("color_decoder."):
             sd[k] = sd[k].clone().requires_grad_(True)
     opt = torch.optim.Adam([v for k, v in sd.items() if v.requires_grad] + list(grids.values()), lr=0.005)
-    samples, iters, t0 = 0, 0, time.perf_counter()
-    while iters < 2 or (time.perf_counter() - t0 < budget_s and iters < 50):
+
+    def iteration():
         ro, rd, gt, gc = (x.cpu() for x in scene.sample_batch())
         keep = orc.inside_mask(ro, rd, gt, bound)
         ro, rd, gt, gc = ro[keep], rd[keep], gt[keep], gc[keep]
-        if iters == 0:
-            t0 = time.perf_counter()  # first iteration = warm-up
         opt.zero_grad()
         d, v, c = orc.render_batch_ray(sd, grids, rd, ro, "color", bound, gt)
         orc.mapper_loss(d, c, gt, gc, "color").backward()
         opt.step()
-        if iters > 0:
-            samples += ro.shape[0] * 48
-        iters += 1
-    dt = time.perf_counter() - t0
-    return {"value": samples / dt, "unit": "ray-samples/s", "cores": threads, "kind": "port",
-            "sample": f"{iters - 1} colour-stage mapping iterations (1000 rays x 48 samples, fwd+bwd+Adam) after "
-                      f"1 warm-up, oracle/nslam_oracle.py on {threads} host threads, {dt:.1f} s"}
+        return ro.shape[0] * 48
+
+    t0 = time.perf_counter()
+    iteration()                                        # warm-up
+    per_iter = time.perf_counter() - t0
+    n = max(1, int(budget_s / reps / max(per_iter, 1e-3)))
+    rates, tot_iters, tot_s = [], 0, 0.0
+    for _ in range(reps):
+        samples, t0 = 0, time.perf_counter()
+        for _ in range(n):
+            samples += iteration()
+        dt = time.perf_counter() - t0
+        rates.append(samples / dt)
+        tot_iters, tot_s = tot_iters + n, tot_s + dt
+    rates.sort()
+    return {"value": rates[reps // 2], "unit": "ray-samples/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "samples_per_s_all": rates,
+            "sample": f"median of {reps} samples of {n} colour-stage mapping iterations each (1000 rays x 48 "
+                      f"samples, fwd+bwd+Adam) after 1 warm-up, oracle/nslam_oracle.py on {threads} host threads "
+                      f"({cpu_model()}), {tot_iters} iterations in {tot_s:.1f} s"}
 
 
 def stress_grid_query(dev, side=512, rays=65536, samples=64, reps=10):
@@ -377,11 +420,71 @@ def stress_grid_query(dev, side=512, rays=65536, samples=64, reps=10):
     achieved = n * bpp / (tm["avg_ms"] * 1e-3) / 1e9
     del grid, out, coords
     torch.cuda.empty_cache()
-    return {"kernel": "k_grid_fwd (nslam_grid_sample_fwd)", "bound": "hbm", "achieved": achieved,
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+    traffic = pmc_traffic("k_grid_fwd", STRESS_TRAFFIC_FILE)
+    # frac on the PMC-counted HBM bytes (FETCH_SIZE x2 + WRITE_SIZE per launch) when the committed
+    # summary has them: the algorithmic count includes L2 / MALL reuse between a ray's samples
+    counted = traffic / (tm["avg_ms"] * 1e-3) / 1e9 if traffic else None
+    return {"kernel": "k_grid_fwd (nslam_grid_sample_fwd)", "bound": "hbm",
+            "achieved": counted if counted else achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": (counted if counted else achieved) / HBM_PEAK_GBS, "frac_basis": "pmc" if counted else "algorithmic",
+            "achieved_algorithmic": achieved, "frac_algorithmic": achieved / HBM_PEAK_GBS, "traffic": traffic,
             "avg_launch_ms": tm["avg_ms"], "points": n, "bytes_per_point": bpp,
             "workload": f"grid [1,32,{side},{side},{side}] fp32 channels-last (16 GiB), {rays} rays x {samples} "
                         "samples, random rays through the cube"}
+
+
+def stress_iteration(dev, steps=10):
+    """configs[4] as a whole mapping iteration on the fused engine (SURVEY §8(d) stress row): the
+    colour-stage iteration of the room0 bench at the stress shape — 8 m cube, fine / colour grids
+    512^3 x 32 (16 GiB each), middle 256^3, 65536 pixels over 4 frames x 64 samples, frustum-masked
+    Adam — replayed in a hipGraph.  Per-kernel HIP-event spans come from extra eager iterations;
+    the forward's 3 trilinear lookups (3 KiB per sample) are priced against the HBM roof, its FLOPs
+    against the fp32 MFMA roof."""
+    scene = Room0Scene(dev, 0, cfg=dict(STRESS), path="fused", device_init=True)
+    P = pkg()
+    for _ in range(2):
+        scene.step()
+    torch.cuda.synchronize()
+    if os.environ.get("NSLAM_BENCH_EAGER"):  # PMC passes (tools/gpu_traffic_stress.sh): per-dispatch counters
+        g, mode = None, "eager"
+    else:
+        g, mode = capture_step_graphs(scene.step, block=2, sync=scene.flip_parity)
+        g.run(2)
+    torch.cuda.synchronize()
+    scene.kept.zero_()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    if g is not None:
+        g.run(steps)
+    else:
+        for _ in range(steps):
+            scene.step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if g is not None:
+        g.finish()
+    samples = int(scene.kept) * (STRESS["n_strat"] + STRESS["n_surf"])
+    P.ops.TIMER = P.ops.KernelTimer()
+    for _ in range(3):
+        scene.step()
+    timers = P.ops.TIMER.summary()
+    P.ops.TIMER = None
+    pts = samples / steps
+    fwd = timers["query_fwd"]["avg_ms"] * 1e-3
+    rows = {k: int(v.numel()) for k, v in scene.rows.items()}
+    out = {"value": samples / dt, "unit": "ray-samples/s", "ms_per_iteration": dt / steps * 1e3, "steps": steps,
+           "launch_mode": mode, "ray_samples_per_iteration": pts,
+           "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in timers.items()},
+           "query_fwd_roofline": kernel_roofline("query_fwd", timers["query_fwd"]["avg_ms"], pts, STRESS_TRAFFIC_FILE),
+           "query_fwd_gather_gbs": pts * BYTES_FWD_PER_SAMPLE / fwd / 1e9,
+           "query_fwd_gather_hbm_frac": pts * BYTES_FWD_PER_SAMPLE / fwd / 1e9 / HBM_PEAK_GBS,
+           "frustum_rows": rows,
+           "workload": "configs[4]: 8 m cube, grids middle 256^3 / fine 512^3 / colour 512^3 x 32 fp32 "
+                       "channels-last, 65536 pixels (4 frames x 16384) x 64 samples, colour stage, Adam on "
+                       "the frustum rows"}
+    del scene
+    torch.cuda.empty_cache()
+    return out
 
 
 def bulk_queries(scene, res=256, reps=2):
@@ -513,23 +616,34 @@ def reference_gpu_baseline(scene, budget_s=4.0):
                       "(torch ops of the reference path) on the GPU, eager"}
 
 
-def kernel_roofline(name, avg_ms, pts):
+def kernel_roofline(name, avg_ms, pts, traffic_path=None):
     """Roofline of one timed launch: algorithmic FLOPs and bytes (KERNEL_WORK × ray-samples per
     launch) over its HIP-event average; the bound is whichever roof (fp32 MFMA, HBM) the
-    algorithmic work would hit first."""
+    algorithmic work would hit first — or, for the frozen decoders' mask-only backward, the
+    chip-wide float-atomic rate its grid-gradient scatter is bound by (ATOMIC_SPANS)."""
     fl, by = KERNEL_WORK[name]
     t = avg_ms * 1e-3
     tflops, gbs = pts * fl / t / 1e12, pts * by / t / 1e9
     mfma = fl / (F32_PEAK_TFLOPS * 1e12) >= by / (HBM_PEAK_GBS * 1e9)
     achieved, peak, unit = (tflops, F32_PEAK_TFLOPS, "TFLOP/s") if mfma else (gbs, HBM_PEAK_GBS, "GB/s")
-    return {"kernel": name, "bound": "mfma" if mfma else "hbm", "achieved": achieved, "peak": peak, "unit": unit,
-            "frac": achieved / peak, "traffic": pmc_traffic(name), "avg_launch_ms": avg_ms,
-            "ray_samples_per_launch": pts, "flop_per_sample": fl, "bytes_per_sample": by,
+    bound = "mfma" if mfma else "hbm"
+    extra = {}
+    if name in ATOMIC_SPANS:
+        bound, achieved, peak, unit = "atomic", pts * ATOMIC_SPANS[name] / t / 1e9, ATOMIC_PEAK_GBS, "GB/s"
+        extra = {"atomic_bytes_per_sample": ATOMIC_SPANS[name],
+                 "atomic_note": "float-atomic adds into the grid gradient (8 corners x 32 ch x 4 B per sample "
+                                "before the scatter walk merges runs) against ~1.3 TB/s of added bytes chip-wide "
+                                "(MI355X_MICROARCH.md atomics table); mfma_frac = input-gradient FLOPs vs fp32 peak",
+                 "mfma_frac": tflops / F32_PEAK_TFLOPS}
+    tp = traffic_path or TRAFFIC_FILE
+    return {"kernel": name, "bound": bound, "achieved": achieved, "peak": peak, "unit": unit,
+            "frac": achieved / peak, "traffic": pmc_traffic(name, tp), "avg_launch_ms": avg_ms,
+            "ray_samples_per_launch": pts, "flop_per_sample": fl, "bytes_per_sample": by, **extra,
             # the HIP-event span brackets these rocprofv3 kernels back to back: compare its average
-            # with the SUM of their average durations in profiles/r02_room0_kernels.md
+            # with the SUM of their average durations in the rocprof summary under profiles/
             "rocprof_kernels": list(SPAN_KERNELS.get(name, ())),
             "traffic_note": "HBM bytes per launch: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, "
-                            "profiles/r02_traffic.json"}
+                            + os.path.relpath(tp, REPO)}
 
 
 def room0_frame_rate(scene, reps=100):
@@ -595,6 +709,8 @@ def leg_main(leg):
     dev = torch.device("cuda", 0)
     if leg == "stress":
         res = stress_grid_query(dev)
+    elif leg == "stress_iter":
+        res = stress_iteration(dev)
     elif leg == "frame_io":
         res = frame_io(dev)
     else:
@@ -640,7 +756,7 @@ def main():
                     help="fused engine (default) or the autograd drop-in path")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="draw + sample each iteration's rays inside it (no overlap with the previous backward)")
-    ap.add_argument("--leg", choices=("frames", "stress", "bulk", "frame_io"), default=None,
+    ap.add_argument("--leg", choices=("frames", "stress", "stress_iter", "bulk", "frame_io"), default=None,
                     help="run one auxiliary measurement and print its JSON (bench.py spawns these itself)")
     args = ap.parse_args()
     global PREFETCH
@@ -747,6 +863,7 @@ def main():
             out["room0"] = run_leg("frames")
         if world == 1 and not args.no_stress:
             out["grid_query_stress"] = run_leg("stress")
+            out["stress_iteration"] = run_leg("stress_iter")
         if world == 1 and not args.no_bulk:
             out["bulk_forward"] = run_leg("bulk")
             out["frame_io"] = run_leg("frame_io")

@@ -309,6 +309,30 @@ __device__ __forceinline__ f32x16 gather_tile(const float* __restrict__ grid, co
   return acc;
 }
 
+// gather_tile with at most NB corners' loads in flight (a scheduling fence between batches): for a
+// gather whose result is only stored, in a kernel whose register budget is set elsewhere
+template <int NB>
+__device__ __forceinline__ f32x16 gather_tile_batched(const float* __restrict__ grid, const Corners& c, int lane) {
+  const int h = lane >> 5;
+  f32x16 acc = zero16();
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (k % NB == 0) __builtin_amdgcn_sched_barrier(0);
+    const gptr_t<f32x4> row = as_global(reinterpret_cast<const f32x4*>(grid + (size_t)c.row[k] * NSLAM_C_DIM + 4 * h));
+    const f32x4 v0 = row[0], v1 = row[2], v2 = row[4], v3 = row[6];
+    const float w = c.w[k];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc[j] += v0[j] * w;
+      acc[4 + j] += v1[j] * w;
+      acc[8 + j] += v2[j] * w;
+      acc[12 + j] += v3[j] * w;
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  return acc;
+}
+
 // d out / d (normalised coords) for cotangent tile g (this lane's 16 channels; caller adds the
 // other half with xor32 and multiplies by gmul)
 __device__ __forceinline__ void coord_grad_partial(const float* __restrict__ grid, const Corners& c,

@@ -154,13 +154,24 @@ __device__ __forceinline__ void load_masks(const QueryKArgs& a, int dec, int64_t
 // Activation tape of the colour decoder (ABI v9 nslam_query_cfg.act_tape): the forward stores the
 // post-ReLU hidden tiles h0..h4 of every tile (C layout) and the weight-gradient backward reads them
 // instead of recomputing the decoder (it needs them as the inputs of dW; Mapper.py:503).
-constexpr int kTapeFloats = 6 * 16 * 64;  // per tile: h0..h4 and (slot 5) the colour feature c
-constexpr int kTapeFeat = 5;
-// Cotangent tape of the colour decoder's weight-gradient backward: dh_0..dh_4 (the cotangents of
-// the five hidden layers before their ReLU masks) of every tile, in the activation tape's layout,
+constexpr int kTapeFloats = 5 * 16 * 64;  // per tile: h0..h4
+// Cotangent tape of the colour decoder's weight-gradient backward, written by the lean chain, in the
+// activation tape's point-major layout ([32 points][32 features] per slot):
+//   slots 0-4  dh_0..dh_4, the cotangents of the five hidden layers before their ReLU masks
+//   slots 5-7  Gc_b = (L3_b^T da_3 + L0_b^T da_0) ⊙ cos(x B_b): the embedding cotangent times the
+//              sin derivative (dims 32b..32b+31, b = 0..2), the operand of dB
+//   slots 8-10 S_b = sin(x B_b), the embedding itself (the input of dW_0 and of dW_3's first 93
+//              columns): sin and cos by one range reduction, bit-identical to the forward's
+//   slot 11    the colour feature c (the fc_c weight gradients' input)
 // then a [32 points][8] block of x (float, 3 + pad) and the colour cotangent g (3 + pad): every
-// tile is 21 KiB of whole 1-KiB pieces (k_color_wgrad stages them by LDS-DMA).
-constexpr int kCotXg = 5 * 16 * 64;
+// tile is 49 KiB of whole 1-KiB pieces (k_color_wgrad stages them by LDS-DMA).
+#ifndef NSLAM_CGATHER_NB
+#define NSLAM_CGATHER_NB 4  // corners in flight of the lean chain's colour-feature gather
+#endif
+constexpr int kCotG = 5;
+constexpr int kCotS = 8;
+constexpr int kCotC = 11;
+constexpr int kCotXg = 12 * 16 * 64;
 constexpr int kCotFloats = kCotXg + 32 * 8;
 // Layout [tile][layer][register r][64 lanes] float: every store / load instruction moves 256 B
 // contiguous, and no 4-register grouping of the tile is needed (a float4 layout cost the forward
@@ -175,6 +186,14 @@ __device__ __forceinline__ void tape_store(float* __restrict__ t, int i, const f
       reinterpret_cast<__attribute__((address_space(1))) f32x4*>(as_global_w(t) + i * 1024 + p * 32 + 4 * h);
 #pragma unroll
   for (int k = 0; k < 4; ++k) q[2 * k] = f32x4{v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]};
+}
+// tape_store with one 4-B store per register: no 4-register tuples (storing the colour feature
+// with 16-B stores right after the forward chain cost that kernel 52 VGPRs and half its occupancy)
+__device__ __forceinline__ void tape_store_dw(float* __restrict__ t, int i, const f32x16& v, int lane) {
+  const int p = lane & 31, h = lane >> 5;
+  __attribute__((address_space(1))) float* q = as_global_w(t) + i * 1024 + p * 32 + 4 * h;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) q[(r & 3) + 8 * (r >> 2)] = v[r];
 }
 // Layer i of the tape as an MFMA B-operand stream over the points: element s of lane (j, h) is
 // h_i[point 2s+h][feature j] (each load instruction reads two 128-B point rows).
@@ -726,6 +745,37 @@ __device__ __forceinline__ void xyz_backward_saved(const float* __restrict__ pk,
   if (cot) tape_store(cot, 0, dh, lane);
   gemm_acc(dc, pk + L.FCT(0) * NSLAM_FRAG, dh, lane);
   gx[0] = gx[1] = gx[2] = 0.f;
+  if (cot) {  // a colour weight-gradient backward's embedding operands: Gc_b and S_b
+    const f32x16 da0 = apply_mask(dh, m[0]);
+    const float* FB = pk + L.FB();
+    const int p = lane & 31;
+    __attribute__((address_space(1))) float* ct = as_global_w(cot);
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      f32x16 de = zero16();
+      gemm_acc(de, pk + (L.L3T() + b) * NSLAM_FRAG, da3, lane);
+      gemm_acc(de, pk + (L.L0T() + b) * NSLAM_FRAG, da0, lane);
+      // registers 4k..4k+3 of lane (p, h) are dims 32b + 8k + 4h + 0..3 of point p (tape_store's layout)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int kd = 32 * b + 8 * k + 4 * h;
+        const f32x4 B0 = *as_global(reinterpret_cast<const f32x4*>(FB + kd));
+        const f32x4 B1 = *as_global(reinterpret_cast<const f32x4*>(FB + 96 + kd));
+        const f32x4 B2 = *as_global(reinterpret_cast<const f32x4*>(FB + 192 + kd));
+        f32x4 gc, sn;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float sv, cv;
+          fsincos(fourier_arg(x, B0[e], B1[e], B2[e]), sv, cv);  // decoder.py:29-30
+          gc[e] = de[4 * k + e] * cv;
+          sn[e] = sv;
+        }
+        const int o = p * 32 + 8 * k + 4 * h;
+        *reinterpret_cast<__attribute__((address_space(1))) f32x4*>(ct + (kCotG + b) * 1024 + o) = gc;
+        *reinterpret_cast<__attribute__((address_space(1))) f32x4*>(ct + (kCotS + b) * 1024 + o) = sn;
+      }
+    }
+  }
   if (EMBG) {
     da = apply_mask(dh, m[0]);
     const float* FB = pk + L.FB();
@@ -1064,10 +1114,8 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd(QueryKArgs a) {
       const float* pk = a.c.packed[NSLAM_DEC_COLOR];
       const XyzPack L{1};
       f32x16 h4;
-      if (a.c.act_tape) {
-        tape_store(a.c.act_tape + tile * kTapeFloats, kTapeFeat, cc[0], lane);
+      if (a.c.act_tape)
         h4 = xyz_forward<1, false, false, true>(pk, cc, q.x, lane, m, nullptr, a.c.act_tape + tile * kTapeFloats);
-      }
       else
         h4 = xyz_forward<1, false>(pk, cc, q.x, lane, m, nullptr);
       save_masks(a, NSLAM_DEC_COLOR, tile, m, lane);
@@ -1157,7 +1205,6 @@ __device__ __forceinline__ void fwd_part_color(const QueryKArgs& a, const Pt& q,
   const float* pk = a.c.packed[NSLAM_DEC_COLOR];
   const XyzPack L{1};
   float* tp = TAPE ? a.c.act_tape + tile * kTapeFloats : nullptr;
-  if (TAPE) tape_store(tp, kTapeFeat, cc[0], lane);  // the fc_c weight gradients' input
   const f32x16 h4 = xyz_forward<1, false, true, TAPE, true>(pk, cc, q.x, lane, m, nullptr, tp, vec);
   save_masks(a, NSLAM_DEC_COLOR, tile, m, lane);
   float o[3];
@@ -1246,10 +1293,13 @@ constexpr int kScratchFloats = 2 * TILE_FLOATS + 32 * 4 + 32 * 3 + 32 * 8 * 2 + 
 constexpr int kWavesBwd = 4;
 constexpr int kMaxSlabs = 4096;  // WG == 2 above this many tiles
 
-template <int DEC, int WG, bool PG, bool FIRST, bool SAVED>
+// COT: the colour tile may store the cotangent tape (a.cot) of a colour weight-gradient backward (a
+// compile-time switch: the tape path's registers would otherwise be every caller's)
+template <int DEC, int WG, bool PG, bool FIRST, bool SAVED, bool COT = true>
 __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, const Slab& A, const Scratch& S,
                                              int lane, double* __restrict__ gpts, int64_t gbase = 0) {
   // gpts: d/dpts of point idx at gpts[(idx - gbase) * 3 + k] (gbase: a tile's LDS staging rows)
+  float* const cot = COT ? a.cot : nullptr;
   // Every scratch / slab address is a function of the lane only, i.e. invariant across the tile
   // loop; letting LICM hoist the ~300 of them pins (and spills) the register file.  Re-derive
   // them per tile.
@@ -1291,6 +1341,8 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
   float gx[3] = {0.f, 0.f, 0.f};
   static_assert(!(SAVED && WG), "weight gradients from saved masks run as k_color_wgrad");
   if (SAVED) {  // masks from the forward: no recompute (the mask-only chain)
+    if (DEC == NSLAM_DEC_COLOR && cot)  // the colour feature: the fc_c weight gradients' input
+      tape_store(cot + tile * kCotFloats, kCotC, gather_tile_batched<NSLAM_CGATHER_NB>(gr.data, cr, lane), lane);
     uint32_t m[5];
     load_masks(a, DEC, tile, m, lane);
     if (DEC == NSLAM_DEC_COARSE) {
@@ -1298,10 +1350,10 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
     } else if (DEC == NSLAM_DEC_FINE) {
       xyz_backward_saved<2, 1, 3, PG>(pk, m, q.x, g, lane, dc, gx);
     } else if (DEC == NSLAM_DEC_COLOR) {  // + the cotangent tape of a colour weight-gradient backward
-      xyz_backward_saved<1, 3, 0, PG>(pk, m, q.x, g, lane, dc, gx, a.cot ? a.cot + tile * kCotFloats : nullptr);
-      if (a.cot) {  // x (half 0) and g (half 1) of point p; g is 0 past the end
+      xyz_backward_saved<1, 3, 0, PG>(pk, m, q.x, g, lane, dc, gx, cot ? cot + tile * kCotFloats : nullptr);
+      if (cot) {  // x (half 0) and g (half 1) of point p (g is 0 past the end)
         const f32x4 v = h == 0 ? f32x4{q.x[0], q.x[1], q.x[2], 0.f} : f32x4{g[0], g[1], g[2], 0.f};
-        *reinterpret_cast<__attribute__((address_space(1))) f32x4*>(as_global_w(a.cot) + tile * kCotFloats + kCotXg +
+        *reinterpret_cast<__attribute__((address_space(1))) f32x4*>(as_global_w(cot) + tile * kCotFloats + kCotXg +
                                                                     p * 8 + 4 * h) = v;
       }
     } else {
@@ -1416,7 +1468,7 @@ struct MultiDecArgs {
 // The colour decoder may be a part WITH weight gradients: its tiles run the same mask-only chain
 // and store their cotangents in a.cot (k_color_wgrad, launched after this kernel, forms the
 // weight gradients), so every part is lean and the launch keeps the lean kernels' occupancy.
-template <bool PG>
+template <bool PG, bool COT>
 __global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd_multi(QueryKArgs a, MultiDecArgs m) {
   constexpr int kScr = TILE_FLOATS + kWalkFloats;
   __shared__ __attribute__((aligned(16))) float lds[kWavesBwd * kScr];
@@ -1437,7 +1489,7 @@ __global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd_multi(QueryKArgs 
     case NSLAM_DEC_COARSE: dec_bwd_tile<NSLAM_DEC_COARSE, 0, PG, true, true>(a, w, A, S, lane, gp); break;
     case NSLAM_DEC_MIDDLE: dec_bwd_tile<NSLAM_DEC_MIDDLE, 0, PG, true, true>(a, w, A, S, lane, gp); break;
     case NSLAM_DEC_FINE: dec_bwd_tile<NSLAM_DEC_FINE, 0, PG, true, true>(a, w, A, S, lane, gp); break;
-    default: dec_bwd_tile<NSLAM_DEC_COLOR, 0, PG, true, true>(a, w, A, S, lane, gp); break;
+    default: dec_bwd_tile<NSLAM_DEC_COLOR, 0, PG, true, true, COT>(a, w, A, S, lane, gp); break;
   }
 }
 
@@ -1466,7 +1518,7 @@ __global__ __launch_bounds__(256, 2) void k_dec_bwd_multi_sum(QueryKArgs a, Mult
     case NSLAM_DEC_COARSE: dec_bwd_tile<NSLAM_DEC_COARSE, 0, true, true, true>(a, tile, A, S, lane, st, gb); break;
     case NSLAM_DEC_MIDDLE: dec_bwd_tile<NSLAM_DEC_MIDDLE, 0, true, true, true>(a, tile, A, S, lane, st, gb); break;
     case NSLAM_DEC_FINE: dec_bwd_tile<NSLAM_DEC_FINE, 0, true, true, true>(a, tile, A, S, lane, st, gb); break;
-    default: dec_bwd_tile<NSLAM_DEC_COLOR, 0, true, true, true>(a, tile, A, S, lane, st, gb); break;
+    default: dec_bwd_tile<NSLAM_DEC_COLOR, 0, true, true, true, false>(a, tile, A, S, lane, st, gb); break;
   }
   __syncthreads();
   if (part == 0) {

@@ -50,10 +50,12 @@ extern "C" int nslam_query_bwd_decoders(const nslam_query_cfg* cfg, int32_t dec_
   }
   const dim3 grid((unsigned)(groups * m.ndec)), block(64 * kWavesBwd);
   if (cw) a.cot = reinterpret_cast<float*>(ws);  // the colour part stores its cotangent tape
-  if (cfg->need_pts_grad)
-    hipLaunchKernelGGL((k_dec_bwd_multi<true>), grid, block, 0, s, a, m);
+  if (cfg->need_pts_grad)  // (a tape backward has no d/dpts)
+    hipLaunchKernelGGL((k_dec_bwd_multi<true, false>), grid, block, 0, s, a, m);
+  else if (cw)
+    hipLaunchKernelGGL((k_dec_bwd_multi<false, true>), grid, block, 0, s, a, m);
   else
-    hipLaunchKernelGGL((k_dec_bwd_multi<false>), grid, block, 0, s, a, m);
+    hipLaunchKernelGGL((k_dec_bwd_multi<false, false>), grid, block, 0, s, a, m);
   const int lrc = hip_status();
   if (lrc || !cw) return lrc;
   return launch_color_wgrad(a, reinterpret_cast<float*>(ws), s);

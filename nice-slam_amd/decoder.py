@@ -50,7 +50,7 @@ def _check_supported(hidden_size, n_blocks, skips, leaky, sample_mode):
 
 
 class MLP(nn.Module):
-    """Middle / fine / color decoder (decoder.py:91-203); forward via NICE (fused kernel)."""
+    """Middle / fine / color decoder (decoder.py:91-203); forward through the fused kernel."""
 
     def __init__(self, name="", dim=3, c_dim=128, hidden_size=256, n_blocks=5, leaky=False, sample_mode="bilinear",
                  color=False, skips=[2], grid_len=0.16, pos_embedding_method="fourier", concat_feature=False):
@@ -89,7 +89,9 @@ class MLP(nn.Module):
         return self._packer
 
     def forward(self, p, c_grid=None):
-        raise NotImplementedError("decoders are evaluated together by NICE.forward (one fused kernel per stage)")
+        """decoder.py:177-203 for this decoder alone (NICE.forward evaluates a whole stage in one
+        fused launch instead): occupancy [P] (middle, fine) or [P, 4] (colour)."""
+        return ops.query_decoder(self, p, c_grid)
 
 
 class MLP_no_xyz(nn.Module):
@@ -123,7 +125,8 @@ class MLP_no_xyz(nn.Module):
         return self._packer
 
     def forward(self, p, c_grid, **kwargs):
-        raise NotImplementedError("decoders are evaluated together by NICE.forward (one fused kernel per stage)")
+        """decoder.py:262-274: coarse occupancy [P] (the grid is read over the enlarged bound)."""
+        return ops.query_decoder(self, p, c_grid)
 
 
 class NICE(nn.Module):

@@ -287,6 +287,136 @@ def query_points(nice, p, c_grid, stage, oob_bound=None):
 
 
 # ----------------------------------------------------------------------------------------------
+# one decoder alone: MLP.forward / MLP_no_xyz.forward (decoder.py:177-203, 262-274)
+# ----------------------------------------------------------------------------------------------
+_ZERO_PACKED = {}
+
+
+class _Stub:
+    """Stands in for a decoder the kernel's stage evaluates beside the one asked for (its output is
+    discarded): all-zero packed weights, no parameters, no gradient."""
+
+    def __init__(self, nc, device):
+        from .packing import xyz_layout
+        key = (nc, str(device))
+        if key not in _ZERO_PACKED:
+            _ZERO_PACKED[key] = torch.zeros(xyz_layout(nc)["total"], dtype=torch.float32, device=device)
+        self.packed = _ZERO_PACKED[key]
+
+    def pack(self, params):
+        return self.packed
+
+    def grad_struct(self, base):
+        return _lib.NslamDecGrad()
+
+
+class _OneDecoder(torch.autograd.Function):
+    """The fine or colour decoder evaluated alone, through the stage that holds it (fine: middle |
+    fine, colour: middle | fine | colour) with the other decoders as zero stubs: the fine
+    occupancy comes from the forward's deferred-combine mode (raw[...,3] = fine only), the colour
+    decoder's rgb from raw[..., :3], and its 4th output row (which NICE.forward overwrites,
+    decoder.py:341) from the forward's activation tape h4 (returned as a second output so torch
+    forms h4 @ Wo[3] + bo[3]).  Backward: that decoder's share only (nslam_query_bwd_decoder)."""
+
+    @staticmethod
+    def forward(ctx, meta, name, pts, g_own, g_middle, *params):
+        ctx.set_materialize_grads(False)
+        pts = pts.detach().to(torch.float64).contiguous()
+        n = pts.shape[0]
+        own = channels_last(g_own.detach())
+        mid = channels_last(g_middle.detach()) if g_middle is not None else own
+        d = _DEC_ID[name]
+        grids = [None] * 4
+        grids[_lib.DEC_MIDDLE] = (mid, None)
+        grids[_lib.DEC_FINE] = (own if name == "fine" else mid, None)
+        grids[d] = (own, None)
+        packed = {k: meta.packers[k].pack(params if k == name else ()) for k in meta.decs}
+        cfg = _fill_cfg(meta, grids, packed, {}, False)
+        raw = torch.empty(n, 4, dtype=torch.float32, device=pts.device)
+        saved = torch.empty(lib().nslam_query_saved_size(n), dtype=torch.uint8, device=pts.device)
+        cfg.saved_masks = saved.data_ptr()
+        tape = None
+        if name == "color":
+            tape = torch.empty(lib().nslam_query_tape_size(n) // 4, dtype=torch.float32, device=pts.device)
+            cfg.act_tape = tape.data_ptr()
+        if n:
+            query_fwd_launch(cfg, pts, n, raw, split=True, defer_occ=name == "fine")
+        ctx.meta, ctx.name, ctx.grids, ctx.packed = meta, name, grids, packed
+        ctx.saved_masks, ctx.tape = saved, tape
+        ctx.save_for_backward(pts)
+        if name == "fine":
+            return raw[:, 3].clone(), None
+        # h4 of point i: tape [tile][layer][32 points][32 features], layer 4 (nslam.h act_tape)
+        h4 = tape.view(-1, 5, 32, 32)[:, 4].reshape(-1, 32)[:n].clone()
+        return raw[:, :3].clone(), h4
+
+    @staticmethod
+    def backward(ctx, g_out, g_h4):
+        meta, name = ctx.meta, ctx.name
+        (pts,) = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        if g_h4 is not None and need[2:].count(True) and bool(g_h4.ne(0).any()):
+            raise NotImplementedError("gradient of the colour decoder's 4th output through its hidden layers "
+                                      "(NICE.forward overwrites that row, decoder.py:341)")
+        n = pts.shape[0]
+        d = _DEC_ID[name]
+        g_raw = torch.zeros(n, 4, dtype=torch.float32, device=pts.device)
+        if g_out is not None:
+            if name == "fine":
+                g_raw[:, 3] = g_out
+            else:
+                g_raw[:, :3] = g_out
+        grids = list(ctx.grids)
+        own = grids[d][0]
+        g_grid = torch.zeros_like(own, memory_format=torch.channels_last_3d) if need[3] else None
+        grids[d] = (own, g_grid)
+        dgrad = torch.zeros(meta.packers[name].n_params, dtype=torch.float32, device=pts.device) \
+            if any(need[5:]) else None
+        g_pts = torch.empty_like(pts) if need[2] else None
+        cfg = _fill_cfg(meta, grids, ctx.packed, {name: dgrad} if dgrad is not None else {}, need[2])
+        cfg.saved_masks = ctx.saved_masks.data_ptr()
+        if ctx.tape is not None:
+            cfg.act_tape = ctx.tape.data_ptr()
+        if n and (g_grid is not None or dgrad is not None or g_pts is not None):
+            wsb = lib().nslam_query_bwd_decoder_workspace_size(ctypes.byref(cfg), d, n)
+            ws = torch.empty(wsb, dtype=torch.uint8, device=pts.device) if wsb else None
+            rc = lib().nslam_query_bwd_decoder(ctypes.byref(cfg), d, 0, ptr(pts), n, ptr(g_raw), ptr(g_pts),
+                                               ptr(ws), wsb, stream_ptr(pts.device))
+            check(rc, "nslam_query_bwd_decoder")
+        elif g_pts is not None:
+            g_pts.zero_()
+        grads = meta.packers[name].split_grad(dgrad) if dgrad is not None else [None] * meta.n_params[name]
+        return (None, None, g_pts, g_grid, None, *grads)
+
+
+def query_decoder(dec, p, c_grid):
+    """One decoder's forward (MLP.forward / MLP_no_xyz.forward): coarse [P], middle [P], fine [P]
+    (occupancy, out.squeeze(-1)), colour [P, 4] — the reference module's output for p [P, 3]."""
+    name = dec.name
+    p = p.reshape(-1, 3)
+    if p.dtype != torch.float64:
+        p = p.double()
+    bl = _bound_list(dec.bound)
+    params = list(dec.parameters())
+    if name in ("coarse", "middle"):
+        meta = QueryMeta(name, (name,), {name: dec.packer()}, {name: bl}, None, {name: len(params)})
+        grids = [None] * 4
+        grids[_DEC_ID[name]] = c_grid["grid_" + name]
+        return _Query.apply(meta, p, *grids, *params)[:, 3]
+    stage = name
+    decs = _DEC_FOR_STAGE[stage]
+    packers = {k: (dec.packer() if k == name else _Stub(2 if k == "fine" else 1, p.device)) for k in decs}
+    meta = QueryMeta(stage, decs, packers, {k: bl for k in decs}, None, {k: (len(params) if k == name else 0)
+                                                                          for k in decs})
+    own = c_grid["grid_" + name]
+    out, h4 = _OneDecoder.apply(meta, name, p, own, c_grid.get("grid_middle"), *params)
+    if name == "fine":
+        return out
+    W, b = dec.output_linear.weight, dec.output_linear.bias
+    return torch.cat([out, (h4 @ W[3] + b[3])[:, None]], 1)
+
+
+# ----------------------------------------------------------------------------------------------
 # compositing
 # ----------------------------------------------------------------------------------------------
 class _Composite(torch.autograd.Function):

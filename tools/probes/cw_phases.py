@@ -15,7 +15,7 @@ sys.path.insert(0, REPO)
 os.environ.setdefault("NSLAM_LIB", os.path.join(REPO, "nice-slam_amd", "libnslam_phases.so"))
 import bench  # noqa: E402
 
-STEPS = {(1, 2): "LDS-DMA issue", (2, 3): "phase A", (3, 4): "mid barrier + phase B", (4, 5): "end barrier"}
+STEPS = {(1, 2): "LDS-DMA issue", (2, 3): "compute", (3, 4): "end barrier"}
 
 
 def main():
@@ -50,7 +50,7 @@ def main():
             continue
         parts = " ".join(f"{nm} {np.median(tt[:, b] - tt[:, a]):6.0f}" for (a, b), nm in STEPS.items()
                          if (tt[:, a] != 0).all() and (tt[:, b] != 0).all())
-        print(f"  wave {w}: tile {np.median(tt[:, 5] - tt[:, 1]):6.0f} | {parts}")
+        print(f"  wave {w}: tile {np.median(tt[:, 4] - tt[:, 1]):6.0f} | {parts}")
 
 
 if __name__ == "__main__":
