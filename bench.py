@@ -56,6 +56,10 @@ HBM_PEAK_GBS = 8000.0
 KERNEL_WORK = {
     "query_fwd": (FLOP_FWD_PER_SAMPLE, BYTES_FWD_PER_SAMPLE),
     "query_bwd.color": (2 * 2 * 15575, 2048),
+    # ABI v11 split: the colour decoder's lean chain (input gradients, grid scatter, cotangent tape)
+    # and its weight-gradient reduction (dW = Σ cotangent ⊗ input: one MAC per weight per sample)
+    "query_bwd.color_lean": (2 * 15575, 2048),
+    "query_bwd.color_wgrad": (2 * 15575, 0),
     "query_bwd.fine": (2 * 20599, 2048),
     "query_bwd.middle": (2 * 15479, 2048),
     # the frozen decoders' mask-only backward as one launch (ABI v10 nslam_query_bwd_decoders)
@@ -66,12 +70,15 @@ KERNEL_WORK = {
 # not by HBM or MFMA: 8 corners x 32 channels x 4 B = 1024 added bytes per ray-sample against the
 # chip-wide float-atomic rate of ~1.3 TB/s of added bytes (MI355X_MICROARCH.md, atomics table: every
 # CU issuing, any footprint or contention).  Their roofline is stated against that ceiling.
-ATOMIC_SPANS = {"query_bwd.fine": 1024, "query_bwd.middle": 1024, "query_bwd.middle+fine": 2048}
+ATOMIC_SPANS = {"query_bwd.fine": 1024, "query_bwd.middle": 1024, "query_bwd.middle+fine": 2048,
+                "query_bwd.color_lean": 1024}
 ATOMIC_PEAK_GBS = 1300.0
 # rocprofv3 kernel names behind each span (for the PMC traffic of profiles/*traffic*.json)
 SPAN_KERNELS = {
     "query_fwd": ("k_query_fwd", "k_occ_combine"),
     "query_bwd.color": ("k_dec_bwd<3,", "k_color_wgrad", "k_slab_reduce"),
+    "query_bwd.color_lean": ("k_dec_bwd<3,",),
+    "query_bwd.color_wgrad": ("k_color_wgrad", "k_slab_reduce"),
     "query_bwd.fine": ("k_dec_bwd<2,",),
     "query_bwd.middle": ("k_dec_bwd<1,",),
     "query_bwd.middle+fine": ("k_dec_bwd_multi<false, false>",),

@@ -170,8 +170,19 @@ size_t nslam_query_tape_size(int64_t n_pts); /* ABI v9 */
  * colour: the order of summing the per-decoder buffers).  Replaces the per-decoder loop of
  * Tracker.optimize_cam_in_batch's backward (Tracker.py:125) / Mapper.optimize_map's (Mapper.py:503). */
 #define NSLAM_BWD_SUM_PTS 0x100
+/* ABI v11: dec_mask | NSLAM_BWD_DEFER_WGRAD (the colour decoder with weight gradients in the call):
+ * the call runs the colour decoder's lean chain only (its grid gradient, and its cotangent tape into
+ * ws); nslam_color_wgrad, with the same cfg and ws, later forms its weight gradients — so a mapping
+ * iteration can run the frozen decoders' backward beside that weight-gradient reduction. */
+#define NSLAM_BWD_DEFER_WGRAD 0x200
 int nslam_query_bwd_decoders(const nslam_query_cfg* cfg, int32_t dec_mask, const double* pts, int64_t n_pts,
                              const float* g_raw, double* const* g_pts, void* ws, size_t ws_bytes, void* stream);
+/* ABI v11: the colour decoder's parameter gradients (into cfg->dgrad[COLOR], added) from the tapes a
+ * nslam_query_bwd_decoders(... | NSLAM_BWD_DEFER_WGRAD) call left: the forward's activation tape and
+ * ReLU masks (cfg->act_tape, cfg->saved_masks) and the cotangent tape in ws (unchanged since, at least
+ * nslam_query_bwd_decoder_workspace_size(cfg, COLOR, n_pts) bytes).  Mapper.py:503 for
+ * color_decoder.parameters(); split-K over the points, deterministic. */
+int nslam_color_wgrad(const nslam_query_cfg* cfg, int64_t n_pts, void* ws, size_t ws_bytes, void* stream);
 
 /* ---- compositing: raw2outputs_nerf_color, src/common.py:204-245 (occupancy mode) ------------ */
 int nslam_composite_fwd(const float* raw, const double* z_vals, int64_t n_rays, int32_t n_samples,

@@ -27,6 +27,9 @@ struct QueryKArgs {
   // colour-decoder cotangent tape (workspace of a colour weight-gradient backward, NULL = none):
   // the lean backward stores dh_0..dh_4 of every tile here for k_color_wgrad
   float* cot = nullptr;
+  // ABI v11 NSLAM_BWD_DEFER_WGRAD: the colour tape backward stops after its lean chain (the
+  // cotangent tape in ws); nslam_color_wgrad forms the weight gradients later
+  bool defer_wgrad = false;
 };
 
 // ------------------------------------------------------------------------------------------
@@ -1679,7 +1682,7 @@ int launch_dec_bwd(const QueryKArgs& a, bool first, float* slab, hipStream_t s) 
       QueryKArgs b = a;
       b.cot = slab;
       rc = launch_one<DEC, 0, false, true, true>(b, nullptr, 0, (tiles + kWavesBwd - 1) / kWavesBwd, s);
-      return rc ? rc : launch_color_wgrad(a, slab, s);
+      return rc || a.defer_wgrad ? rc : launch_color_wgrad(a, slab, s);
     }
   }
   if (tiles > max_slabs() && hipMemsetAsync(slab, 0, (size_t)nslab * acc * sizeof(float), s) != hipSuccess)

@@ -11,7 +11,8 @@ extern "C" int nslam_query_bwd_decoders(const nslam_query_cfg* cfg, int32_t dec_
   const int rc = check_cfg(cfg, true);
   if (rc) return rc;
   const bool sum_pts = (dec_mask & NSLAM_BWD_SUM_PTS) != 0;
-  dec_mask &= ~NSLAM_BWD_SUM_PTS;
+  const bool defer = (dec_mask & NSLAM_BWD_DEFER_WGRAD) != 0;
+  dec_mask &= ~(NSLAM_BWD_SUM_PTS | NSLAM_BWD_DEFER_WGRAD);
   if (dec_mask <= 0 || dec_mask > 15) return NSLAM_EINVAL;
   if (sum_pts && (!cfg->need_pts_grad || (n_pts > 0 && (!g_pts || !g_pts[0])))) return NSLAM_EINVAL;
   if (n_pts < 0 || (n_pts > 0 && ((!pts && !cfg->rays_o) || !g_raw))) return NSLAM_EINVAL;
@@ -33,6 +34,7 @@ extern "C" int nslam_query_bwd_decoders(const nslam_query_cfg* cfg, int32_t dec_
     m.gp[m.ndec] = cfg->need_pts_grad && !sum_pts ? g_pts[d] : nullptr;
     ++m.ndec;
   }
+  if (defer && !cw) return NSLAM_EINVAL;
   if (n_pts > 0 && !cfg->saved_masks) return NSLAM_EUNSUPPORTED;
   if (n_pts == 0) return NSLAM_OK;
   const int64_t tiles = (n_pts + 31) / 32;
@@ -42,7 +44,11 @@ extern "C" int nslam_query_bwd_decoders(const nslam_query_cfg* cfg, int32_t dec_
     if (!ws || ws_bytes < need) return NSLAM_EWORKSPACE;
   }
   QueryKArgs a{*cfg, pts, n_pts, nullptr, g_raw, nullptr};
+  a.defer_wgrad = defer;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  // the colour decoder alone (its lean chain + weight gradients): its own kernel, which has the
+  // lean kernels' registers (the multi-decoder kernel with the tape path takes ~170)
+  if (cw && m.ndec == 1) return dispatch_dec_bwd<NSLAM_DEC_COLOR>(a, true, reinterpret_cast<float*>(ws), s);
   if (sum_pts) {  // one workgroup per tile, one wave per decoder, d/dpts summed in decoder order
     if (cw) return NSLAM_EUNSUPPORTED;
     hipLaunchKernelGGL(k_dec_bwd_multi_sum<>, dim3((unsigned)tiles), dim3(64 * m.ndec), 0, s, a, m, g_pts[0]);
@@ -57,6 +63,21 @@ extern "C" int nslam_query_bwd_decoders(const nslam_query_cfg* cfg, int32_t dec_
   else
     hipLaunchKernelGGL((k_dec_bwd_multi<false, false>), grid, block, 0, s, a, m);
   const int lrc = hip_status();
-  if (lrc || !cw) return lrc;
+  if (lrc || !cw || defer) return lrc;
   return launch_color_wgrad(a, reinterpret_cast<float*>(ws), s);
+}
+
+// ABI v11: the colour decoder's weight gradients of a tape backward whose lean chain ran earlier
+// (nslam_query_bwd_decoders with NSLAM_BWD_DEFER_WGRAD) and left its cotangent tape in ws.
+extern "C" int nslam_color_wgrad(const nslam_query_cfg* cfg, int64_t n_pts, void* ws, size_t ws_bytes, void* stream) {
+  const int rc = check_cfg(cfg, true);
+  if (rc) return rc;
+  if (cfg->stage != NSLAM_STAGE_COLOR || n_pts < 0) return NSLAM_EINVAL;
+  if (!cfg->dgrad[NSLAM_DEC_COLOR].base || cfg->dgrad[NSLAM_DEC_COLOR].count <= 0 || cfg->need_pts_grad)
+    return NSLAM_EUNSUPPORTED;
+  if (n_pts > 0 && !cw_tape_path(cfg)) return NSLAM_EUNSUPPORTED;
+  if (n_pts == 0) return NSLAM_OK;
+  if (!ws || ws_bytes < dec_ws_bytes(cfg, NSLAM_DEC_COLOR, n_pts)) return NSLAM_EWORKSPACE;
+  QueryKArgs a{*cfg, nullptr, n_pts, nullptr, nullptr, nullptr};
+  return launch_color_wgrad(a, reinterpret_cast<float*>(ws), reinterpret_cast<hipStream_t>(stream));
 }

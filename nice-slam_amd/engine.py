@@ -101,11 +101,18 @@ class MappingEngine:
         self.priority = False  # concurrent: run the weight-gradient branch on a high-priority stream
         self.all_side = False  # concurrent: every branch on a side stream (main only forks / joins)
         self.lean_first = False  # concurrent: enqueue the frozen decoders' branches before the weight-gradient one
-        # frozen decoders' mask-only backward as one launch (ABI v10): None = when every decoder of
-        # the stage is frozen (tracking: 0.199 -> 0.117 ms per iteration); with a weight-gradient
-        # branch beside them (mapping) two concurrent launches measured faster (200 vs 193 M/s);
-        # "all": every decoder, the colour weight gradients included, in one launch (experiment)
-        self.merge_frozen = None
+        # frozen decoders' mask-only backward as one launch (ABI v10) whenever there are several
+        # (tracking: 0.199 -> 0.117 ms per iteration; mapping, beside the colour branch's lean chain +
+        # k_color_wgrad: 205-208 vs 195-197 M ray-samples/s, profiles/r03_knobs.txt); False = one
+        # launch per decoder; "all": every decoder, the colour weight gradients included, in one
+        # launch (experiment)
+        self.merge_frozen = True
+        # ABI v11 split: the colour lean chain alone first, then its weight-gradient reduction beside
+        # the frozen decoders' backward (wgrad_side: which of the two forks off).  Measured slower
+        # (182 vs 199 M ray-samples/s, profiles/r03_knobs.txt): the lean kernels are latency-bound at
+        # the colour chain's 1500 waves (60 us alone vs 76 us for all three decoders together).
+        self.split_wgrad = False
+        self.wgrad_side = True
         # merged d/dpts summed inside the launch (NSLAM_BWD_SUM_PTS, one workgroup per tile): measured
         # 0.109 vs 0.102 ms per tracking iteration for per-decoder buffers + two adds — kept off
         self.sum_pts = False
@@ -210,11 +217,14 @@ class MappingEngine:
         cfg = self._cfg(stage, ro, rd, z, grid_grads, dec_grads)
         cfg.need_pts_grad = int(bool(pts_grad))
         decs = sorted(ops._DEC_FOR_STAGE[stage], key=lambda d: d not in dec_grads)  # weight-grad one first
+        frozen = [d for d in decs if d not in dec_grads]
+        if (self.split_wgrad and concurrent and not pts_grad and list(dec_grads) == ["color"] and frozen
+                and self._tape is not None and self._saved is not None and n > 0):
+            return self._query_bwd_split(cfg, n, z, g_raw, frozen, on_branch)
         gp = [torch.empty(n, 3, dtype=torch.float64, device=z.device) for _ in decs] if pts_grad else None
         # units of work: (decoder names, stream index); the frozen decoders' mask-only backward is one
         # launch (ABI v10 nslam_query_bwd_decoders) — no fork / join between their streams
-        frozen = [d for d in decs if d not in dec_grads]
-        merge = self.merge_frozen if self.merge_frozen is not None else len(frozen) == len(decs)
+        merge = self.merge_frozen
         wgt = [d for d in decs if d in dec_grads]
         if (merge == "all" and self._saved is not None and not pts_grad and wgt == ["color"]
                 and self._tape is not None):
@@ -295,6 +305,47 @@ class MappingEngine:
             for g in gp[1:]:
                 out += g
             return out
+        return None
+
+    def _query_bwd_split(self, cfg, n, z, g_raw, frozen, on_branch):
+        """The mapping iteration's backward with the colour decoder's weight gradients split off
+        (ABI v11): the colour lean chain first (its grid gradient and cotangent tape), then its
+        weight-gradient reduction (MFMA / LDS bound) on one stream beside the frozen decoders'
+        mask-only backward (float-atomic bound) on the other, so the two kinds of work overlap."""
+        main = torch.cuda.current_stream(z.device)
+        if not self._side:
+            self._side.append(torch.cuda.Stream(z.device))
+        side = self._side[0]
+        dcol = ops._DEC_ID["color"]
+        wsb = lib().nslam_query_bwd_decoder_workspace_size(ctypes.byref(cfg), dcol, n)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=z.device)
+        gps = (ctypes.c_void_p * 4)()
+        with ops._span("query_bwd"):
+            with ops._span("query_bwd.color_lean"):
+                rc = lib().nslam_query_bwd_decoders(ctypes.byref(cfg), (1 << dcol) | _lib.BWD_DEFER_WGRAD, None, n,
+                                                    ptr(g_raw), gps, ptr(ws), wsb, main.cuda_stream)
+            check(rc, "nslam_query_bwd_decoders(colour lean)")
+            side.wait_stream(main)
+            for t in (z, g_raw, self._saved, self._tape, ws):
+                t.record_stream(side)
+            wst, fst = (side, main) if self.wgrad_side else (main, side)
+            with torch.cuda.stream(wst):
+                with ops._span("query_bwd.color_wgrad"):
+                    rc = lib().nslam_color_wgrad(ctypes.byref(cfg), n, ptr(ws), wsb, wst.cuda_stream)
+                check(rc, "nslam_color_wgrad")
+                if on_branch is not None:
+                    on_branch(["color"])
+            with torch.cuda.stream(fst):
+                mask = 0
+                for name in frozen:
+                    mask |= 1 << ops._DEC_ID[name]
+                with ops._span("query_bwd." + "+".join(frozen)):
+                    rc = lib().nslam_query_bwd_decoders(ctypes.byref(cfg), mask, None, n, ptr(g_raw), gps, None, 0,
+                                                        fst.cuda_stream)
+                check(rc, "nslam_query_bwd_decoders")
+                if on_branch is not None:
+                    on_branch(frozen)
+            main.wait_stream(side)
         return None
 
     # -- one iteration ---------------------------------------------------------------------------

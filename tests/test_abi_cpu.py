@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_strerror(pkg):
     L = pkg._lib.lib()
-    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 10
+    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 11
     assert L.nslam_strerror(0) == b"ok"
     assert b"invalid" in L.nslam_strerror(-1)
 
@@ -150,3 +150,17 @@ def test_v10_bwd_decoders_validates_without_gpu(pkg):
     ok = pkg._lib.NslamQueryCfg()
     rc = L.nslam_query_bwd_decoders(ctypes.byref(ok), 0, None, 0, None, gps, None, 0, None)
     assert rc < 0  # an empty decoder mask (or an otherwise incomplete config) is never launched
+
+
+def test_v11_color_wgrad_validates_without_gpu(pkg):
+    """nslam_color_wgrad and NSLAM_BWD_DEFER_WGRAD reject configs without a colour weight-gradient
+    tape backward before any launch."""
+    L = pkg._lib.lib()
+    cfg = pkg._lib.NslamQueryCfg()
+    cfg.stage = 7
+    assert L.nslam_color_wgrad(ctypes.byref(cfg), 10, None, 0, None) == -1            # bad stage
+    cfg.stage = pkg._lib.STAGES["middle"]
+    assert L.nslam_color_wgrad(ctypes.byref(cfg), 10, None, 0, None) < 0              # not the colour stage
+    gps = (ctypes.c_void_p * 4)()
+    mask = (1 << pkg._lib.DEC_MIDDLE) | pkg._lib.BWD_DEFER_WGRAD                       # nothing to defer
+    assert L.nslam_query_bwd_decoders(ctypes.byref(cfg), mask, None, 0, None, gps, None, 0, None) < 0

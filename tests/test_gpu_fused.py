@@ -605,10 +605,13 @@ def test_merged_frozen_backward_matches_per_decoder_launches(tiny):
     keys = ("grid_middle", "grid_fine", "grid_color")
     pix = torch.randint(96 * 128, (3 * 150,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(21))
     out = {}
-    for merge in (False, True, "all"):  # "all": the colour weight-gradient backward joins the launch
+    # "all": the colour weight-gradient backward joins the launch; "split": ABI v11, the colour lean
+    # chain first, then nslam_color_wgrad beside the frozen decoders' launch
+    for merge in (False, True, "all", "split"):
         nice, c = _nice(sc)
         eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV)
-        eng.merge_frozen = merge
+        eng.merge_frozen = True if merge == "split" else merge
+        eng.split_wgrad = merge == "split"
         opt = P.ops.FusedAdam([{"params": [eng.decs["color"].param], "lr": 0.0}] +
                               [{"params": [c[k]], "lr": 0.0} for k in keys])
         gr = {}
@@ -620,7 +623,7 @@ def test_merged_frozen_backward_matches_per_decoder_launches(tiny):
 
         eng.iteration("color", frames, pix, 150, (96, 128), (sc.fx, sc.fy, sc.cx, sc.cy), opt, exchange=snapshot)
         out[merge] = gr
-    for merge in (True, "all"):
+    for merge in (True, "all", "split"):
         for k in keys:
             assert float(out[False][k].abs().sum()) > 0, k
             assert rel_l2(out[merge][k], out[False][k]) < 1e-6, (merge, k)
@@ -635,7 +638,7 @@ def test_merged_frozen_backward_matches_per_decoder_launches(tiny):
         te = P.engine.TrackingEngine(copy.deepcopy(slam.shared_decoders), slam.shared_c, scn.bound, 32, 16,
                                      (scn.H, scn.W), (scn.fx, scn.fy, scn.cx, scn.cy), ignore_edge=(20, 20),
                                      w_color=0.5, handle_dynamic=True, use_color=True, device=DEV)
-        te.eng.merge_frozen = bool(merge)  # (the default, None, merges here: every tracking decoder is frozen)
+        te.eng.merge_frozen = bool(merge)  # (the default, True, merges the frozen decoders)
         te.eng.sum_pts = merge is True  # in-kernel sum of the decoders' d/dpts (NSLAM_BWD_SUM_PTS)
         cam = cam0.clone().requires_grad_(True)
         opt = P.ops.FusedAdam([{"params": [cam], "lr": 0.0}])

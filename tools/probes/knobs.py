@@ -37,10 +37,16 @@ def main():
     dev = torch.device("cuda:0")
     scene = bench.Room0Scene(dev, 0, path="fused")
     tag = os.environ.get("NSLAM_FWD_PARTS", "auto") + " " + os.path.basename(os.environ.get("NSLAM_LIB", "libnslam.so"))
-    base = {"priority": False, "concurrent": True, "all_side": False, "lean_first": False, "merge_frozen": None}
+    base = {"priority": False, "concurrent": True, "all_side": False, "lean_first": False, "merge_frozen": True,
+            "split_wgrad": False, "wgrad_side": True}
     for name, knobs in (("default", {}), ("priority", {"priority": True}), ("sequential", {"concurrent": False}),
                         ("all_side", {"all_side": True}), ("lean_first", {"lean_first": True}),
                         ("side+lean", {"all_side": True, "lean_first": True}), ("merged", {"merge_frozen": True}), ("merged_all", {"merge_frozen": "all"}),
+                        ("merged+prio", {"merge_frozen": True, "priority": True}),
+                        ("merged+side", {"merge_frozen": True, "all_side": True}),
+                        ("merged+lean_first", {"merge_frozen": True, "lean_first": True}),
+                        ("unmerged", {"merge_frozen": False}),
+                        ("split", {"split_wgrad": True}), ("split_main", {"split_wgrad": True, "wgrad_side": False}),
                         ("default", {})):
         if len(sys.argv) > 1 and name not in sys.argv[1:]:
             continue
