@@ -42,6 +42,12 @@ ROOM0 = {
 STRESS = dict(ROOM0, bound=[[0.0, 7.9]] * 3, bound_divisible=0.5,
               grid_len={"coarse": 2.0, "middle": 1 / 32, "fine": 1 / 64, "color": 1 / 64},
               pixels=65536, window=4, n_strat=48, n_surf=16)
+# configs[3] (BASELINE.json): Apartment (configs/Apartment/apartment.yaml bound, Azure camera 720x1280),
+# 5000 pixels per GPU (5 frames x 1000) x 48 samples, the full coarse -> middle -> fine -> colour
+# hierarchy; the coarse mapper's iteration samples 32 stratified points without gt (Mapper.py:482-484)
+APARTMENT = dict(ROOM0, bound=[[-5.8, 11.3], [-4.0, 4.5], [-7.9, 4.9]], bound_divisible=0.32,
+                 H=720, W=1280, fx=607.4694213867188, fy=607.4534912109375, cx=636.9967041015625,
+                 cy=369.2689514160156, pixels=5000, window=5, coarse=True)
 FLOP_FWD_PER_SAMPLE = 2 * (15479 + 20599 + 15575)   # SURVEY §8(a10) MACs, colour stage
 FLOP_FINE_STAGE_PER_POINT = 2 * (15479 + 20599)          # fine stage: middle + fine decoders
 BYTES_FWD_PER_SAMPLE = 3 * 1024                      # 3 trilinear lookups × 8 corners × 128 B
@@ -185,10 +191,12 @@ class Room0Scene:
         self.cfg, self.dev = cfg, dev
         g = torch.Generator().manual_seed(2)
         self.bound = enlarge_bound(cfg)
-        std = {"middle": 0.01, "fine": 1e-4, "color": 0.01}
+        std = {"coarse": 0.01, "middle": 0.01, "fine": 1e-4, "color": 0.01}
         self.grids = {}
-        for k in ("middle", "fine", "color"):
-            shp = grid_shape(self.bound, cfg["grid_len"][k])
+        self.coarse = bool(cfg.get("coarse"))
+        for k in ("coarse",) * self.coarse + ("middle", "fine", "color"):
+            # the coarse grid spans the bound enlarged x2 (NICE_SLAM.py:211-220, coarse_bound_enlarge)
+            shp = grid_shape(self.bound, cfg["grid_len"][k] / (2.0 if k == "coarse" else 1.0))
             if device_init:  # stress grids (16 GiB): drawn on the device, channels-last directly
                 gd = torch.Generator(device=dev).manual_seed(2 + len(self.grids))
                 t = torch.empty(shp[0], shp[2], shp[3], shp[4], shp[1], device=dev).normal_(0.0, std[k], generator=gd)
@@ -198,7 +206,7 @@ class Room0Scene:
             self.grids["grid_" + k] = t.requires_grad_(True)
         torch.manual_seed(3)
         self.nice = P.NICE(c_dim=32, coarse_grid_len=2.0, middle_grid_len=0.32, fine_grid_len=0.16,
-                           color_grid_len=0.16, hidden_size=32, coarse=False)
+                           color_grid_len=0.16, hidden_size=32, coarse=self.coarse)
         self.nice.set_bound(self.bound)
         self.nice = self.nice.to(dev)
         for d in (self.nice.middle_decoder, self.nice.fine_decoder):  # fix_fine; middle never optimised
@@ -257,6 +265,7 @@ class Room0Scene:
                                                  w_color=cfg["w_color"], device=dev, rows=self.rows)
             self.opt = P.ops.FusedAdam(
                 [{"params": [self.engine.decs["color"].param], "lr": cfg["lr"]["decoders"]}] +
+                [{"params": [self.grids["grid_coarse"]], "lr": cfg["lr"]["middle"]}] * self.coarse +  # dense
                 [{"params": [self.grids[k]], "lr": cfg["lr"][k[5:]], "rows": self.rows[k]}
                  for k in ("grid_middle", "grid_fine", "grid_color")])
             # ray-sharded: all-reduce only the frustum rows Adam reads (+ colour-decoder grads)
@@ -653,6 +662,59 @@ def kernel_roofline(name, avg_ms, pts, traffic_path=None):
                             + os.path.relpath(tp, REPO)}
 
 
+def graph_time(scene, fn, reps):
+    """(ms per call, launch mode) of fn = one iteration, captured in hipGraphs and replayed `reps`
+    times after 3 eager and 10 replayed warm-ups."""
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    try:
+        g, mode = capture_step_graphs(fn, sync=scene.flip_parity)
+        run = g.run
+    except Exception:  # pragma: no cover - eager fallback
+        g, mode = None, "eager"
+
+        def run(k):
+            for _ in range(k):
+                fn()
+    run(10)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(reps)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps * 1e3
+    if g is not None:
+        g.finish()
+    return dt, mode
+
+
+def apartment_iterations(dev, reps=50):
+    """configs[3] on one GPU (its per-rank share of the 8-GPU job): Apartment bound and camera, 5000
+    pixels over a 5-frame window, every stage of the hierarchy as one fused-engine mapping iteration
+    replayed in a hipGraph — the coarse mapper's iteration (Mapper.py:403-404,482-484: stage
+    'coarse', no gt in the sampler so 32 stratified samples, depth loss, dense coarse-grid Adam) and
+    the fine mapper's middle / fine / colour iterations (frustum-masked grids, colour decoder)."""
+    scene = Room0Scene(dev, 0, cfg=dict(APARTMENT), path="fused")
+    cfg = scene.cfg
+    out = {"ms_per_iteration": {}, "ray_samples_per_s": {}}
+    for stage in ("coarse", "middle", "fine", "color"):
+        ms, mode = graph_time(scene, lambda: scene.step(stage=stage), reps)
+        out["ms_per_iteration"]["map_" + stage] = round(ms, 4)
+        spr = cfg["n_strat"] if stage == "coarse" else cfg["n_strat"] + cfg["n_surf"]
+        # kept rays per iteration from one extra eager iteration's count
+        scene.kept.zero_()
+        scene.step(stage=stage)
+        torch.cuda.synchronize()
+        out["ray_samples_per_s"]["map_" + stage] = int(scene.kept) * spr / (ms * 1e-3)
+    out["launch_mode"] = mode
+    out["grids"] = {k: list(v.shape) for k, v in scene.grids.items()}
+    out["workload"] = ("configs[3] Apartment, 1 GPU: 5000 pixels (5 frames x 1000) per iteration; coarse 32 samples "
+                       "(no gt), middle/fine/colour 48 samples, frustum-masked Adam (coarse grid dense)")
+    del scene
+    torch.cuda.empty_cache()
+    return out
+
+
 def room0_frame_rate(scene, reps=100):
     """frames/s on Replica room0 (BASELINE metric) from measured iteration times:
     per frame 10 tracking iterations × 200 pixels (replica.yaml tracking, edges 100 px) and 12
@@ -665,27 +727,7 @@ def room0_frame_rate(scene, reps=100):
     H, W = cfg["H"], cfg["W"]
 
     def timed(fn):
-        for _ in range(3):
-            fn()
-        torch.cuda.synchronize()
-        try:
-            g, mode = capture_step_graphs(fn, sync=scene.flip_parity)
-            run = g.run
-        except Exception:  # pragma: no cover - eager fallback
-            g, mode = None, "eager"
-
-            def run(k):
-                for _ in range(k):
-                    fn()
-        run(10)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        run(reps)
-        torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / reps * 1e3
-        if g is not None:
-            g.finish()
-        return dt, mode
+        return graph_time(scene, fn, reps)
 
     ms = {}
     for stage in ("middle", "fine", "color"):
@@ -720,6 +762,8 @@ def leg_main(leg):
         res = stress_iteration(dev)
     elif leg == "frame_io":
         res = frame_io(dev)
+    elif leg == "apartment":
+        res = apartment_iterations(dev)
     else:
         scene = Room0Scene(dev, 0, cfg=dict(ROOM0), path="fused")
         for _ in range(3):
@@ -763,7 +807,7 @@ def main():
                     help="fused engine (default) or the autograd drop-in path")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="draw + sample each iteration's rays inside it (no overlap with the previous backward)")
-    ap.add_argument("--leg", choices=("frames", "stress", "stress_iter", "bulk", "frame_io"), default=None,
+    ap.add_argument("--leg", choices=("frames", "stress", "stress_iter", "bulk", "frame_io", "apartment"), default=None,
                     help="run one auxiliary measurement and print its JSON (bench.py spawns these itself)")
     args = ap.parse_args()
     global PREFETCH
@@ -868,6 +912,7 @@ def main():
         # box ended in a host heap abort inside a later leg) cannot take the headline line with it
         if world == 1 and not args.no_frames and args.path == "fused":
             out["room0"] = run_leg("frames")
+            out["apartment"] = run_leg("apartment")
         if world == 1 and not args.no_stress:
             out["grid_query_stress"] = run_leg("stress")
             out["stress_iteration"] = run_leg("stress_iter")

@@ -286,14 +286,14 @@ __global__ __launch_bounds__(64 * kCwWaves, 1) void k_color_wgrad(CwArgs w) {
   CW_PHASE(9, true);
 }
 
-int launch_color_wgrad(const QueryKArgs& a, float* ws, hipStream_t s) {
+int launch_color_wgrad(const QueryKArgs& a, float* ws, hipStream_t s, const SlabAdam* adam) {
   const nslam_dec_grad& dg = a.c.dgrad[NSLAM_DEC_COLOR];
   const CwPlan pl = cw_plan(dg, a.n);
   CwArgs w{a, ws + pl.cot_bytes / sizeof(float), acc_floats_of(dg), pl.nchunks, pl.chunk_tiles};
   w.a.cot = ws;
   hipLaunchKernelGGL(k_color_wgrad, dim3((unsigned)pl.nchunks), dim3(64 * kCwWaves), 0, s, w);
   const int rc = hip_status();
-  return rc ? rc : slab_reduce(dg, w.slab, false, pl.nchunks, 0, w.acc, s);
+  return rc ? rc : slab_reduce(dg, w.slab, false, pl.nchunks, 0, w.acc, s, adam);
 }
 
 }  // namespace nslamq

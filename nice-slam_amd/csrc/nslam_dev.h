@@ -414,3 +414,36 @@ __device__ __forceinline__ float fcos(float x) {
   const float v = (q & 1) ? s : c;
   return ((q + 1) & 2) ? -v : v;
 }
+
+// ------------------------------------------------------------------------------------------
+// Adam element update (torch.optim.Adam single-tensor form, the reference's torch 1.11):
+//   m = b1 m + (1-b1) g;  v = b2 v + (1-b2) g g;  p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+// with torch's GPU division by a host scalar done as a multiply by its float reciprocal.  Shared by
+// k_adam (nslam_mapping.hip) and the Adam epilogue of k_slab_reduce (nslam_query_impl.h).
+// ------------------------------------------------------------------------------------------
+struct AdamCoef {
+  float b1, omb1, b2, omb2, eps, rbc2s, step_size;
+};
+
+__device__ __forceinline__ AdamCoef adam_coef(float b1, float b2, float eps, float lr, float step) {
+  const float t = step + 1.f;
+  const double bc1 = 1.0 - pow((double)b1, (double)t);
+  const double bc2 = 1.0 - pow((double)b2, (double)t);
+  AdamCoef c;
+  c.b1 = b1;
+  c.omb1 = 1.f - b1;
+  c.b2 = b2;
+  c.omb2 = 1.f - b2;
+  c.eps = eps;
+  c.rbc2s = 1.f / (float)sqrt(bc2);
+  c.step_size = (float)((double)lr / bc1);
+  return c;
+}
+
+__device__ __forceinline__ float adam_one(float& p, float g, float& m, float& v, const AdamCoef& c) {
+  m = c.b1 * m + c.omb1 * g;
+  v = c.b2 * v + c.omb2 * g * g;
+  const float den = sqrtf(v) * c.rbc2s + c.eps;
+  p = p - c.step_size * (m / den);
+  return p;
+}

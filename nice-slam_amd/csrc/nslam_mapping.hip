@@ -177,37 +177,13 @@ struct AdamArgs {
 constexpr int kAdamThreads = 256;
 constexpr int kDensePerBlock = kAdamThreads;  // one float per thread (dense segments are small)
 
-// torch.optim.Adam (single-tensor form, the reference's torch 1.11):
-//   m = b1 m + (1-b1) g;  v = b2 v + (1-b2) g g;  p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
-// with torch's GPU division by a host scalar done as a multiply by its float reciprocal.
-struct AdamCoef {
-  float b1, omb1, b2, omb2, eps, rbc2s, step_size;
-};
-
-__device__ __forceinline__ float adam_one(float& p, float g, float& m, float& v, const AdamCoef& c) {
-  m = c.b1 * m + c.omb1 * g;
-  v = c.b2 * v + c.omb2 * g * g;
-  const float den = sqrtf(v) * c.rbc2s + c.eps;
-  p = p - c.step_size * (m / den);
-  return p;
-}
-
+// the element update and its coefficients: adam_coef / adam_one (nslam_dev.h)
 __global__ __launch_bounds__(kAdamThreads) void k_adam(AdamArgs a) {
   const int64_t b = blockIdx.x;
   int s = 0;
   while (s + 1 < a.nseg && b >= a.blk0[s + 1]) ++s;
   const nslam_adam_seg& sg = a.seg[s];
-  const float t = *sg.step + 1.f;
-  const double bc1 = 1.0 - pow((double)a.b1, (double)t);
-  const double bc2 = 1.0 - pow((double)a.b2, (double)t);
-  AdamCoef c;
-  c.b1 = a.b1;
-  c.omb1 = 1.f - a.b1;
-  c.b2 = a.b2;
-  c.omb2 = 1.f - a.b2;
-  c.eps = a.eps;
-  c.rbc2s = 1.f / (float)sqrt(bc2);
-  c.step_size = (float)((double)sg.lr / bc1);
+  const AdamCoef c = adam_coef(a.b1, a.b2, a.eps, sg.lr, *sg.step);
   const int64_t lb = b - a.blk0[s];
   if (!sg.rows) {
     const int64_t e = lb * kDensePerBlock + threadIdx.x;

@@ -1540,10 +1540,22 @@ __global__ __launch_bounds__(256, 2) void k_dec_bwd_multi_sum(QueryKArgs a, Mult
 // float4 c of slab r of every 64th slab group, so the 16 waves x 4 lane rows keep 64 slab streams
 // in flight per workgroup (~count/64 workgroups fill the chip; a wave load is 4 x 256-B
 // segments).  The 64 partials are combined in LDS in a fixed order: deterministic.
+// Optional Adam epilogue (ABI v12 nslam_color_wgrad_adam): the reduced gradient g = base + sum is
+// consumed at once by the same element update as k_adam (seg: the decoder's dense segment, its grad
+// == base) — param, exp_avg, exp_avg_sq and the packed mirror are written, base is left g (or 0 with
+// zero_grad), and the last workgroup advances the step count by the ticket (k_adam's protocol), so a
+// mapping iteration's decoder update needs no separate launch after its weight-gradient reduction.
+struct SlabAdam {
+  nslam_adam_seg seg;
+  float b1, b2, eps;
+  int32_t zero_grad;
+  uint32_t* ticket;
+  int32_t on;
+};
 constexpr int kReduceWaves = 16;
 static __global__ __launch_bounds__(64 * kReduceWaves) void k_slab_reduce(const float* __restrict__ slab, int64_t nslab,
                                                                    int acc_floats, int count,
-                                                                   float* __restrict__ base) {
+                                                                   float* __restrict__ base, SlabAdam ad) {
   __shared__ f32x4 part[kReduceWaves * 4][16];
   const int lane = threadIdx.x & 63, wave = wave_id();
   const int c = lane & 15, r = wave * 4 + (lane >> 4);  // r: slab stream 0..63
@@ -1564,9 +1576,42 @@ static __global__ __launch_bounds__(64 * kReduceWaves) void k_slab_reduce(const 
     f32x4 t = part[0][c];
 #pragma unroll 8
     for (int k = 1; k < kReduceWaves * 4; ++k) t += part[k][c];
+    if (!ad.on) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if (j + e < count) base[j + e] += t[e];
+      for (int e = 0; e < 4; ++e)
+        if (j + e < count) base[j + e] += t[e];
+    } else {
+      const nslam_adam_seg& sg = ad.seg;
+      const AdamCoef co = adam_coef(ad.b1, ad.b2, ad.eps, sg.lr, *sg.step);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t i = j + e;
+        if (i < count) {
+          const float g = base[i] + t[e];
+          float p = sg.param[i], m = sg.exp_avg[i], v = sg.exp_avg_sq[i];
+          adam_one(p, g, m, v, co);
+          sg.param[i] = p;
+          sg.exp_avg[i] = m;
+          sg.exp_avg_sq[i] = v;
+          base[i] = ad.zero_grad ? 0.f : g;
+          if (sg.mirror) {
+            const int i0 = sg.mirror_idx[2 * i], i1 = sg.mirror_idx[2 * i + 1];
+            if (i0 >= 0) sg.mirror[i0] = p;
+            if (i1 >= 0) sg.mirror[i1] = p;
+          }
+        }
+      }
+    }
+  }
+  if (ad.on) {  // every workgroup has read the step count: the last one advances it (k_adam's ticket)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t tk = __hip_atomic_fetch_add(ad.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tk == gridDim.x - 1) {
+        *ad.seg.step += 1.f;
+        __hip_atomic_store(ad.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
 }
 
@@ -1624,7 +1669,7 @@ inline CwPlan cw_plan(const nslam_dec_grad& dg, int64_t n_pts) {
 inline bool cw_tape_path(const nslam_query_cfg* c) { return c->act_tape != nullptr && c->saved_masks != nullptr; }
 // k_color_wgrad + k_slab_reduce into a.c.dgrad[COLOR] after the lean chain has filled the cotangent
 // tape at ws (a.cot is set from ws); nslam_color_wgrad.hip
-int launch_color_wgrad(const QueryKArgs& a, float* ws, hipStream_t s);
+int launch_color_wgrad(const QueryKArgs& a, float* ws, hipStream_t s, const SlabAdam* adam = nullptr);
 
 // Slab cap: kMaxSlabs, or NSLAM_MAX_SLABS from the environment (tests use it to reach the
 // multi-tile read-modify-write mode at small sizes).
@@ -1650,11 +1695,13 @@ int launch_one(const QueryKArgs& a, float* slab, int acc, int64_t blocks, hipStr
 
 // WG == 1 launches leave one folded slab per workgroup (stride kWavesBwd slabs); WG == 2 one per wave
 inline int slab_reduce(const nslam_dec_grad& dg, float* slab, bool folded, int64_t nslab, int64_t blocks, int acc,
-                       hipStream_t s) {
+                       hipStream_t s, const SlabAdam* adam = nullptr) {
   const int64_t n = folded ? blocks : nslab;
   const int stride = folded ? acc * kWavesBwd : acc;
+  SlabAdam ad{};
+  if (adam) ad = *adam;
   hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((dg.count + 63) / 64)), dim3(64 * kReduceWaves), 0, s, slab, n,
-                     stride, (int)dg.count, dg.base);
+                     stride, (int)dg.count, dg.base, ad);
   return hip_status();
 }
 

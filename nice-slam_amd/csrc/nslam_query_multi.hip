@@ -81,3 +81,25 @@ extern "C" int nslam_color_wgrad(const nslam_query_cfg* cfg, int64_t n_pts, void
   QueryKArgs a{*cfg, nullptr, n_pts, nullptr, nullptr, nullptr};
   return launch_color_wgrad(a, reinterpret_cast<float*>(ws), reinterpret_cast<hipStream_t>(stream));
 }
+
+// ABI v12: nslam_color_wgrad, then the colour decoder's Adam step inside the slab reduction (one
+// launch fewer on the mapping iteration's critical path).  seg: the decoder's dense segment (its grad
+// is cfg->dgrad[COLOR].base, count elements); the same element update as nslam_adam_step.
+extern "C" int nslam_color_wgrad_adam(const nslam_query_cfg* cfg, int64_t n_pts, void* ws, size_t ws_bytes,
+                                      const nslam_adam_seg* seg, float beta1, float beta2, float eps,
+                                      int32_t zero_grad, uint32_t* ticket, void* stream) {
+  const int rc = check_cfg(cfg, true);
+  if (rc) return rc;
+  if (cfg->stage != NSLAM_STAGE_COLOR || n_pts < 0 || !seg || !ticket) return NSLAM_EINVAL;
+  const nslam_dec_grad& dg = cfg->dgrad[NSLAM_DEC_COLOR];
+  if (!dg.base || dg.count <= 0 || cfg->need_pts_grad) return NSLAM_EUNSUPPORTED;
+  if (seg->rows || seg->grad != dg.base || seg->n != dg.count || !seg->step || !seg->param || !seg->exp_avg ||
+      !seg->exp_avg_sq || (seg->mirror && !seg->mirror_idx))
+    return NSLAM_EINVAL;
+  if (n_pts == 0) return NSLAM_OK;  // (nothing to reduce: like a segment without a gradient, no step)
+  if (!cw_tape_path(cfg)) return NSLAM_EUNSUPPORTED;
+  if (!ws || ws_bytes < dec_ws_bytes(cfg, NSLAM_DEC_COLOR, n_pts)) return NSLAM_EWORKSPACE;
+  QueryKArgs a{*cfg, nullptr, n_pts, nullptr, nullptr, nullptr};
+  SlabAdam ad{*seg, beta1, beta2, eps, zero_grad, ticket, 1};
+  return launch_color_wgrad(a, reinterpret_cast<float*>(ws), reinterpret_cast<hipStream_t>(stream), &ad);
+}

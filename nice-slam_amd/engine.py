@@ -116,6 +116,11 @@ class MappingEngine:
         # merged d/dpts summed inside the launch (NSLAM_BWD_SUM_PTS, one workgroup per tile): measured
         # 0.109 vs 0.102 ms per tracking iteration for per-decoder buffers + two adds — kept off
         self.sum_pts = False
+        # ABI v12: with per-branch Adam the colour branch runs its lean chain, forks the colour grid's
+        # Adam onto a side stream, and folds the colour decoder's Adam step into the weight-gradient
+        # slab reduction (nslam_color_wgrad_adam) — no Adam launch after the reduction
+        self.fuse_adam = True
+        self._gadam_stream = None
         self._hi = None
         for k, v in c.items():
             if not v.is_contiguous(memory_format=torch.channels_last_3d):
@@ -246,6 +251,7 @@ class MappingEngine:
                 streams = [self._side[len(units) - 1]]
             streams += self._side[:len(units) - 1]
         used = [st for st in streams if st is not main]
+        joins = []  # further side streams forked inside a branch (the fused colour branch's grid Adam)
         summed = False
         with ops._span("query_bwd"):
             for st in used:  # fork: every branch starts from the same point of the main stream
@@ -286,17 +292,36 @@ class MappingEngine:
                         d = ops._DEC_ID[name]
                         wsb = lib().nslam_query_bwd_decoder_workspace_size(ctypes.byref(cfg), d, n)
                         ws = torch.empty(wsb, dtype=torch.uint8, device=z.device) if wsb else None
+                        fused = (name == "color" and name in dec_grads and self.fuse_adam and not pts_grad
+                                 and on_branch is not None and hasattr(on_branch, "color_wgrad")
+                                 and self._tape is not None and self._saved is not None)
                         with ops._span("query_bwd." + name):  # this branch alone, on its own stream
-                            rc = lib().nslam_query_bwd_decoder(ctypes.byref(cfg), d, 0, None, n, ptr(g_raw),
-                                                               ptr(gp[decs.index(name)]) if pts_grad else None,
-                                                               ptr(ws), wsb, st.cuda_stream)
-                        check(rc, "nslam_query_bwd_decoder")
+                            if fused:  # lean chain | colour-grid Adam (side) | weight gradients + decoder Adam
+                                rc = lib().nslam_query_bwd_decoders(ctypes.byref(cfg), (1 << d) | _lib.BWD_DEFER_WGRAD,
+                                                                    None, n, ptr(g_raw), (ctypes.c_void_p * 4)(),
+                                                                    ptr(ws), wsb, st.cuda_stream)
+                                check(rc, "nslam_query_bwd_decoders(colour lean)")
+                                if self._gadam_stream is None:
+                                    self._gadam_stream = torch.cuda.Stream(z.device)
+                                gs = self._gadam_stream
+                                gs.wait_stream(st)
+                                with torch.cuda.stream(gs):
+                                    on_branch(names, part="grids")
+                                joins.append(gs)
+                                on_branch.color_wgrad(cfg, n, ws, wsb, st)
+                            else:
+                                rc = lib().nslam_query_bwd_decoder(ctypes.byref(cfg), d, 0, None, n, ptr(g_raw),
+                                                                   ptr(gp[decs.index(name)]) if pts_grad else None,
+                                                                   ptr(ws), wsb, st.cuda_stream)
+                                check(rc, "nslam_query_bwd_decoder")
+                        if fused:
+                            continue
                     if on_branch is not None:
                         on_branch(names)
                 if pts_grad and st is not main:
                     for name in names:
                         gp[decs.index(name)].record_stream(st)
-            for st in used:
+            for st in used + joins:
                 main.wait_stream(st)
         if pts_grad and summed:
             return gp[0]
@@ -456,15 +481,22 @@ class MappingEngine:
             # one rank: each decoder branch updates its own grid's rows (+ the trainable decoder's
             # parameters, after its slab reduction) on its own stream — the update of a grid needs
             # that branch's gradients alone, so no branch waits for the others before its Adam
-            def on_branch(names):  # the decoders of one launch: one Adam call for their grids
+            def on_branch(names, part=None):  # the decoders of one launch: one Adam call for their grids
                 sub = {}
                 for name in names:
                     if _GRID_OF[name] in keys:
                         sub[self.c[_GRID_OF[name]]] = grads[self.c[_GRID_OF[name]]]
-                    if name in dnames:
+                    if name in dnames and part != "grids":
                         sub[self.decs[name].param] = grads[self.decs[name].param]
                 if sub:
                     optimizer.step(grads=sub, zero_grad=clean)
+
+            if hasattr(optimizer, "color_wgrad_step"):
+                def color_wgrad(cfg, n, ws, wsb, st):  # weight gradients + the decoder's Adam, one reduction
+                    p = self.decs["color"].param
+                    optimizer.color_wgrad_step(cfg, n, ws, wsb, p, grads[p], zero_grad=clean, stream=st)
+
+                on_branch.color_wgrad = color_wgrad
         self.query_bwd(stage, ro, rd, z, g_raw, keys, dnames, on_branch=on_branch)
         if exchange is not None:  # frustum-compacted all-reduce (distributed.SparseGradExchange)
             exchange(keys, dnames)

@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_strerror(pkg):
     L = pkg._lib.lib()
-    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 11
+    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 12
     assert L.nslam_strerror(0) == b"ok"
     assert b"invalid" in L.nslam_strerror(-1)
 
@@ -164,3 +164,19 @@ def test_v11_color_wgrad_validates_without_gpu(pkg):
     gps = (ctypes.c_void_p * 4)()
     mask = (1 << pkg._lib.DEC_MIDDLE) | pkg._lib.BWD_DEFER_WGRAD                       # nothing to defer
     assert L.nslam_query_bwd_decoders(ctypes.byref(cfg), mask, None, 0, None, gps, None, 0, None) < 0
+
+
+def test_v12_color_wgrad_adam_validates_without_gpu(pkg):
+    """nslam_color_wgrad_adam rejects a missing segment / ticket, a segment that is not the colour
+    decoder's gradient, and non-colour stages before any launch."""
+    L = pkg._lib.lib()
+    cfg = pkg._lib.NslamQueryCfg()
+    seg = pkg._lib.NslamAdamSeg()
+    cfg.stage = 7
+    assert L.nslam_color_wgrad_adam(ctypes.byref(cfg), 10, None, 0, ctypes.byref(seg), 0.9, 0.999, 1e-8, 0, None,
+                                    None) == -1                                          # bad stage
+    cfg.stage = pkg._lib.STAGES["middle"]
+    assert L.nslam_color_wgrad_adam(ctypes.byref(cfg), 10, None, 0, ctypes.byref(seg), 0.9, 0.999, 1e-8, 0, None,
+                                    None) < 0                                            # not the colour stage
+    cfg.stage = pkg._lib.STAGES["color"]
+    assert L.nslam_color_wgrad_adam(ctypes.byref(cfg), 10, None, 0, None, 0.9, 0.999, 1e-8, 0, None, None) < 0

@@ -322,6 +322,42 @@ def test_engine_per_branch_adam_matches_single_adam(tiny):
     assert sorted(out[True][2].values()) == sorted(out[False][2].values()) == [3.0] * 4
 
 
+def test_engine_fused_colour_adam_matches_separate_adam(tiny):
+    """ABI v12: the colour decoder's Adam step inside the weight-gradient slab reduction
+    (nslam_color_wgrad_adam, the colour grid's Adam forked beside it) == the separate reduction then
+    nslam_adam_step — bit for bit after one iteration (decoder parameters, Adam state, packed copy),
+    and the same map after three."""
+    sc, frames = _frames(tiny)
+    out = {}
+    for fuse in (True, False):
+        nice, c = _nice(sc)
+        eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV)
+        eng.fuse_adam = fuse
+        opt = P.ops.FusedAdam([{"params": [eng.decs["color"].param], "lr": 0.005}] +
+                              [{"params": [c[k]], "lr": 0.005} for k in ("grid_middle", "grid_fine", "grid_color")])
+        pix = torch.randint(96 * 128, (3 * 150,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(12))
+        snaps = []
+        for _ in range(3):
+            eng.iteration("color", frames, pix, 150, (96, 128), (sc.fx, sc.fy, sc.cx, sc.cy), opt)
+            torch.cuda.synchronize()
+            p = eng.decs["color"].param
+            st = opt.state[p]
+            snaps.append((p.detach().clone(), st["exp_avg"].clone(), st["exp_avg_sq"].clone(), float(st["step"]),
+                          eng.decs["color"].packed.clone(), eng.decs["color"].grad.clone(),
+                          {k: v.detach().clone() for k, v in c.items()}))
+        out[fuse] = snaps
+    a, b = out[True][0], out[False][0]
+    for i in range(5):
+        assert torch.equal(a[i], b[i]) if i != 3 else a[i] == b[i] == 1.0, i
+    # the reduced gradient is left in the buffer (no rows: the engine zeroes it with a memset next time)
+    assert torch.equal(a[5], b[5]) and float(a[5].abs().sum()) > 0
+    a, b = out[True][2], out[False][2]
+    assert a[3] == b[3] == 3.0
+    assert rel_l2(a[0], b[0]) < 1e-5
+    for k in a[6]:
+        assert rel_l2(a[6][k], b[6][k]) < 1e-5, k
+
+
 def test_rows_pack_unpack_bitexact():
     """nslam_rows_pack / nslam_rows_unpack (the sparse gradient exchange) vs torch indexing."""
     g = torch.Generator(device=DEV).manual_seed(9)
