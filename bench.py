@@ -29,6 +29,9 @@ sys.path.insert(0, REPO)
 # the next iteration's pixel gather + sampler run beside this iteration's render/backward
 # (engine.MappingEngine.iteration(prefetch=True)); --no-prefetch for the strictly serial step
 PREFETCH = True
+# cross-iteration pipelining of the colour stage (engine.MappingEngine.pipeline): the next iteration's
+# middle | fine forward overlaps this iteration's colour weight gradients (--pipeline to turn on)
+PIPELINE = False
 
 ROOM0 = {
     "bound": [[-2.9, 8.9], [-3.2, 5.5], [-3.5, 3.3]], "bound_divisible": 0.32,
@@ -61,6 +64,10 @@ HBM_PEAK_GBS = 8000.0
 # into its grid = 1024 B read + 1024 B written (float-atomic RMW).
 KERNEL_WORK = {
     "query_fwd": (FLOP_FWD_PER_SAMPLE, BYTES_FWD_PER_SAMPLE),
+    # the pipelined iteration's forward halves (ABI v13 nslam_query_fwd_parts): middle | fine
+    # (middle and fine MACs; middle lookup + fine's fine and middle lookups) and colour
+    "query_fwd.middle+fine": (2 * (15479 + 20599), 3 * 1024),
+    "query_fwd.color": (2 * 15575, 1024),
     "query_bwd.color": (2 * 2 * 15575, 2048),
     # ABI v11 split: the colour decoder's lean chain (input gradients, grid scatter, cotangent tape)
     # and its weight-gradient reduction (dW = Σ cotangent ⊗ input: one MAC per weight per sample)
@@ -82,6 +89,8 @@ ATOMIC_PEAK_GBS = 1300.0
 # rocprofv3 kernel names behind each span (for the PMC traffic of profiles/*traffic*.json)
 SPAN_KERNELS = {
     "query_fwd": ("k_query_fwd", "k_occ_combine"),
+    "query_fwd.middle+fine": ("k_query_fwd_parts<3, 2, false, 1>",),
+    "query_fwd.color": ("k_query_fwd_parts<3, 1, true, 2>",),
     "query_bwd.color": ("k_dec_bwd<3,", "k_color_wgrad", "k_slab_reduce"),
     "query_bwd.color_lean": ("k_dec_bwd<3,",),
     "query_bwd.color_wgrad": ("k_color_wgrad", "k_slab_reduce"),
@@ -140,24 +149,30 @@ class StepGraphs:
     (one per ray-buffer parity of the prefetching engine) cover remainders.  run(k) executes exactly
     k iterations; finish() re-aligns the engine's host-side buffer parity (sync) with the device."""
 
-    def __init__(self, fn, block=10, sync=None):
+    def __init__(self, fn, block=10, sync=None, tail=None):
+        # tail(): joins streams an iteration may leave in flight (the pipelined engine's colour
+        # branch) into the capturing stream before a capture ends
+        tail = tail or (lambda: None)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for _ in range(2):
                 fn()
+            tail()
         torch.cuda.current_stream().wait_stream(side)
         self.single = []
         for _ in range(2):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 fn()
+                tail()
             self.single.append(g)
         self.block = max(2, block - block % 2)
         self.blockg = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.blockg):
             for _ in range(self.block):
                 fn()
+            tail()
         self.par = 0  # device-side parity relative to the capture start
         self.sync = sync
 
@@ -178,9 +193,9 @@ class StepGraphs:
         self.par = 0
 
 
-def capture_step_graphs(fn, block=10, sync=None):
+def capture_step_graphs(fn, block=10, sync=None, tail=None):
     """(StepGraphs, "hipgraph") for fn = one mapping iteration."""
-    return StepGraphs(fn, block, sync), "hipgraph"
+    return StepGraphs(fn, block, sync, tail), "hipgraph"
 
 
 class Room0Scene:
@@ -263,9 +278,10 @@ class Room0Scene:
             # grid gradients accumulate only on the frustum-selected rows Adam optimises (compact)
             self.engine = P.engine.MappingEngine(self.nice, self.grids, self.bound, cfg["n_strat"], cfg["n_surf"],
                                                  w_color=cfg["w_color"], device=dev, rows=self.rows)
+            self.engine.pipeline = PIPELINE
             self.opt = P.ops.FusedAdam(
                 [{"params": [self.engine.decs["color"].param], "lr": cfg["lr"]["decoders"]}] +
-                [{"params": [self.grids["grid_coarse"]], "lr": cfg["lr"]["middle"]}] * self.coarse +  # dense
+                ([{"params": [self.grids["grid_coarse"]], "lr": cfg["lr"]["middle"]}] if self.coarse else []) +
                 [{"params": [self.grids[k]], "lr": cfg["lr"][k[5:]], "rows": self.rows[k]}
                  for k in ("grid_middle", "grid_fine", "grid_color")])
             # ray-sharded: all-reduce only the frustum rows Adam reads (+ colour-decoder grads)
@@ -308,6 +324,11 @@ class Room0Scene:
             stage, self.frames, None, n, (H, W), (cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"]), self.opt,
             trainable_decoders=("color",), exchange=self.exchange if sharded else None, n_kept=self.kept,
             seed=1000, world=world, rank=self.rank if sharded else 0, prefetch=PREFETCH)
+
+    def join(self):
+        """Join a pipelined iteration's colour branch into the current stream."""
+        if self.path == "fused":
+            self.engine.join()
 
     def flip_parity(self):
         """The prefetching engine's host-side ray-buffer parity, after an odd number of replayed
@@ -464,7 +485,7 @@ def stress_iteration(dev, steps=10):
     if os.environ.get("NSLAM_BENCH_EAGER"):  # PMC passes (tools/gpu_traffic_stress.sh): per-dispatch counters
         g, mode = None, "eager"
     else:
-        g, mode = capture_step_graphs(scene.step, block=2, sync=scene.flip_parity)
+        g, mode = capture_step_graphs(scene.step, block=2, sync=scene.flip_parity, tail=scene.join)
         g.run(2)
     torch.cuda.synchronize()
     scene.kept.zero_()
@@ -669,7 +690,7 @@ def graph_time(scene, fn, reps):
         fn()
     torch.cuda.synchronize()
     try:
-        g, mode = capture_step_graphs(fn, sync=scene.flip_parity)
+        g, mode = capture_step_graphs(fn, sync=scene.flip_parity, tail=scene.join)
         run = g.run
     except Exception:  # pragma: no cover - eager fallback
         g, mode = None, "eager"
@@ -805,13 +826,17 @@ def main():
                     help="override mapping pixels per iteration (scaling studies; the metric uses room0's 1000)")
     ap.add_argument("--path", choices=("fused", "autograd"), default="fused",
                     help="fused engine (default) or the autograd drop-in path")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="cross-iteration overlap of the colour branch with the next forward (experiment)")
+    ap.add_argument("--no-pipeline", action="store_true", help="(the default) no cross-iteration overlap")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="draw + sample each iteration's rays inside it (no overlap with the previous backward)")
     ap.add_argument("--leg", choices=("frames", "stress", "stress_iter", "bulk", "frame_io", "apartment"), default=None,
                     help="run one auxiliary measurement and print its JSON (bench.py spawns these itself)")
     args = ap.parse_args()
-    global PREFETCH
+    global PREFETCH, PIPELINE
     PREFETCH = not args.no_prefetch
+    PIPELINE = (args.pipeline or PIPELINE) and not args.no_pipeline
     if args.leg:
         return leg_main(args.leg)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -839,7 +864,8 @@ def main():
     if not args.eager and not (world > 1 and args.backend == "gloo"):
         try:  # whole mapping iterations as hipGraphs (removes per-op host launch cost); two of them,
             # replayed in turn, since the prefetching engine alternates its ray buffers
-            graph, mode = capture_step_graphs(lambda: scene.step(sharded=sharded), sync=scene.flip_parity)
+            graph, mode = capture_step_graphs(lambda: scene.step(sharded=sharded), sync=scene.flip_parity,
+                                              tail=scene.join)
             graph.run(graph.block)
             torch.cuda.synchronize()
         except Exception as e:  # pragma: no cover - fall back to eager launches
@@ -901,7 +927,9 @@ def main():
             "roofline": roof,
             "kernel_rooflines": per_kernel,
             "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in timers.items()},
-            "query_fwd_hbm_frac": (pts_per_step * BYTES_FWD_PER_SAMPLE / (qf["avg_ms"] * 1e-3) / 1e9) / HBM_PEAK_GBS,
+            "query_fwd_hbm_frac": (pts_per_step * BYTES_FWD_PER_SAMPLE / (qf["avg_ms"] * 1e-3) / 1e9) / HBM_PEAK_GBS
+            if "query_fwd" in timers else None,
+            "pipeline": PIPELINE,
             "query_bwd_ms": qb["avg_ms"],
         }
         if sharded and args.path == "fused":

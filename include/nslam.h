@@ -146,6 +146,13 @@ size_t nslam_query_fwd_workspace_size(const nslam_query_cfg* cfg, int64_t n_pts)
 int nslam_query_bwd(const nslam_query_cfg* cfg, const double* pts, int64_t n_pts, const float* g_raw,
                     double* g_pts, void* ws, size_t ws_bytes, void* stream);
 size_t nslam_query_bwd_workspace_size(const nslam_query_cfg* cfg, int64_t n_pts);
+/* ABI v13: part of the colour stage's decoder-parallel forward, for callers that overlap the
+ * parts with other work (cfg->defer_occ must be 1).  part_mask: 0b011 = the middle and fine
+ * decoders (middle occupancy into ws, at least nslam_query_fwd_workspace_size bytes; fine occupancy
+ * into raw[...,3]; their ReLU masks), 0b100 = the colour decoder (raw[...,0:3], its masks and the
+ * activation tape), 0b111 = nslam_query_fwd_ws.  The two halves touch disjoint bytes. */
+int nslam_query_fwd_parts(const nslam_query_cfg* cfg, const double* pts, int64_t n_pts, float* raw, void* ws,
+                          size_t ws_bytes, int32_t part_mask, void* stream);
 /* One decoder's share of nslam_query_bwd (ABI v4): its grid gradient, its parameter gradients
  * and its d/dpts (written, or added when accumulate_pts).  Decoders whose gradients go to
  * different buffers may run concurrently on different streams (the mapping iteration does:

@@ -1235,9 +1235,15 @@ __device__ __forceinline__ void fwd_part_color(const QueryKArgs& a, const Pt& q,
 #define NSLAM_FWD_LB 2  // min waves per SIMD (experiments: 3..5 trade VGPRs for occupancy)
 #endif
 constexpr int kVecFloats = 744;  // XyzPack vector section (740) rounded to float4s
-template <int STAGE, int NPARTS, bool TAPE>
+// PSET (ABI v13 nslam_query_fwd_parts, colour stage): 0 = the whole forward as above; 1 = only the
+// middle | fine parts (NPARTS 2: part 0 middle, part 1 fine writing raw[p][3]); 2 = only the colour
+// part (NPARTS 1) — so a pipelined mapping loop can start the next iteration's middle and fine
+// decoders (which read neither the colour grid nor the colour decoder) while this iteration's colour
+// weight gradients and colour Adam step are still running.
+template <int STAGE, int NPARTS, bool TAPE, int PSET = 0>
 __global__ __launch_bounds__(256, NSLAM_FWD_LB) void k_query_fwd_parts(QueryKArgs a, float* __restrict__ occ_mid) {
-  const int part = (int)(blockIdx.x % NPARTS);
+  static_assert(PSET == 0 || (STAGE == NSLAM_STAGE_COLOR && NPARTS == (PSET == 1 ? 2 : 1)), "part set");
+  const int part = PSET == 2 ? 2 : (int)(blockIdx.x % NPARTS);
   const int lane = threadIdx.x & 63;
   // The part's decoder vector sections (biases, output rows, Fourier B: ~3 KiB each) are read by
   // every layer of every wave: an LDS copy per workgroup turns ~90 global loads per wave into
@@ -1247,7 +1253,7 @@ __global__ __launch_bounds__(256, NSLAM_FWD_LB) void k_query_fwd_parts(QueryKArg
     const int d0 = part == 0 ? NSLAM_DEC_MIDDLE : part == 1 ? NSLAM_DEC_FINE : NSLAM_DEC_COLOR;
     const int nc0 = d0 == NSLAM_DEC_FINE ? 2 : 1;
     const float* src0 = a.c.packed[d0] + XyzPack{nc0}.V();
-    const bool two = NPARTS == 2 && STAGE == NSLAM_STAGE_COLOR && part == 0;
+    const bool two = PSET == 0 && NPARTS == 2 && STAGE == NSLAM_STAGE_COLOR && part == 0;
     const float* src1 = two ? a.c.packed[NSLAM_DEC_COLOR] + XyzPack{1}.V() : nullptr;
     for (int i = threadIdx.x; i < 740; i += 256) {
       vsec[0][i] = src0[i];
@@ -1261,7 +1267,7 @@ __global__ __launch_bounds__(256, NSLAM_FWD_LB) void k_query_fwd_parts(QueryKArg
   PHASE(0, 0);
   const Pt q = load_point(a, idx);
   PHASE(0, 1);
-  if (NPARTS == 2 && STAGE == NSLAM_STAGE_COLOR) {
+  if (PSET == 0 && NPARTS == 2 && STAGE == NSLAM_STAGE_COLOR) {
     if (part == 0) {
       fwd_part_middle(a, q, tile, idx, lane, occ_mid, vsec[0]);
       fwd_part_color<TAPE>(a, q, tile, idx, lane, vsec[1]);
@@ -1471,8 +1477,11 @@ struct MultiDecArgs {
 // The colour decoder may be a part WITH weight gradients: its tiles run the same mask-only chain
 // and store their cotangents in a.cot (k_color_wgrad, launched after this kernel, forms the
 // weight gradients), so every part is lean and the launch keeps the lean kernels' occupancy.
+#ifndef NSLAM_MULTI_COT_LB
+#define NSLAM_MULTI_COT_LB 2  // min workgroups per CU of the all-decoder lean launch with the colour tape
+#endif
 template <bool PG, bool COT>
-__global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd_multi(QueryKArgs a, MultiDecArgs m) {
+__global__ __launch_bounds__(64 * kWavesBwd, COT ? NSLAM_MULTI_COT_LB : 2) void k_dec_bwd_multi(QueryKArgs a, MultiDecArgs m) {
   constexpr int kScr = TILE_FLOATS + kWalkFloats;
   __shared__ __attribute__((aligned(16))) float lds[kWavesBwd * kScr];
   const int lane = threadIdx.x & 63, wave = wave_id();

@@ -21,6 +21,7 @@ the frustum-selected voxels in place instead of through masked copies (Mapper.py
 from __future__ import annotations
 
 import ctypes
+import os
 import math
 
 import numpy as np
@@ -121,6 +122,19 @@ class MappingEngine:
         # slab reduction (nslam_color_wgrad_adam) — no Adam launch after the reduction
         self.fuse_adam = True
         self._gadam_stream = None
+        # Cross-iteration pipelining (colour stage, one rank, per-branch Adam, ray prefetch): the colour
+        # branch (lean chain -> weight gradients + decoder Adam, colour-grid Adam beside it) stays on
+        # its own stream past the end of iteration(), and the next iteration's forward is split
+        # (ABI v13 nslam_query_fwd_parts): its middle | fine parts — which read neither the colour grid
+        # nor the colour decoder — start as soon as the frozen branch's grid Adam is done, its colour
+        # part queues behind the colour branch.  Every iteration still sees the map its predecessor
+        # left (the same dependencies as the serial loop).  Callers join() before reading the colour
+        # decoder / grid or ending a graph capture.
+        self.pipeline = False
+        self.pipe_order = int(os.environ.get("NSLAM_PIPE_ORDER", "0"))  # capture-order experiment
+        self._col_pending = False
+        self._col_stream = None   # the colour branch (+ the next forward's colour part)
+        self._frz_stream = None   # the frozen decoders' branch
         self._hi = None
         for k, v in c.items():
             if not v.is_contiguous(memory_format=torch.channels_last_3d):
@@ -373,6 +387,109 @@ class MappingEngine:
             main.wait_stream(side)
         return None
 
+    # -- cross-iteration pipelining (self.pipeline) ------------------------------------------------
+    def join(self):
+        """Make the current stream wait for a pipelined colour branch still in flight (call before
+        reading the colour decoder / colour grid, or before ending a graph capture)."""
+        if self._col_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._col_stream)
+        self._col_pending = False
+
+    def _pipe_streams(self):
+        if self._col_stream is None:
+            self._col_stream = torch.cuda.Stream(self.device)
+            self._frz_stream = torch.cuda.Stream(self.device)
+            self._gadam_stream = self._gadam_stream or torch.cuda.Stream(self.device)
+        return self._col_stream, self._frz_stream, self._gadam_stream
+
+    def _query_fwd_pipelined(self, ro, rd, z):
+        """Colour-stage forward as two launches: middle | fine on the current stream, colour on the
+        colour stream (behind the previous iteration's colour branch); returns raw (occupancy of the
+        middle decoder deferred into self.occ_add, as query_fwd(defer_occ=True))."""
+        main = torch.cuda.current_stream(self.device)
+        sc, _, _ = self._pipe_streams()
+        n = z.numel()
+        raw = torch.empty(n, 4, dtype=torch.float32, device=z.device)
+        self._saved = torch.empty(lib().nslam_query_saved_size(n), dtype=torch.uint8, device=z.device)
+        self._tape = torch.empty(lib().nslam_query_tape_size(n) // 4, dtype=torch.float32, device=z.device)
+        cfg = self._cfg("color", ro, rd, z, (), ())
+        cfg.defer_occ = 1
+        wsb = lib().nslam_query_fwd_workspace_size(ctypes.byref(cfg), n)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=z.device)
+        with ops._span("query_fwd.middle+fine"):
+            rc = lib().nslam_query_fwd_parts(ctypes.byref(cfg), None, n, ptr(raw), ptr(ws), wsb, 3, main.cuda_stream)
+        check(rc, "nslam_query_fwd_parts(middle | fine)")
+        sc.wait_stream(main)  # the rays, and the buffers just allocated on main
+        with torch.cuda.stream(sc):
+            with ops._span("query_fwd.color"):
+                rc = lib().nslam_query_fwd_parts(ctypes.byref(cfg), None, n, ptr(raw), ptr(ws), wsb, 4,
+                                                 sc.cuda_stream)
+        check(rc, "nslam_query_fwd_parts(colour)")
+        main.wait_stream(sc)
+        self.occ_add = ws[:n * 4].view(torch.float32)
+        return raw
+
+    def _query_bwd_pipelined(self, ro, rd, z, g_raw, keys, frozen, on_branch):
+        """The colour stage's backward with per-branch Adam: the colour stream runs the colour lean
+        chain, then the weight gradients with the decoder's Adam, and is NOT joined into the current
+        stream (the next iteration's colour forward queues behind it); the current stream runs the
+        frozen decoders' merged mask-only launch and the middle / fine grids' Adam, then — once the
+        colour lean chain is done — the colour grid's Adam.  So the next forward's middle | fine half
+        follows every grid update but not the colour weight gradients.  (Stream topology chosen for
+        hipGraph capture on this stack: a stream forked off the colour stream and joined back into
+        it crashes hipStreamEndCapture, tools/probes/capture_topology.py pattern t3; and a separate
+        frozen-branch stream was serialised behind the weight gradients by the graph's queue
+        assignment.)"""
+        main = torch.cuda.current_stream(self.device)
+        sc, _, _ = self._pipe_streams()
+        n = z.numel()
+        cfg = self._cfg("color", ro, rd, z, keys, ("color",))
+        cfg.need_pts_grad = 0
+        self._clean = False
+        dcol = ops._DEC_ID["color"]
+        # the colour workspace is allocated on the current stream (inside a graph capture the caching
+        # allocator serves the capturing stream's pool)
+        wsb = lib().nslam_query_bwd_decoder_workspace_size(ctypes.byref(cfg), dcol, n)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=z.device)
+        mask = 0
+        for name in frozen:
+            mask |= 1 << ops._DEC_ID[name]
+        def frozen_launch():
+            with ops._span("query_bwd." + "+".join(frozen)):
+                rc = lib().nslam_query_bwd_decoders(ctypes.byref(cfg), mask, None, n, ptr(g_raw),
+                                                    (ctypes.c_void_p * 4)(), None, 0, main.cuda_stream)
+            check(rc, "nslam_query_bwd_decoders")
+
+        order = self.pipe_order
+        with ops._span("query_bwd"):
+            sc.wait_stream(main)
+            for t in (ro, rd, z, g_raw, self._saved, self._tape, ws):
+                t.record_stream(sc)
+            if order == 1:
+                frozen_launch()
+            with torch.cuda.stream(sc):
+                with ops._span("query_bwd.color_lean"):
+                    rc = lib().nslam_query_bwd_decoders(ctypes.byref(cfg), (1 << dcol) | _lib.BWD_DEFER_WGRAD, None, n,
+                                                        ptr(g_raw), (ctypes.c_void_p * 4)(), ptr(ws), wsb,
+                                                        sc.cuda_stream)
+                check(rc, "nslam_query_bwd_decoders(colour lean)")
+            if order != 1:
+                frozen_launch()
+            if order == 2:  # the colour grid's Adam on the colour stream too: no join in the backward
+                on_branch(frozen)
+                with torch.cuda.stream(sc):
+                    on_branch(["color"], part="grids")
+                    with ops._span("query_bwd.color_wgrad"):
+                        on_branch.color_wgrad(cfg, n, ws, wsb, sc)
+                self._col_pending = True  # the next prefetch reuses this batch's rays: it waits for sc
+                return
+            on_branch(frozen)
+            main.wait_stream(sc)  # the colour lean chain (its grid gradient) is done; the next
+            on_branch(["color"], part="grids")  # prefetch, which reuses this batch's rays, follows it
+            with torch.cuda.stream(sc):
+                with ops._span("query_bwd.color_wgrad"):
+                    on_branch.color_wgrad(cfg, n, ws, wsb, sc)
+
     # -- one iteration ---------------------------------------------------------------------------
     def grads_for(self, stage, trainable_decoders):
         """(grid keys, decoder names) that receive gradients in `stage` (Mapper.py:335-341)."""
@@ -455,21 +572,31 @@ class MappingEngine:
                 self._pre_stream = torch.cuda.Stream(self.device)
             side = self._pre_stream
             side.wait_stream(main)  # the previous iteration's backward has released `nxt`
+            if self._col_pending and self._col_stream is not None:
+                side.wait_stream(self._col_stream)  # (a pipelined colour lean chain reads `nxt` too)
             with torch.cuda.stream(side):
                 rays(out=nxt)  # the next iteration's batch, beside this iteration's render + backward
             ro, rd, gd, gc, keep, z = cur
         else:
             ro, rd, gd, gc, keep, z = rays()
         keys, dnames = self.grads_for(stage, trainable_decoders)
-        raw = self.query_fwd(stage, ro, rd, z, defer_occ=True, tape="color" in dnames)
+        mirror = hasattr(optimizer, "set_mirror")
+        pipe = (self.pipeline and self.fuse_adam and stage == "color" and tuple(dnames) == ("color",)
+                and exchange is None and allreduce is None and mirror and hasattr(optimizer, "color_wgrad_step"))
+        if not pipe:
+            self.join()  # a pipelined predecessor's colour branch must finish before a serial iteration
+        if pipe:
+            raw = self._query_fwd_pipelined(ro, rd, z)
+        else:
+            raw = self.query_fwd(stage, ro, rd, z, defer_occ=True, tape="color" in dnames)
         _, _, _, ray_loss, g_raw = ops.render_loss(raw, z, gd, gc, keep, mode="mapper", use_color=stage == "color",
                                                    w_color=self.w_color, occ_add=self.occ_add)
         if not self._clean:
+            self.join()  # (a pipelined colour branch may still be writing the decoder gradient)
             self.gall.zero_()  # grid and decoder gradients: one memset
         # Adam resets every gradient entry it reads.  With compact gradients for every grid of the
         # stage that is every entry the backward wrote, so the next iteration needs no memsets.
         clean = all(k in self.rows for k in keys)
-        mirror = hasattr(optimizer, "set_mirror")
         if mirror:  # Adam stores updated decoder parameters straight into their packed copies
             for n in dnames:
                 d = self.decs[n]
@@ -497,7 +624,11 @@ class MappingEngine:
                     optimizer.color_wgrad_step(cfg, n, ws, wsb, p, grads[p], zero_grad=clean, stream=st)
 
                 on_branch.color_wgrad = color_wgrad
-        self.query_bwd(stage, ro, rd, z, g_raw, keys, dnames, on_branch=on_branch)
+        if pipe:
+            self._query_bwd_pipelined(ro, rd, z, g_raw, keys, [d for d in ops._DEC_FOR_STAGE[stage] if d != "color"],
+                                      on_branch)
+        else:
+            self.query_bwd(stage, ro, rd, z, g_raw, keys, dnames, on_branch=on_branch)
         if exchange is not None:  # frustum-compacted all-reduce (distributed.SparseGradExchange)
             exchange(keys, dnames)
         elif allreduce is not None:  # the grid gradients as one flat buffer, plus the decoder gradients

@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_strerror(pkg):
     L = pkg._lib.lib()
-    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 12
+    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 13
     assert L.nslam_strerror(0) == b"ok"
     assert b"invalid" in L.nslam_strerror(-1)
 
@@ -180,3 +180,14 @@ def test_v12_color_wgrad_adam_validates_without_gpu(pkg):
                                     None) < 0                                            # not the colour stage
     cfg.stage = pkg._lib.STAGES["color"]
     assert L.nslam_color_wgrad_adam(ctypes.byref(cfg), 10, None, 0, None, 0.9, 0.999, 1e-8, 0, None, None) < 0
+
+
+def test_v13_query_fwd_parts_validates_without_gpu(pkg):
+    """nslam_query_fwd_parts takes only the colour stage with deferred occupancy and the part masks
+    0b011 / 0b100 / 0b111, checked before any launch."""
+    L = pkg._lib.lib()
+    cfg = pkg._lib.NslamQueryCfg()
+    cfg.stage = 7
+    assert L.nslam_query_fwd_parts(ctypes.byref(cfg), None, 10, None, None, 0, 3, None) == -1    # bad stage
+    ok = pkg._lib.NslamQueryCfg()
+    assert L.nslam_query_fwd_parts(ctypes.byref(ok), None, 10, None, None, 0, 3, None) < 0      # incomplete cfg

@@ -358,6 +358,61 @@ def test_engine_fused_colour_adam_matches_separate_adam(tiny):
         assert rel_l2(a[6][k], b[6][k]) < 1e-5, k
 
 
+def test_query_fwd_parts_match_whole_forward(tiny):
+    """ABI v13: the colour stage's forward as its middle | fine half and its colour half (two
+    launches, the halves on separate streams) == nslam_query_fwd_ws with deferred occupancy, bit for
+    bit: raw, the middle occupancy, the saved ReLU masks and the colour activation tape."""
+    sc, frames = _frames(tiny)
+    nice, c = _nice(sc)
+    eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV)
+    pix = torch.randint(96 * 128, (3 * 150,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(3))
+    ro, rd, gd, gc, keep = P.ops.gather_rays(frames, pix, 150, 96, 128, (0, 96, 0, 128), sc.fx, sc.fy, sc.cx, sc.cy)
+    z = P.ops.sample_z(ro, rd, gd, sc.bound, 32, 16)
+    raw0 = eng.query_fwd("color", ro, rd, z, defer_occ=True, tape=True)
+    ref = (raw0.clone(), eng.occ_add.clone(), eng._saved.clone(), eng._tape.clone())
+    raw1 = eng._query_fwd_pipelined(ro, rd, z)
+    torch.cuda.synchronize()
+    got = (raw1, eng.occ_add, eng._saved, eng._tape)
+    tiles = (z.numel() + 31) // 32
+    for i, (a, b) in enumerate(zip(got, ref)):
+        if i == 2:  # masks [decoder][tile][layer][64] u16: the colour stage writes decoders 1..3 (no coarse)
+            a, b = (t.view(torch.int16).view(4, tiles, 5, 64)[1:] for t in (a, b))
+        assert torch.equal(a, b), i
+
+
+def test_engine_pipelined_matches_serial(tiny):
+    """Cross-iteration pipelining (the next iteration's middle | fine forward beside this one's
+    colour weight gradients and Adam) keeps every dependency of the serial loop: three iterations
+    give the same map, decoder and Adam steps (grid atomics order aside)."""
+    sc, frames = _frames(tiny)
+    out = {}
+    for pipe in (True, False):
+        nice, c = _nice(sc)
+        eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV)
+        eng.pipeline = pipe
+        opt = P.ops.FusedAdam([{"params": [eng.decs["color"].param], "lr": 0.005}] +
+                              [{"params": [c[k]], "lr": 0.005} for k in ("grid_middle", "grid_fine", "grid_color")])
+        losses = []
+        for it in range(3):
+            pix = torch.randint(96 * 128, (3 * 150,), device=DEV,
+                                generator=torch.Generator(device=DEV).manual_seed(20 + it))
+            loss, _ = eng.iteration("color", frames, pix, 150, (96, 128), (sc.fx, sc.fy, sc.cx, sc.cy), opt)
+            losses.append(loss.sum())
+        eng.join()
+        torch.cuda.synchronize()
+        out[pipe] = ({k: v.detach().clone() for k, v in c.items()}, eng.decs["color"].param.detach().clone(),
+                     eng.decs["color"].packed.clone(), [float(x) for x in losses],
+                     sorted(float(st["step"]) for st in opt.state.values()))
+    a, b = out[True], out[False]
+    for k in a[0]:
+        assert rel_l2(a[0][k], b[0][k]) < 1e-5, k
+    assert rel_l2(a[1], b[1]) < 1e-5 and rel_l2(a[2], b[2]) < 1e-5
+    assert abs(a[3][0] - b[3][0]) <= 1e-9 * abs(b[3][0])  # the first iteration's loss: same map, same rays
+    for x, y in zip(a[3][1:], b[3][1:]):
+        assert abs(x - y) <= 1e-4 * abs(y)
+    assert a[4] == b[4] == [3.0] * 4
+
+
 def test_rows_pack_unpack_bitexact():
     """nslam_rows_pack / nslam_rows_unpack (the sparse gradient exchange) vs torch indexing."""
     g = torch.Generator(device=DEV).manual_seed(9)
