@@ -318,13 +318,15 @@ typedef struct nslam_adam_seg {
  * may run concurrently (other streams, other processes) each pass their own. */
 int nslam_adam_step(const nslam_adam_seg* segs, int32_t n_segs, float beta1, float beta2, float eps,
                     int32_t zero_grad, uint32_t* ticket, void* stream);
-/* ABI v12: nslam_color_wgrad followed by the colour decoder's Adam step (Mapper.py:504 for
- * color_decoder.parameters()) inside the same slab reduction: `seg` is the decoder's dense segment
- * with seg->grad == cfg->dgrad[COLOR].base and seg->n == its count (mirror allowed); the update,
- * zero_grad and the ticket (required) behave as nslam_adam_step's for that one segment, bit for bit. */
+/* ABI v14 (v12 took one segment): nslam_color_wgrad followed by the Adam step (Mapper.py:504) of the
+ * colour decoder and of up to 3 further segments inside the same slab-reduction launch: segs[0] is
+ * the decoder's dense segment with segs[0].grad == cfg->dgrad[COLOR].base and segs[0].n == its count
+ * (mirror allowed); segs[1..n_segs) are any segments nslam_adam_step takes (e.g. the colour grid's
+ * frustum rows, whose gradient the lean chain completed).  The update, zero_grad and the ticket
+ * (required) behave as nslam_adam_step's over those segments, bit for bit. */
 int nslam_color_wgrad_adam(const nslam_query_cfg* cfg, int64_t n_pts, void* ws, size_t ws_bytes,
-                           const nslam_adam_seg* seg, float beta1, float beta2, float eps, int32_t zero_grad,
-                           uint32_t* ticket, void* stream);
+                           const nslam_adam_seg* segs, int32_t n_segs, float beta1, float beta2, float eps,
+                           int32_t zero_grad, uint32_t* ticket, void* stream);
 
 /* Sparse gradient exchange of a ray-sharded mapping iteration (ABI v5).  Only the frustum-
  * selected grid rows reach Adam (Mapper.py:314-333,394-401,504), so only they need summing across

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NSLAM_LIB") or os.path.join(_HERE, "libnslam.so")  # NSLAM_LIB: instrumented builds
 
 NSLAM_OK = 0
-ABI_VERSION = 13
+ABI_VERSION = 14
 BWD_SUM_PTS = 0x100  # nslam.h NSLAM_BWD_SUM_PTS (nslam_query_bwd_decoders)
 BWD_DEFER_WGRAD = 0x200  # nslam.h NSLAM_BWD_DEFER_WGRAD (ABI v11; then nslam_color_wgrad)
 STAGES = {"coarse": 0, "middle": 1, "fine": 2, "color": 3}
@@ -154,7 +154,7 @@ def lib():
                                                sz, vp]
         L.nslam_color_wgrad.argtypes = [ctypes.POINTER(NslamQueryCfg), i64, vp, sz, vp]
         L.nslam_color_wgrad_adam.argtypes = [ctypes.POINTER(NslamQueryCfg), i64, vp, sz, ctypes.POINTER(NslamAdamSeg),
-                                             ctypes.c_float, ctypes.c_float, ctypes.c_float, i32, vp, vp]
+                                             i32, ctypes.c_float, ctypes.c_float, ctypes.c_float, i32, vp, vp]
         L.nslam_query_bwd_decoder_workspace_size.argtypes = [ctypes.POINTER(NslamQueryCfg), i32, i64]
         L.nslam_query_bwd_decoder_workspace_size.restype = sz
         L.nslam_query_saved_size.argtypes = [i64]

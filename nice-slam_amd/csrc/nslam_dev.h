@@ -447,3 +447,64 @@ __device__ __forceinline__ float adam_one(float& p, float g, float& m, float& v,
   p = p - c.step_size * (m / den);
   return p;
 }
+
+// One workgroup's share of a segment's update (k_adam's body; nthreads = the workgroup's size):
+// dense segments one element per thread (lb * nthreads + tid), row-masked segments row_len/4
+// threads per row (float4 each) — the same element update everywhere, so any launch that hands a
+// segment's workgroups this function updates it bit-identically.
+__device__ __forceinline__ void adam_segment_block(const nslam_adam_seg& sg, const AdamCoef& c, int64_t lb,
+                                                   int zero_grad, int tid, int nthreads) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  if (!sg.rows) {
+    const int64_t e = lb * nthreads + tid;
+    if (e < sg.n) {
+      float p = sg.param[e], m = sg.exp_avg[e], v = sg.exp_avg_sq[e];
+      const float g = sg.grad[e];
+      adam_one(p, g, m, v, c);
+      sg.param[e] = p;
+      sg.exp_avg[e] = m;
+      sg.exp_avg_sq[e] = v;
+      if (zero_grad) sg.grad[e] = 0.f;
+      if (sg.mirror) {  // the packed MFMA copy of this parameter (up to two slots)
+        const int i0 = sg.mirror_idx[2 * e], i1 = sg.mirror_idx[2 * e + 1];
+        if (i0 >= 0) sg.mirror[i0] = p;
+        if (i1 >= 0) sg.mirror[i1] = p;
+      }
+    }
+  } else {
+    const int q = sg.row_len / 4;  // float4 per row
+    const int64_t rows_per_block = nthreads / q;
+    const int64_t ri = lb * rows_per_block + tid / q;
+    const int part = tid % q;
+    if (tid < rows_per_block * q && ri < sg.n) {
+      const int64_t base = (int64_t)sg.rows[ri] * sg.row_len + part * 4;
+      const int64_t sbase = ri * sg.row_len + part * 4;
+      f4 p = *reinterpret_cast<const f4*>(sg.param + base);
+      const int64_t gbase = sg.grad_rows ? sbase : base;
+      const f4 g = *reinterpret_cast<const f4*>(sg.grad + gbase);
+      f4 m = *reinterpret_cast<const f4*>(sg.exp_avg + sbase);
+      f4 v = *reinterpret_cast<const f4*>(sg.exp_avg_sq + sbase);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float pk = p[k], mk = m[k], vk = v[k];
+        adam_one(pk, g[k], mk, vk, c);
+        p[k] = pk;
+        m[k] = mk;
+        v[k] = vk;
+      }
+      *reinterpret_cast<f4*>(sg.param + base) = p;
+      *reinterpret_cast<f4*>(sg.exp_avg + sbase) = m;
+      *reinterpret_cast<f4*>(sg.exp_avg_sq + sbase) = v;
+      if (zero_grad) *reinterpret_cast<f4*>(sg.grad + gbase) = f4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+}
+
+// workgroups of `nthreads` threads a segment's update takes (adam_segment_block)
+__host__ __device__ inline int64_t adam_segment_blocks(const nslam_adam_seg& sg, int nthreads) {
+  if (sg.rows) {
+    const int64_t rpb = nthreads / (sg.row_len / 4);
+    return (sg.n + rpb - 1) / rpb;
+  }
+  return (sg.n + nthreads - 1) / nthreads;
+}

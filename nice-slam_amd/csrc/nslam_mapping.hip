@@ -184,50 +184,7 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam(AdamArgs a) {
   while (s + 1 < a.nseg && b >= a.blk0[s + 1]) ++s;
   const nslam_adam_seg& sg = a.seg[s];
   const AdamCoef c = adam_coef(a.b1, a.b2, a.eps, sg.lr, *sg.step);
-  const int64_t lb = b - a.blk0[s];
-  if (!sg.rows) {
-    const int64_t e = lb * kDensePerBlock + threadIdx.x;
-    if (e < sg.n) {
-      float p = sg.param[e], m = sg.exp_avg[e], v = sg.exp_avg_sq[e];
-      const float g = sg.grad[e];
-      adam_one(p, g, m, v, c);
-      sg.param[e] = p;
-      sg.exp_avg[e] = m;
-      sg.exp_avg_sq[e] = v;
-      if (a.zero_grad) sg.grad[e] = 0.f;
-      if (sg.mirror) {  // the packed MFMA copy of this parameter (up to two slots)
-        const int i0 = sg.mirror_idx[2 * e], i1 = sg.mirror_idx[2 * e + 1];
-        if (i0 >= 0) sg.mirror[i0] = p;
-        if (i1 >= 0) sg.mirror[i1] = p;
-      }
-    }
-  } else {
-    const int q = sg.row_len / 4;                 // float4 per row
-    const int64_t rows_per_block = kAdamThreads / q;
-    const int64_t ri = lb * rows_per_block + threadIdx.x / q;
-    const int part = threadIdx.x % q;
-    if (threadIdx.x < rows_per_block * q && ri < sg.n) {
-      const int64_t base = (int64_t)sg.rows[ri] * sg.row_len + part * 4;
-      const int64_t sbase = ri * sg.row_len + part * 4;
-      f32x4 p = *reinterpret_cast<const f32x4*>(sg.param + base);
-      const int64_t gbase = sg.grad_rows ? sbase : base;
-      const f32x4 g = *reinterpret_cast<const f32x4*>(sg.grad + gbase);
-      f32x4 m = *reinterpret_cast<const f32x4*>(sg.exp_avg + sbase);
-      f32x4 v = *reinterpret_cast<const f32x4*>(sg.exp_avg_sq + sbase);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float pk = p[k], mk = m[k], vk = v[k];
-        adam_one(pk, g[k], mk, vk, c);
-        p[k] = pk;
-        m[k] = mk;
-        v[k] = vk;
-      }
-      *reinterpret_cast<f32x4*>(sg.param + base) = p;
-      *reinterpret_cast<f32x4*>(sg.exp_avg + sbase) = m;
-      *reinterpret_cast<f32x4*>(sg.exp_avg_sq + sbase) = v;
-      if (a.zero_grad) *reinterpret_cast<f32x4*>(sg.grad + gbase) = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
+  adam_segment_block(sg, c, b - a.blk0[s], a.zero_grad, (int)threadIdx.x, kAdamThreads);
   if (a.ticket) {
     // Every workgroup read its segment's step count at its start (the value was consumed long
     // before this point), so once all of them have drawn a ticket no read is outstanding and the

@@ -1554,70 +1554,87 @@ __global__ __launch_bounds__(256, 2) void k_dec_bwd_multi_sum(QueryKArgs a, Mult
 // == base) — param, exp_avg, exp_avg_sq and the packed mirror are written, base is left g (or 0 with
 // zero_grad), and the last workgroup advances the step count by the ticket (k_adam's protocol), so a
 // mapping iteration's decoder update needs no separate launch after its weight-gradient reduction.
+// ABI v14: further segments (the colour grid's frustum rows) ride in the same launch as workgroups
+// past the reduction's, each running k_adam's segment update (adam_segment_block).
+constexpr int kSlabAdamExtra = 3;
 struct SlabAdam {
   nslam_adam_seg seg;
   float b1, b2, eps;
   int32_t zero_grad;
   uint32_t* ticket;
   int32_t on;
+  int32_t n_extra;
+  nslam_adam_seg extra[kSlabAdamExtra];
+  int64_t extra_blk0[kSlabAdamExtra + 1];  // first workgroup of each extra segment, past the reduction's
 };
 constexpr int kReduceWaves = 16;
 static __global__ __launch_bounds__(64 * kReduceWaves) void k_slab_reduce(const float* __restrict__ slab, int64_t nslab,
                                                                    int acc_floats, int count,
                                                                    float* __restrict__ base, SlabAdam ad) {
   __shared__ f32x4 part[kReduceWaves * 4][16];
-  const int lane = threadIdx.x & 63, wave = wave_id();
-  const int c = lane & 15, r = wave * 4 + (lane >> 4);  // r: slab stream 0..63
-  const int j = (blockIdx.x * 16 + c) * 4;
-  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
-  if (j < count) {
-    const float* p = slab + j;
-    int64_t b = r;
-    for (; b + 64 < nslab; b += 128) {
-      s0 += *reinterpret_cast<const f32x4*>(p + b * acc_floats);
-      s1 += *reinterpret_cast<const f32x4*>(p + (b + 64) * acc_floats);
+  if (ad.on && (int64_t)blockIdx.x >= ad.extra_blk0[0]) {  // an extra segment's Adam workgroup
+    const int64_t b = blockIdx.x;
+    int s = 0;
+    while (s + 1 < ad.n_extra && b >= ad.extra_blk0[s + 1]) ++s;
+    const nslam_adam_seg& sg = ad.extra[s];
+    const AdamCoef co = adam_coef(ad.b1, ad.b2, ad.eps, sg.lr, *sg.step);
+    adam_segment_block(sg, co, b - ad.extra_blk0[s], ad.zero_grad, (int)threadIdx.x, 64 * kReduceWaves);
+  } else {  // the reduction (+ the decoder's Adam)
+    const int lane = threadIdx.x & 63, wave = wave_id();
+    const int c = lane & 15, r = wave * 4 + (lane >> 4);  // r: slab stream 0..63
+    const int j = (blockIdx.x * 16 + c) * 4;
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
+    if (j < count) {
+      const float* p = slab + j;
+      int64_t b = r;
+      for (; b + 64 < nslab; b += 128) {
+        s0 += *reinterpret_cast<const f32x4*>(p + b * acc_floats);
+        s1 += *reinterpret_cast<const f32x4*>(p + (b + 64) * acc_floats);
+      }
+      if (b < nslab) s0 += *reinterpret_cast<const f32x4*>(p + b * acc_floats);
     }
-    if (b < nslab) s0 += *reinterpret_cast<const f32x4*>(p + b * acc_floats);
-  }
-  part[r][c] = s0 + s1;
-  __syncthreads();
-  if (threadIdx.x < 16 && j < count) {
-    f32x4 t = part[0][c];
+    part[r][c] = s0 + s1;
+    __syncthreads();
+    if (threadIdx.x < 16 && j < count) {
+      f32x4 t = part[0][c];
 #pragma unroll 8
-    for (int k = 1; k < kReduceWaves * 4; ++k) t += part[k][c];
-    if (!ad.on) {
+      for (int k = 1; k < kReduceWaves * 4; ++k) t += part[k][c];
+      if (!ad.on) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (j + e < count) base[j + e] += t[e];
-    } else {
-      const nslam_adam_seg& sg = ad.seg;
-      const AdamCoef co = adam_coef(ad.b1, ad.b2, ad.eps, sg.lr, *sg.step);
+        for (int e = 0; e < 4; ++e)
+          if (j + e < count) base[j + e] += t[e];
+      } else {
+        const nslam_adam_seg& sg = ad.seg;
+        const AdamCoef co = adam_coef(ad.b1, ad.b2, ad.eps, sg.lr, *sg.step);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int64_t i = j + e;
-        if (i < count) {
-          const float g = base[i] + t[e];
-          float p = sg.param[i], m = sg.exp_avg[i], v = sg.exp_avg_sq[i];
-          adam_one(p, g, m, v, co);
-          sg.param[i] = p;
-          sg.exp_avg[i] = m;
-          sg.exp_avg_sq[i] = v;
-          base[i] = ad.zero_grad ? 0.f : g;
-          if (sg.mirror) {
-            const int i0 = sg.mirror_idx[2 * i], i1 = sg.mirror_idx[2 * i + 1];
-            if (i0 >= 0) sg.mirror[i0] = p;
-            if (i1 >= 0) sg.mirror[i1] = p;
+        for (int e = 0; e < 4; ++e) {
+          const int64_t i = j + e;
+          if (i < count) {
+            const float g = base[i] + t[e];
+            float p = sg.param[i], m = sg.exp_avg[i], v = sg.exp_avg_sq[i];
+            adam_one(p, g, m, v, co);
+            sg.param[i] = p;
+            sg.exp_avg[i] = m;
+            sg.exp_avg_sq[i] = v;
+            base[i] = ad.zero_grad ? 0.f : g;
+            if (sg.mirror) {
+              const int i0 = sg.mirror_idx[2 * i], i1 = sg.mirror_idx[2 * i + 1];
+              if (i0 >= 0) sg.mirror[i0] = p;
+              if (i1 >= 0) sg.mirror[i1] = p;
+            }
           }
         }
       }
     }
+  
   }
-  if (ad.on) {  // every workgroup has read the step count: the last one advances it (k_adam's ticket)
+  if (ad.on) {  // every workgroup has read its step count: the last one advances them (k_adam's ticket)
     __syncthreads();
     if (threadIdx.x == 0) {
       const uint32_t tk = __hip_atomic_fetch_add(ad.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (tk == gridDim.x - 1) {
         *ad.seg.step += 1.f;
+        for (int k = 0; k < ad.n_extra; ++k) *ad.extra[k].step += 1.f;
         __hip_atomic_store(ad.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -1708,8 +1725,16 @@ inline int slab_reduce(const nslam_dec_grad& dg, float* slab, bool folded, int64
   const int64_t n = folded ? blocks : nslab;
   const int stride = folded ? acc * kWavesBwd : acc;
   SlabAdam ad{};
-  if (adam) ad = *adam;
-  hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)((dg.count + 63) / 64)), dim3(64 * kReduceWaves), 0, s, slab, n,
+  int64_t nblk = (dg.count + 63) / 64;  // the reduction's workgroups, then the extra segments'
+  if (adam) {
+    ad = *adam;
+    for (int k = 0; k < ad.n_extra; ++k) {
+      ad.extra_blk0[k] = nblk;
+      nblk += adam_segment_blocks(ad.extra[k], 64 * kReduceWaves);
+    }
+    ad.extra_blk0[ad.n_extra] = nblk;
+  }
+  hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)nblk), dim3(64 * kReduceWaves), 0, s, slab, n,
                      stride, (int)dg.count, dg.base, ad);
   return hip_status();
 }

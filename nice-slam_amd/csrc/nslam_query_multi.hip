@@ -82,24 +82,45 @@ extern "C" int nslam_color_wgrad(const nslam_query_cfg* cfg, int64_t n_pts, void
   return launch_color_wgrad(a, reinterpret_cast<float*>(ws), reinterpret_cast<hipStream_t>(stream));
 }
 
-// ABI v12: nslam_color_wgrad, then the colour decoder's Adam step inside the slab reduction (one
-// launch fewer on the mapping iteration's critical path).  seg: the decoder's dense segment (its grad
-// is cfg->dgrad[COLOR].base, count elements); the same element update as nslam_adam_step.
+// ABI v12/v14: nslam_color_wgrad, then the Adam step of the colour decoder (segs[0]: its dense
+// segment, grad == cfg->dgrad[COLOR].base) and of up to kSlabAdamExtra further segments (segs[1..]:
+// e.g. the colour grid's frustum rows) inside the slab-reduction launch — one launch fewer on the
+// mapping iteration's critical path.  The same element update as nslam_adam_step.
 extern "C" int nslam_color_wgrad_adam(const nslam_query_cfg* cfg, int64_t n_pts, void* ws, size_t ws_bytes,
-                                      const nslam_adam_seg* seg, float beta1, float beta2, float eps,
-                                      int32_t zero_grad, uint32_t* ticket, void* stream) {
+                                      const nslam_adam_seg* segs, int32_t n_segs, float beta1, float beta2,
+                                      float eps, int32_t zero_grad, uint32_t* ticket, void* stream) {
   const int rc = check_cfg(cfg, true);
   if (rc) return rc;
-  if (cfg->stage != NSLAM_STAGE_COLOR || n_pts < 0 || !seg || !ticket) return NSLAM_EINVAL;
+  if (cfg->stage != NSLAM_STAGE_COLOR || n_pts < 0 || !segs || n_segs < 1 || n_segs > 1 + kSlabAdamExtra || !ticket)
+    return NSLAM_EINVAL;
   const nslam_dec_grad& dg = cfg->dgrad[NSLAM_DEC_COLOR];
   if (!dg.base || dg.count <= 0 || cfg->need_pts_grad) return NSLAM_EUNSUPPORTED;
-  if (seg->rows || seg->grad != dg.base || seg->n != dg.count || !seg->step || !seg->param || !seg->exp_avg ||
-      !seg->exp_avg_sq || (seg->mirror && !seg->mirror_idx))
+  const nslam_adam_seg& seg = segs[0];
+  if (seg.rows || seg.grad != dg.base || seg.n != dg.count || !seg.step || !seg.param || !seg.exp_avg ||
+      !seg.exp_avg_sq || (seg.mirror && !seg.mirror_idx))
     return NSLAM_EINVAL;
+  SlabAdam ad{};
+  ad.seg = seg;
+  ad.b1 = beta1;
+  ad.b2 = beta2;
+  ad.eps = eps;
+  ad.zero_grad = zero_grad;
+  ad.ticket = ticket;
+  ad.on = 1;
+  ad.n_extra = n_segs - 1;
+  for (int k = 1; k < n_segs; ++k) {  // nslam_adam_step's checks
+    const nslam_adam_seg& g = segs[k];
+    if (g.n <= 0 || !g.step || !g.param || !g.grad || !g.exp_avg || !g.exp_avg_sq) return NSLAM_EINVAL;
+    if (g.rows) {
+      if (g.row_len <= 0 || g.row_len % 4 || g.row_len / 4 > 64 * kReduceWaves) return NSLAM_EINVAL;
+      const uintptr_t al = (uintptr_t)g.param | (uintptr_t)g.grad | (uintptr_t)g.exp_avg | (uintptr_t)g.exp_avg_sq;
+      if (al & 15) return NSLAM_EINVAL;
+    }
+    ad.extra[k - 1] = g;
+  }
   if (n_pts == 0) return NSLAM_OK;  // (nothing to reduce: like a segment without a gradient, no step)
   if (!cw_tape_path(cfg)) return NSLAM_EUNSUPPORTED;
   if (!ws || ws_bytes < dec_ws_bytes(cfg, NSLAM_DEC_COLOR, n_pts)) return NSLAM_EWORKSPACE;
   QueryKArgs a{*cfg, nullptr, n_pts, nullptr, nullptr, nullptr};
-  SlabAdam ad{*seg, beta1, beta2, eps, zero_grad, ticket, 1};
   return launch_color_wgrad(a, reinterpret_cast<float*>(ws), reinterpret_cast<hipStream_t>(stream), &ad);
 }

@@ -120,8 +120,7 @@ class MappingEngine:
         # ABI v12: with per-branch Adam the colour branch runs its lean chain, forks the colour grid's
         # Adam onto a side stream, and folds the colour decoder's Adam step into the weight-gradient
         # slab reduction (nslam_color_wgrad_adam) — no Adam launch after the reduction
-        self.fuse_adam = True
-        self._gadam_stream = None
+        self.fuse_adam = os.environ.get("NSLAM_FUSE_ADAM", "1") != "0"
         # Cross-iteration pipelining (colour stage, one rank, per-branch Adam, ray prefetch): the colour
         # branch (lean chain -> weight gradients + decoder Adam, colour-grid Adam beside it) stays on
         # its own stream past the end of iteration(), and the next iteration's forward is split
@@ -131,10 +130,8 @@ class MappingEngine:
         # left (the same dependencies as the serial loop).  Callers join() before reading the colour
         # decoder / grid or ending a graph capture.
         self.pipeline = False
-        self.pipe_order = int(os.environ.get("NSLAM_PIPE_ORDER", "0"))  # capture-order experiment
         self._col_pending = False
         self._col_stream = None   # the colour branch (+ the next forward's colour part)
-        self._frz_stream = None   # the frozen decoders' branch
         self._hi = None
         for k, v in c.items():
             if not v.is_contiguous(memory_format=torch.channels_last_3d):
@@ -265,7 +262,6 @@ class MappingEngine:
                 streams = [self._side[len(units) - 1]]
             streams += self._side[:len(units) - 1]
         used = [st for st in streams if st is not main]
-        joins = []  # further side streams forked inside a branch (the fused colour branch's grid Adam)
         summed = False
         with ops._span("query_bwd"):
             for st in used:  # fork: every branch starts from the same point of the main stream
@@ -310,18 +306,11 @@ class MappingEngine:
                                  and on_branch is not None and hasattr(on_branch, "color_wgrad")
                                  and self._tape is not None and self._saved is not None)
                         with ops._span("query_bwd." + name):  # this branch alone, on its own stream
-                            if fused:  # lean chain | colour-grid Adam (side) | weight gradients + decoder Adam
+                            if fused:  # lean chain, then weight gradients + the colour Adam in the reduction
                                 rc = lib().nslam_query_bwd_decoders(ctypes.byref(cfg), (1 << d) | _lib.BWD_DEFER_WGRAD,
                                                                     None, n, ptr(g_raw), (ctypes.c_void_p * 4)(),
                                                                     ptr(ws), wsb, st.cuda_stream)
                                 check(rc, "nslam_query_bwd_decoders(colour lean)")
-                                if self._gadam_stream is None:
-                                    self._gadam_stream = torch.cuda.Stream(z.device)
-                                gs = self._gadam_stream
-                                gs.wait_stream(st)
-                                with torch.cuda.stream(gs):
-                                    on_branch(names, part="grids")
-                                joins.append(gs)
                                 on_branch.color_wgrad(cfg, n, ws, wsb, st)
                             else:
                                 rc = lib().nslam_query_bwd_decoder(ctypes.byref(cfg), d, 0, None, n, ptr(g_raw),
@@ -335,7 +324,7 @@ class MappingEngine:
                 if pts_grad and st is not main:
                     for name in names:
                         gp[decs.index(name)].record_stream(st)
-            for st in used + joins:
+            for st in used:
                 main.wait_stream(st)
         if pts_grad and summed:
             return gp[0]
@@ -398,16 +387,14 @@ class MappingEngine:
     def _pipe_streams(self):
         if self._col_stream is None:
             self._col_stream = torch.cuda.Stream(self.device)
-            self._frz_stream = torch.cuda.Stream(self.device)
-            self._gadam_stream = self._gadam_stream or torch.cuda.Stream(self.device)
-        return self._col_stream, self._frz_stream, self._gadam_stream
+        return self._col_stream
 
     def _query_fwd_pipelined(self, ro, rd, z):
         """Colour-stage forward as two launches: middle | fine on the current stream, colour on the
         colour stream (behind the previous iteration's colour branch); returns raw (occupancy of the
         middle decoder deferred into self.occ_add, as query_fwd(defer_occ=True))."""
         main = torch.cuda.current_stream(self.device)
-        sc, _, _ = self._pipe_streams()
+        sc = self._pipe_streams()
         n = z.numel()
         raw = torch.empty(n, 4, dtype=torch.float32, device=z.device)
         self._saved = torch.empty(lib().nslam_query_saved_size(n), dtype=torch.uint8, device=z.device)
@@ -416,10 +403,12 @@ class MappingEngine:
         cfg.defer_occ = 1
         wsb = lib().nslam_query_fwd_workspace_size(ctypes.byref(cfg), n)
         ws = torch.empty(wsb, dtype=torch.uint8, device=z.device)
+        # fork BEFORE the middle | fine launch: the colour half needs the rays and the buffers just
+        # allocated on main, and (in stream order on sc) the previous iteration's colour branch
+        sc.wait_stream(main)
         with ops._span("query_fwd.middle+fine"):
             rc = lib().nslam_query_fwd_parts(ctypes.byref(cfg), None, n, ptr(raw), ptr(ws), wsb, 3, main.cuda_stream)
         check(rc, "nslam_query_fwd_parts(middle | fine)")
-        sc.wait_stream(main)  # the rays, and the buffers just allocated on main
         with torch.cuda.stream(sc):
             with ops._span("query_fwd.color"):
                 rc = lib().nslam_query_fwd_parts(ctypes.byref(cfg), None, n, ptr(raw), ptr(ws), wsb, 4,
@@ -431,17 +420,16 @@ class MappingEngine:
 
     def _query_bwd_pipelined(self, ro, rd, z, g_raw, keys, frozen, on_branch):
         """The colour stage's backward with per-branch Adam: the colour stream runs the colour lean
-        chain, then the weight gradients with the decoder's Adam, and is NOT joined into the current
-        stream (the next iteration's colour forward queues behind it); the current stream runs the
-        frozen decoders' merged mask-only launch and the middle / fine grids' Adam, then — once the
-        colour lean chain is done — the colour grid's Adam.  So the next forward's middle | fine half
-        follows every grid update but not the colour weight gradients.  (Stream topology chosen for
-        hipGraph capture on this stack: a stream forked off the colour stream and joined back into
-        it crashes hipStreamEndCapture, tools/probes/capture_topology.py pattern t3; and a separate
-        frozen-branch stream was serialised behind the weight gradients by the graph's queue
-        assignment.)"""
+        chain, then the weight gradients with the colour decoder's and colour grid's Adam in the
+        reduction (ABI v14), and is NOT joined into the current stream (the next iteration's colour
+        forward queues behind it); the current stream runs the frozen decoders' merged mask-only
+        launch and the middle / fine grids' Adam.  So the next forward's middle | fine half (which
+        reads neither the colour grid nor the colour decoder) does not wait for the colour branch.
+        (Stream topology chosen for hipGraph capture on this stack: a stream forked off the colour
+        stream and joined back into it crashes hipStreamEndCapture, tools/probes/capture_topology.py
+        pattern t3.)"""
         main = torch.cuda.current_stream(self.device)
-        sc, _, _ = self._pipe_streams()
+        sc = self._pipe_streams()
         n = z.numel()
         cfg = self._cfg("color", ro, rd, z, keys, ("color",))
         cfg.need_pts_grad = 0
@@ -454,41 +442,23 @@ class MappingEngine:
         mask = 0
         for name in frozen:
             mask |= 1 << ops._DEC_ID[name]
-        def frozen_launch():
-            with ops._span("query_bwd." + "+".join(frozen)):
-                rc = lib().nslam_query_bwd_decoders(ctypes.byref(cfg), mask, None, n, ptr(g_raw),
-                                                    (ctypes.c_void_p * 4)(), None, 0, main.cuda_stream)
-            check(rc, "nslam_query_bwd_decoders")
-
-        order = self.pipe_order
         with ops._span("query_bwd"):
             sc.wait_stream(main)
             for t in (ro, rd, z, g_raw, self._saved, self._tape, ws):
                 t.record_stream(sc)
-            if order == 1:
-                frozen_launch()
             with torch.cuda.stream(sc):
-                with ops._span("query_bwd.color_lean"):
+                with ops._span("query_bwd.color"):
                     rc = lib().nslam_query_bwd_decoders(ctypes.byref(cfg), (1 << dcol) | _lib.BWD_DEFER_WGRAD, None, n,
                                                         ptr(g_raw), (ctypes.c_void_p * 4)(), ptr(ws), wsb,
                                                         sc.cuda_stream)
-                check(rc, "nslam_query_bwd_decoders(colour lean)")
-            if order != 1:
-                frozen_launch()
-            if order == 2:  # the colour grid's Adam on the colour stream too: no join in the backward
-                on_branch(frozen)
-                with torch.cuda.stream(sc):
-                    on_branch(["color"], part="grids")
-                    with ops._span("query_bwd.color_wgrad"):
-                        on_branch.color_wgrad(cfg, n, ws, wsb, sc)
-                self._col_pending = True  # the next prefetch reuses this batch's rays: it waits for sc
-                return
+                    check(rc, "nslam_query_bwd_decoders(colour lean)")
+                    on_branch.color_wgrad(cfg, n, ws, wsb, sc)  # (+ the colour decoder's and grid's Adam)
+            with ops._span("query_bwd." + "+".join(frozen)):
+                rc = lib().nslam_query_bwd_decoders(ctypes.byref(cfg), mask, None, n, ptr(g_raw),
+                                                    (ctypes.c_void_p * 4)(), None, 0, main.cuda_stream)
+            check(rc, "nslam_query_bwd_decoders")
             on_branch(frozen)
-            main.wait_stream(sc)  # the colour lean chain (its grid gradient) is done; the next
-            on_branch(["color"], part="grids")  # prefetch, which reuses this batch's rays, follows it
-            with torch.cuda.stream(sc):
-                with ops._span("query_bwd.color_wgrad"):
-                    on_branch.color_wgrad(cfg, n, ws, wsb, sc)
+            self._col_pending = True  # the next prefetch reuses this batch's rays: it waits for sc
 
     # -- one iteration ---------------------------------------------------------------------------
     def grads_for(self, stage, trainable_decoders):
@@ -608,20 +578,21 @@ class MappingEngine:
             # one rank: each decoder branch updates its own grid's rows (+ the trainable decoder's
             # parameters, after its slab reduction) on its own stream — the update of a grid needs
             # that branch's gradients alone, so no branch waits for the others before its Adam
-            def on_branch(names, part=None):  # the decoders of one launch: one Adam call for their grids
+            def on_branch(names):  # the decoders of one launch: one Adam call for their grids
                 sub = {}
                 for name in names:
                     if _GRID_OF[name] in keys:
                         sub[self.c[_GRID_OF[name]]] = grads[self.c[_GRID_OF[name]]]
-                    if name in dnames and part != "grids":
+                    if name in dnames:
                         sub[self.decs[name].param] = grads[self.decs[name].param]
                 if sub:
                     optimizer.step(grads=sub, zero_grad=clean)
 
             if hasattr(optimizer, "color_wgrad_step"):
-                def color_wgrad(cfg, n, ws, wsb, st):  # weight gradients + the decoder's Adam, one reduction
+                def color_wgrad(cfg, n, ws, wsb, st):  # weight gradients + the colour branch's Adam, one reduction
                     p = self.decs["color"].param
-                    optimizer.color_wgrad_step(cfg, n, ws, wsb, p, grads[p], zero_grad=clean, stream=st)
+                    extra = {self.c[k]: grads[self.c[k]] for k in ("grid_color",) if k in keys}
+                    optimizer.color_wgrad_step(cfg, n, ws, wsb, p, grads[p], extra=extra, zero_grad=clean, stream=st)
 
                 on_branch.color_wgrad = color_wgrad
         if pipe:

@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_strerror(pkg):
     L = pkg._lib.lib()
-    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 13
+    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 14
     assert L.nslam_strerror(0) == b"ok"
     assert b"invalid" in L.nslam_strerror(-1)
 
@@ -173,13 +173,15 @@ def test_v12_color_wgrad_adam_validates_without_gpu(pkg):
     cfg = pkg._lib.NslamQueryCfg()
     seg = pkg._lib.NslamAdamSeg()
     cfg.stage = 7
-    assert L.nslam_color_wgrad_adam(ctypes.byref(cfg), 10, None, 0, ctypes.byref(seg), 0.9, 0.999, 1e-8, 0, None,
+    assert L.nslam_color_wgrad_adam(ctypes.byref(cfg), 10, None, 0, ctypes.byref(seg), 1, 0.9, 0.999, 1e-8, 0, None,
                                     None) == -1                                          # bad stage
     cfg.stage = pkg._lib.STAGES["middle"]
-    assert L.nslam_color_wgrad_adam(ctypes.byref(cfg), 10, None, 0, ctypes.byref(seg), 0.9, 0.999, 1e-8, 0, None,
+    assert L.nslam_color_wgrad_adam(ctypes.byref(cfg), 10, None, 0, ctypes.byref(seg), 1, 0.9, 0.999, 1e-8, 0, None,
                                     None) < 0                                            # not the colour stage
     cfg.stage = pkg._lib.STAGES["color"]
-    assert L.nslam_color_wgrad_adam(ctypes.byref(cfg), 10, None, 0, None, 0.9, 0.999, 1e-8, 0, None, None) < 0
+    assert L.nslam_color_wgrad_adam(ctypes.byref(cfg), 10, None, 0, None, 1, 0.9, 0.999, 1e-8, 0, None, None) < 0
+    assert L.nslam_color_wgrad_adam(ctypes.byref(cfg), 10, None, 0, ctypes.byref(seg), 5, 0.9, 0.999, 1e-8, 0, None,
+                                    None) < 0                                            # too many segments
 
 
 def test_v13_query_fwd_parts_validates_without_gpu(pkg):

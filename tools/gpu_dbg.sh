@@ -1,13 +1,20 @@
-# capture-order experiment of the pipelined mapping iteration (quick bench per variant + one timeline)
+# fused colour Adam (ABI v14) vs separate Adam, pipelined vs not: quick bench per variant + timelines
 set -o pipefail
-mkdir -p gpurun_out/r3f
-for V in 0 1 2; do
-  NSLAM_PIPE_ORDER=$V timeout -k 10 200 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-stress --no-bulk --no-frames --pipeline > gpurun_out/r3f/o$V.json 2> gpurun_out/r3f/o$V.err || { tail -5 gpurun_out/r3f/o$V.err; exit 1; }
-  python -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[2], round(d['value']/1e6,1), 'M/s', round(d['ms_per_step'],4))" gpurun_out/r3f/o$V.json order$V
-done
-timeout -k 10 200 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-stress --no-bulk --no-frames --no-pipeline > gpurun_out/r3f/nopipe.json 2> gpurun_out/r3f/nopipe.err || exit 1
-python -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print('nopipe', round(d['value']/1e6,1), 'M/s', round(d['ms_per_step'],4))" gpurun_out/r3f/nopipe.json
-for V in 1 2; do
-NSLAM_PIPE_ORDER=$V timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r3f/trace$V -o run -- python bench.py --steps 8 --warmup 3 --no-cpu-baseline --no-stress --no-frames --no-bulk --pipeline > gpurun_out/r3f/trace$V.log 2>&1 || exit 1
-python tools/timeline.py gpurun_out/r3f/trace$V/run_kernel_trace.csv 7 > gpurun_out/r3f/timeline$V.txt && cat gpurun_out/r3f/timeline$V.txt
+mkdir -p gpurun_out/r3h
+run() {  # name, env..., (BARGS: bench args)
+  local n=$1; shift
+  env "$@" timeout -k 10 200 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-stress --no-bulk --no-frames $BARGS > gpurun_out/r3h/$n.json 2> gpurun_out/r3h/$n.err || { tail -5 gpurun_out/r3h/$n.err; exit 1; }
+  python -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[2], round(d['value']/1e6,1), 'M/s', round(d['ms_per_step'],4))" gpurun_out/r3h/$n.json $n
+}
+timeout -k 10 300 python -u -m pytest tests/test_gpu_fused.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r3h/fused_tests.log 2>&1 || { tail -30 gpurun_out/r3h/fused_tests.log; exit 1; }
+tail -1 gpurun_out/r3h/fused_tests.log
+BARGS= run fused NSLAM_FUSE_ADAM=1
+BARGS= run unfused NSLAM_FUSE_ADAM=0
+BARGS=--pipeline run pipe NSLAM_FUSE_ADAM=1
+BARGS= run fused2 NSLAM_FUSE_ADAM=1
+BARGS= run unfused2 NSLAM_FUSE_ADAM=0
+for V in fused pipe; do
+  if [ $V = pipe ]; then A=--pipeline; else A=; fi
+  timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r3h/trace_$V -o run -- python bench.py --steps 8 --warmup 3 --no-cpu-baseline --no-stress --no-frames --no-bulk $A > gpurun_out/r3h/trace_$V.log 2>&1 || exit 1
+  python tools/timeline.py gpurun_out/r3h/trace_$V/run_kernel_trace.csv 7 > gpurun_out/r3h/timeline_$V.txt && echo "== $V" && cat gpurun_out/r3h/timeline_$V.txt
 done
