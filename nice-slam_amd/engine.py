@@ -117,16 +117,19 @@ class MappingEngine:
         # merged d/dpts summed inside the launch (NSLAM_BWD_SUM_PTS, one workgroup per tile): measured
         # 0.109 vs 0.102 ms per tracking iteration for per-decoder buffers + two adds — kept off
         self.sum_pts = False
-        # ABI v12: with per-branch Adam the colour branch runs its lean chain, forks the colour grid's
-        # Adam onto a side stream, and folds the colour decoder's Adam step into the weight-gradient
-        # slab reduction (nslam_color_wgrad_adam) — no Adam launch after the reduction
-        self.fuse_adam = os.environ.get("NSLAM_FUSE_ADAM", "1") != "0"
-        # Cross-iteration pipelining (colour stage, one rank, per-branch Adam, ray prefetch): the colour
-        # branch (lean chain -> weight gradients + decoder Adam, colour-grid Adam beside it) stays on
-        # its own stream past the end of iteration(), and the next iteration's forward is split
-        # (ABI v13 nslam_query_fwd_parts): its middle | fine parts — which read neither the colour grid
-        # nor the colour decoder — start as soon as the frozen branch's grid Adam is done, its colour
-        # part queues behind the colour branch.  Every iteration still sees the map its predecessor
+        # ABI v14: with per-branch Adam the colour branch may fold the colour decoder's and colour
+        # grid's Adam step into the weight-gradient slab reduction (nslam_color_wgrad_adam) — one
+        # launch fewer.  Measured 199-203 vs 206-208 M ray-samples/s for the separate Adam launch in
+        # the hipGraph'd room0 iteration (the fused reduction takes 16.7 us against 8.8 + 9.7): off.
+        self.fuse_adam = os.environ.get("NSLAM_FUSE_ADAM", "0") == "1"
+        # Cross-iteration pipelining (colour stage, one rank, per-branch Adam; experiment, off: measured
+        # 181-185 vs 206-208 M ray-samples/s — the two forward halves side by side take 100 us against
+        # the single decoder-parallel launch's 91 us, which the overlap does not win back): the colour
+        # branch (lean chain -> weight gradients with the colour decoder's and grid's Adam, ABI v14)
+        # stays on its own stream past the end of iteration(), and the next iteration's forward is
+        # split (ABI v13 nslam_query_fwd_parts): its middle | fine parts — which read neither the
+        # colour grid nor the colour decoder — start as soon as the frozen branch's grid Adam is done,
+        # its colour part queues behind the colour branch.  Every iteration still sees the map its predecessor
         # left (the same dependencies as the serial loop).  Callers join() before reading the colour
         # decoder / grid or ending a graph capture.
         self.pipeline = False
@@ -551,7 +554,7 @@ class MappingEngine:
             ro, rd, gd, gc, keep, z = rays()
         keys, dnames = self.grads_for(stage, trainable_decoders)
         mirror = hasattr(optimizer, "set_mirror")
-        pipe = (self.pipeline and self.fuse_adam and stage == "color" and tuple(dnames) == ("color",)
+        pipe = (self.pipeline and stage == "color" and tuple(dnames) == ("color",)
                 and exchange is None and allreduce is None and mirror and hasattr(optimizer, "color_wgrad_step"))
         if not pipe:
             self.join()  # a pipelined predecessor's colour branch must finish before a serial iteration
