@@ -122,6 +122,10 @@ class MappingEngine:
         # launch fewer.  Measured 199-203 vs 206-208 M ray-samples/s for the separate Adam launch in
         # the hipGraph'd room0 iteration (the fused reduction takes 16.7 us against 8.8 + 9.7): off.
         self.fuse_adam = os.environ.get("NSLAM_FUSE_ADAM", "0") == "1"
+        # the colour grid's Adam in the frozen branch's Adam call (that stream waits for the colour
+        # lean chain), off the colour branch's critical path: lean -> weight gradients -> decoder Adam
+        self.cgrid_side = os.environ.get("NSLAM_CGRID_SIDE", "1") == "1"
+        self._lean_ev = None
         # Cross-iteration pipelining (colour stage, one rank, per-branch Adam; experiment, off: measured
         # 181-185 vs 206-208 M ray-samples/s — the two forward halves side by side take 100 us against
         # the single decoder-parallel launch's 91 us, which the overlap does not win back): the colour
@@ -265,6 +269,7 @@ class MappingEngine:
                 streams = [self._side[len(units) - 1]]
             streams += self._side[:len(units) - 1]
         used = [st for st in streams if st is not main]
+        cgrid_ev = None  # the colour lean chain's completion, when the colour grid's Adam joins the frozen branch
         summed = False
         with ops._span("query_bwd"):
             for st in used:  # fork: every branch starts from the same point of the main stream
@@ -305,16 +310,29 @@ class MappingEngine:
                         d = ops._DEC_ID[name]
                         wsb = lib().nslam_query_bwd_decoder_workspace_size(ctypes.byref(cfg), d, n)
                         ws = torch.empty(wsb, dtype=torch.uint8, device=z.device) if wsb else None
-                        fused = (name == "color" and name in dec_grads and self.fuse_adam and not pts_grad
-                                 and on_branch is not None and hasattr(on_branch, "color_wgrad")
-                                 and self._tape is not None and self._saved is not None)
+                        tape_bwd = (name == "color" and name in dec_grads and not pts_grad and on_branch is not None
+                                    and hasattr(on_branch, "color_wgrad") and self._tape is not None
+                                    and self._saved is not None)
+                        # the colour grid's Adam beside the weight gradients, in the frozen branch's Adam
+                        cside = tape_bwd and self.cgrid_side and any(len(u) > 1 for u in units) and concurrent
+                        fused = tape_bwd and (self.fuse_adam or cside)
                         with ops._span("query_bwd." + name):  # this branch alone, on its own stream
-                            if fused:  # lean chain, then weight gradients + the colour Adam in the reduction
+                            if fused:  # lean chain, then weight gradients (+ the colour Adam in the reduction)
                                 rc = lib().nslam_query_bwd_decoders(ctypes.byref(cfg), (1 << d) | _lib.BWD_DEFER_WGRAD,
                                                                     None, n, ptr(g_raw), (ctypes.c_void_p * 4)(),
                                                                     ptr(ws), wsb, st.cuda_stream)
                                 check(rc, "nslam_query_bwd_decoders(colour lean)")
-                                on_branch.color_wgrad(cfg, n, ws, wsb, st)
+                                if cside:
+                                    if self._lean_ev is None:  # one persistent event (never destroyed mid-capture)
+                                        self._lean_ev = torch.cuda.Event()
+                                    self._lean_ev.record(st)
+                                    cgrid_ev = self._lean_ev
+                                if self.fuse_adam:
+                                    on_branch.color_wgrad(cfg, n, ws, wsb, st, grids=not cside)
+                                else:
+                                    rc = lib().nslam_color_wgrad(ctypes.byref(cfg), n, ptr(ws), wsb, st.cuda_stream)
+                                    check(rc, "nslam_color_wgrad")
+                                    on_branch(names, part="decoders")
                             else:
                                 rc = lib().nslam_query_bwd_decoder(ctypes.byref(cfg), d, 0, None, n, ptr(g_raw),
                                                                    ptr(gp[decs.index(name)]) if pts_grad else None,
@@ -323,7 +341,12 @@ class MappingEngine:
                         if fused:
                             continue
                     if on_branch is not None:
-                        on_branch(names)
+                        if cgrid_ev is not None and len(names) > 1:  # + the colour grid, once its lean chain is done
+                            st.wait_event(cgrid_ev)
+                            on_branch(list(names) + ["color"], part="grids")
+                            cgrid_ev = None
+                        else:
+                            on_branch(names)
                 if pts_grad and st is not main:
                     for name in names:
                         gp[decs.index(name)].record_stream(st)
@@ -581,20 +604,20 @@ class MappingEngine:
             # one rank: each decoder branch updates its own grid's rows (+ the trainable decoder's
             # parameters, after its slab reduction) on its own stream — the update of a grid needs
             # that branch's gradients alone, so no branch waits for the others before its Adam
-            def on_branch(names):  # the decoders of one launch: one Adam call for their grids
-                sub = {}
+            def on_branch(names, part=None):  # the decoders of one launch: one Adam call for their grids
+                sub = {}                         # (part "grids" / "decoders": only those)
                 for name in names:
-                    if _GRID_OF[name] in keys:
+                    if _GRID_OF[name] in keys and part != "decoders":
                         sub[self.c[_GRID_OF[name]]] = grads[self.c[_GRID_OF[name]]]
-                    if name in dnames:
+                    if name in dnames and part != "grids":
                         sub[self.decs[name].param] = grads[self.decs[name].param]
                 if sub:
                     optimizer.step(grads=sub, zero_grad=clean)
 
             if hasattr(optimizer, "color_wgrad_step"):
-                def color_wgrad(cfg, n, ws, wsb, st):  # weight gradients + the colour branch's Adam, one reduction
+                def color_wgrad(cfg, n, ws, wsb, st, grids=True):  # weight gradients + the colour Adam, one reduction
                     p = self.decs["color"].param
-                    extra = {self.c[k]: grads[self.c[k]] for k in ("grid_color",) if k in keys}
+                    extra = {self.c[k]: grads[self.c[k]] for k in ("grid_color",) if k in keys and grids}
                     optimizer.color_wgrad_step(cfg, n, ws, wsb, p, grads[p], extra=extra, zero_grad=clean, stream=st)
 
                 on_branch.color_wgrad = color_wgrad
