@@ -864,8 +864,11 @@ def main():
     if not args.eager and not (world > 1 and args.backend == "gloo"):
         try:  # whole mapping iterations as hipGraphs (removes per-op host launch cost); two of them,
             # replayed in turn, since the prefetching engine alternates its ray buffers
-            graph, mode = capture_step_graphs(lambda: scene.step(sharded=sharded), sync=scene.flip_parity,
-                                              tail=scene.join)
+            # blocks of up to 50 iterations per graph: a replay starts only after the previous one
+            # drained (~20 us), paid once per block (block 10 -> 50: ~1.6 us less per iteration)
+            block = 50 if args.steps >= 50 else 10
+            graph, mode = capture_step_graphs(lambda: scene.step(sharded=sharded), block=block,
+                                              sync=scene.flip_parity, tail=scene.join)
             graph.run(graph.block)
             torch.cuda.synchronize()
         except Exception as e:  # pragma: no cover - fall back to eager launches

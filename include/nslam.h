@@ -350,6 +350,15 @@ int nslam_rows_unpack(const float* in, const int32_t* rows, int64_t n_rows, int3
  * NSLAM_EUNSUPPORTED when 3*n_rays*n_samples >= 2^31 (32-bit g_pts offsets). */
 int nslam_cam_grad(const float* cam, const float* c2w, const double* g_pts, const double* z_vals, const float* rays_d,
                    int64_t n_rays, int32_t n_samples, float* g_cam, void* stream);
+/* ABI v15: the same gradient from n_parts (1..4) d/dpts buffers — the frozen decoders' shares of
+ * nslam_query_bwd_decoders — summed per point in buffer order ((g0 + g1) + g2, float64), over up to
+ * 32 workgroups whose partial sums meet in ws (NSLAM_CAM_GRAD_WS_DOUBLES doubles; the last workgroup,
+ * by `ticket` — a device uint32 zeroed once and re-armed by the call — adds them in workgroup order:
+ * deterministic).  Replaces the buffer adds + single-workgroup nslam_cam_grad of a tracking iteration. */
+#define NSLAM_CAM_GRAD_WS_DOUBLES (32 * 12)
+int nslam_cam_grad_parts(const float* cam, const float* c2w, const double* const* g_pts, int32_t n_parts,
+                         const double* z_vals, const float* rays_d, int64_t n_rays, int32_t n_samples, float* g_cam,
+                         double* ws, uint32_t* ticket, void* stream);
 
 /* ABI v9.  c2w [3,4] f32 = get_camera_from_tensor(cam [7]) (common.py:137-176, quad2rotation's
  * products and differences, no FMA contraction), one thread.  |q|² is summed ((w²+x²)+y²)+z²;

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NSLAM_LIB") or os.path.join(_HERE, "libnslam.so")  # NSLAM_LIB: instrumented builds
 
 NSLAM_OK = 0
-ABI_VERSION = 14
+ABI_VERSION = 15
 BWD_SUM_PTS = 0x100  # nslam.h NSLAM_BWD_SUM_PTS (nslam_query_bwd_decoders)
 BWD_DEFER_WGRAD = 0x200  # nslam.h NSLAM_BWD_DEFER_WGRAD (ABI v11; then nslam_color_wgrad)
 STAGES = {"coarse": 0, "middle": 1, "fine": 2, "color": 3}
@@ -117,7 +117,7 @@ EXPORTS = (
     "nslam_render_loss_workspace_size", "nslam_adam_step", "nslam_rows_pack", "nslam_rows_unpack",
     "nslam_query_fwd_ws", "nslam_query_fwd_workspace_size", "nslam_cam_grad", "nslam_cam_pose",
     "nslam_query_tape_size", "nslam_color_wgrad", "nslam_color_wgrad_adam",
-    "nslam_query_fwd_parts",
+    "nslam_query_fwd_parts", "nslam_cam_grad_parts",
 )
 
 _lib = None
@@ -181,6 +181,7 @@ def lib():
         L.nslam_rows_pack.argtypes = [vp, vp, i64, i32, vp, i64, vp, vp]
         L.nslam_rows_unpack.argtypes = [vp, vp, i64, i32, vp, vp, i64, vp]
         L.nslam_cam_grad.argtypes = [vp, vp, vp, vp, vp, i64, i32, vp, vp]
+        L.nslam_cam_grad_parts.argtypes = [vp, vp, ctypes.POINTER(vp), i32, vp, vp, i64, i32, vp, vp, vp, vp]
         L.nslam_cam_pose.argtypes = [vp, vp, vp]
         if L.nslam_abi_version() != ABI_VERSION:
             raise RuntimeError(f"libnslam.so ABI {L.nslam_abi_version()} != {ABI_VERSION}: rebuild it")

@@ -374,6 +374,51 @@ struct CamArgs {
   float* g_cam;
 };
 
+// The epilogue both camera-gradient kernels share (one thread): g_R = A·R, the quaternion VJP of
+// quad2rotation, and the translation part.  red[k][0], k < 12: Σ g (k < 3) and A (k = 3..11).
+__device__ void cam_grad_epilogue(const float* __restrict__ cam, const float* __restrict__ c2w, const double (*red)[kCamThreads / 64],
+                                  float* __restrict__ g_cam) {
+  struct Ax {
+    const float* cam;
+    const float* c2w;
+    float* g_cam;
+  } a{cam, c2w, g_cam};
+  double A[9], R[9], gR[9];
+  for (int k = 0; k < 9; ++k) A[k] = red[3 + k][0];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) R[3 * i + j] = a.c2w[4 * i + j];
+  for (int i = 0; i < 3; ++i)  // g_R = A · R
+    for (int j = 0; j < 3; ++j) gR[3 * i + j] = A[3 * i + 0] * R[j] + A[3 * i + 1] * R[3 + j] + A[3 * i + 2] * R[6 + j];
+  // quad2rotation (common.py:150-159): R = I + s P(q), q = (w, x, y, z) = indices 0..3.
+  // G[a][b] = Σ_ij gR_ij M_ij,ab with the ±1 terms of each entry of P.
+  double G[4][4] = {};
+  const double* g = gR;
+  G[2][2] -= g[0]; G[3][3] -= g[0];
+  G[1][2] += g[1]; G[3][0] -= g[1];
+  G[1][3] += g[2]; G[2][0] += g[2];
+  G[1][2] += g[3]; G[3][0] += g[3];
+  G[1][1] -= g[4]; G[3][3] -= g[4];
+  G[2][3] += g[5]; G[1][0] -= g[5];
+  G[1][3] += g[6]; G[2][0] -= g[6];
+  G[2][3] += g[7]; G[1][0] += g[7];
+  G[1][1] -= g[8]; G[2][2] -= g[8];
+  double q[4], qq = 0.0;
+  for (int k = 0; k < 4; ++k) {
+    q[k] = a.cam[k];
+    qq += q[k] * q[k];
+  }
+  const double s = 2.0 / qq;
+  double Hq[4], qHq = 0.0;
+  for (int i = 0; i < 4; ++i) {
+    double h = 0.0;
+    for (int j = 0; j < 4; ++j) h += (G[i][j] + G[j][i]) * q[j];
+    Hq[i] = h;
+    qHq += q[i] * h;
+  }
+  for (int i = 0; i < 4; ++i) a.g_cam[i] = (float)(s * Hq[i] - 0.5 * s * s * qHq * q[i]);
+  for (int k = 0; k < 3; ++k) a.g_cam[4 + k] = (float)red[k][0];
+}
+
 __global__ __launch_bounds__(kCamThreads) void k_cam_grad(CamArgs a) {
   // One point per thread per step (coalesced g_pts rows): g_t = Σ g and A = Σ_r g_d,r d_rᵀ, which
   // is linear in the points, = Σ_p (z_p g_p) d_r(p)ᵀ; double partials, wave shuffles, then LDS.
@@ -416,40 +461,92 @@ __global__ __launch_bounds__(kCamThreads) void k_cam_grad(CamArgs a) {
   }
   __syncthreads();
   if (threadIdx.x != 0) return;
-  double A[9], R[9], gR[9];
-  for (int k = 0; k < 9; ++k) A[k] = red[3 + k][0];
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) R[3 * i + j] = a.c2w[4 * i + j];
-  for (int i = 0; i < 3; ++i)  // g_R = A · R
-    for (int j = 0; j < 3; ++j) gR[3 * i + j] = A[3 * i + 0] * R[j] + A[3 * i + 1] * R[3 + j] + A[3 * i + 2] * R[6 + j];
-  // quad2rotation (common.py:150-159): R = I + s P(q), q = (w, x, y, z) = indices 0..3.
-  // G[a][b] = Σ_ij gR_ij M_ij,ab with the ±1 terms of each entry of P.
-  double G[4][4] = {};
-  const double* g = gR;
-  G[2][2] -= g[0]; G[3][3] -= g[0];
-  G[1][2] += g[1]; G[3][0] -= g[1];
-  G[1][3] += g[2]; G[2][0] += g[2];
-  G[1][2] += g[3]; G[3][0] += g[3];
-  G[1][1] -= g[4]; G[3][3] -= g[4];
-  G[2][3] += g[5]; G[1][0] -= g[5];
-  G[1][3] += g[6]; G[2][0] -= g[6];
-  G[2][3] += g[7]; G[1][0] += g[7];
-  G[1][1] -= g[8]; G[2][2] -= g[8];
-  double q[4], qq = 0.0;
-  for (int k = 0; k < 4; ++k) {
-    q[k] = a.cam[k];
-    qq += q[k] * q[k];
+  cam_grad_epilogue(a.cam, a.c2w, red, a.g_cam);
+}
+
+// ABI v15: the same gradient from several d/dpts buffers (the frozen decoders' shares, summed per
+// point in buffer order: what the torch adds in front of nslam_cam_grad did, bit for bit) over up to
+// kCamParts workgroups; each writes its 12 partial sums to ws, the last to arrive (ticket) adds them
+// in workgroup order and runs the epilogue (agent-scope release / acquire around the ticket).
+constexpr int kCamParts = 32;
+struct CamPartsArgs {
+  const float* cam;
+  const float* c2w;
+  const double* gp[4];
+  int32_t nbuf;
+  const double* z;
+  const float* rd;
+  int64_t n;
+  int32_t S;
+  float* g_cam;
+  double* ws;  // [kCamParts][12]
+  uint32_t* ticket;
+};
+
+__global__ __launch_bounds__(kCamThreads) void k_cam_grad_parts(CamPartsArgs a) {
+  double acc[12];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) acc[k] = 0.0;
+  const int np = (int)(a.n * a.S);
+  for (int p = blockIdx.x * kCamThreads + threadIdx.x; p < np; p += gridDim.x * kCamThreads) {
+    const int r = p / a.S;
+    const double zs = a.z[p];
+    double g[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      double v = a.gp[0][p * 3 + k];
+      for (int b = 1; b < a.nbuf; ++b) v = v + a.gp[b][p * 3 + k];
+      g[k] = v;
+      acc[k] += v;
+    }
+    const double d0 = a.rd[r * 3], d1 = a.rd[r * 3 + 1], d2 = a.rd[r * 3 + 2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const double gz = zs * g[i];
+      acc[3 + 3 * i] += gz * d0;
+      acc[4 + 3 * i] += gz * d1;
+      acc[5 + 3 * i] += gz * d2;
+    }
   }
-  const double s = 2.0 / qq;
-  double Hq[4], qHq = 0.0;
-  for (int i = 0; i < 4; ++i) {
-    double h = 0.0;
-    for (int j = 0; j < 4; ++j) h += (G[i][j] + G[j][i]) * q[j];
-    Hq[i] = h;
-    qHq += q[i] * h;
+#pragma unroll
+  for (int k = 0; k < 12; ++k)
+    for (int off = 32; off > 0; off >>= 1) acc[k] += __shfl_xor(acc[k], off, 64);
+  __shared__ double red[12][kCamThreads / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 12; ++k) red[k][wave] = acc[k];
   }
-  for (int i = 0; i < 4; ++i) a.g_cam[i] = (float)(s * Hq[i] - 0.5 * s * s * qHq * q[i]);
-  for (int k = 0; k < 3; ++k) a.g_cam[4 + k] = (float)red[k][0];
+  __syncthreads();
+  if (threadIdx.x < 12) {  // fixed-order sum over the waves, published as this workgroup's partial
+    double t = 0.0;
+    for (int w = 0; w < kCamThreads / 64; ++w) t += red[threadIdx.x][w];
+    a.ws[blockIdx.x * 12 + threadIdx.x] = t;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t tk = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    red[0][0] = tk == gridDim.x - 1 ? 1.0 : 0.0;  // "I am last", through the one LDS array
+  }
+  __syncthreads();
+  if (red[0][0] == 0.0) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed for the next call
+  }
+  __syncthreads();
+  double t = 0.0;
+  if (threadIdx.x < 12)  // the workgroups' partials in workgroup order: deterministic
+    for (unsigned w = 0; w < gridDim.x; ++w) t += a.ws[w * 12 + threadIdx.x];
+  __syncthreads();
+  if (threadIdx.x < 12) red[threadIdx.x][0] = t;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  cam_grad_epilogue(a.cam, a.c2w, red, a.g_cam);
 }
 
 }  // namespace
@@ -462,6 +559,35 @@ extern "C" int nslam_cam_grad(const float* cam, const float* c2w, const double* 
   if (n_rays * (int64_t)n_samples * 3 >= (int64_t(1) << 31)) return NSLAM_EUNSUPPORTED;
   CamArgs a{cam, c2w, g_pts, z_vals, rays_d, n_rays, n_samples, g_cam};
   hipLaunchKernelGGL(k_cam_grad, dim3(1), dim3(kCamThreads), 0, reinterpret_cast<hipStream_t>(stream), a);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? NSLAM_OK : NSLAM_EHIP - (int)e;
+}
+
+extern "C" int nslam_cam_grad_parts(const float* cam, const float* c2w, const double* const* g_pts, int32_t n_parts,
+                                    const double* z_vals, const float* rays_d, int64_t n_rays, int32_t n_samples,
+                                    float* g_cam, double* ws, uint32_t* ticket, void* stream) {
+  if (!cam || !c2w || !g_cam || !ticket || !ws || n_rays < 0 || n_samples <= 0) return NSLAM_EINVAL;
+  if (n_parts < 1 || n_parts > 4 || !g_pts) return NSLAM_EINVAL;
+  if (n_rays > 0 && (!z_vals || !rays_d)) return NSLAM_EINVAL;
+  for (int b = 0; b < n_parts; ++b)
+    if (!g_pts[b]) return NSLAM_EINVAL;
+  if (n_rays * (int64_t)n_samples * 3 >= (int64_t(1) << 31)) return NSLAM_EUNSUPPORTED;
+  CamPartsArgs a{};
+  a.cam = cam;
+  a.c2w = c2w;
+  for (int b = 0; b < n_parts; ++b) a.gp[b] = g_pts[b];
+  a.nbuf = n_parts;
+  a.z = z_vals;
+  a.rd = rays_d;
+  a.n = n_rays;
+  a.S = n_samples;
+  a.g_cam = g_cam;
+  a.ws = ws;
+  a.ticket = ticket;
+  const int64_t np = n_rays * (int64_t)n_samples;
+  int64_t wg = (np + kCamThreads - 1) / kCamThreads;
+  wg = wg < 1 ? 1 : (wg > kCamParts ? kCamParts : wg);
+  hipLaunchKernelGGL(k_cam_grad_parts, dim3((unsigned)wg), dim3(kCamThreads), 0, reinterpret_cast<hipStream_t>(stream), a);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? NSLAM_OK : NSLAM_EHIP - (int)e;
 }

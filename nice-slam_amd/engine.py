@@ -223,7 +223,7 @@ class MappingEngine:
         return raw
 
     def query_bwd(self, stage, ro, rd, z, g_raw, grid_grads, dec_grads, concurrent=None, pts_grad=False,
-                  on_branch=None):
+                  on_branch=None, pts_parts=False):
         """Backward into the engine's gradient buffers.  The decoders write disjoint buffers, so
         each runs as its own launch; with `concurrent` the frozen decoders (mask-only backward,
         atomics-heavy) run on side streams beside the one with weight gradients (MFMA-heavy) —
@@ -354,6 +354,8 @@ class MappingEngine:
                 main.wait_stream(st)
         if pts_grad and summed:
             return gp[0]
+        if pts_grad and pts_parts:  # the per-decoder shares, for a consumer that sums them itself
+            return gp
         if pts_grad:
             out = gp[0]
             for g in gp[1:]:
@@ -693,6 +695,10 @@ class TrackingEngine:
         self.w_color, self.handle_dynamic, self.use_color = w_color, handle_dynamic, use_color
         self.device = torch.device(device)
         self._c2w = None
+        # ABI v15 nslam_cam_grad_parts: the frozen decoders' d/dpts buffers summed inside a
+        # multi-workgroup camera-gradient kernel (no torch adds, no single-workgroup reduction)
+        self.cam_parts = True
+        self._cam_ws = self._cam_ticket = None
 
     def n_window(self):
         h0, h1, w0, w1 = self.window
@@ -715,11 +721,20 @@ class TrackingEngine:
         _, _, _, ray_loss, g_raw = ops.render_loss(raw, z, gd, gc, keep, mode="tracker", use_color=self.use_color,
                                                    handle_dynamic=self.handle_dynamic, w_color=self.w_color,
                                                    occ_add=self.eng.occ_add)
-        g_pts = self.eng.query_bwd("color", ro, rd, z, g_raw, (), (), pts_grad=True)
         if cam.grad is None:
             cam.grad = torch.empty_like(cam)
-        # the whole pts → rays → c2w → 7-vector chain in one launch
-        ops.cam_grad(cam.detach(), c2w, g_pts, z, rd, cam.grad)
+        if self.cam_parts:  # the decoders' d/dpts shares summed inside the multi-workgroup cam_grad (ABI v15)
+            if self._cam_ws is None:
+                self._cam_ws = torch.zeros(384, dtype=torch.float64, device=cam.device)
+                self._cam_ticket = torch.zeros(1, dtype=torch.int32, device=cam.device)
+            gps = self.eng.query_bwd("color", ro, rd, z, g_raw, (), (), pts_grad=True, pts_parts=True)
+            if torch.is_tensor(gps):
+                gps = [gps]
+            ops.cam_grad_parts(cam.detach(), c2w, gps, z, rd, cam.grad, self._cam_ws, self._cam_ticket)
+        else:
+            g_pts = self.eng.query_bwd("color", ro, rd, z, g_raw, (), (), pts_grad=True)
+            # the whole pts → rays → c2w → 7-vector chain in one launch
+            ops.cam_grad(cam.detach(), c2w, g_pts, z, rd, cam.grad)
         optimizer.step()
         return ray_loss.sum()
 

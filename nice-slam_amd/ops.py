@@ -649,6 +649,24 @@ def cam_grad(cam, c2w, g_pts, z, rd, out):
     return out
 
 
+def cam_grad_parts(cam, c2w, g_pts, z, rd, out, ws, ticket):
+    """nslam_cam_grad_parts (ABI v15): cam_grad from the per-decoder d/dpts buffers g_pts (list of
+    [N*S,3] f64, summed per point in list order inside the kernel) over several workgroups; ws: f64
+    [NSLAM_CAM_GRAD_WS_DOUBLES], ticket: int32 [1] zeroed once (both persistent, one per caller)."""
+    n, S = z.shape
+    for t, dt, shp in ((cam, torch.float32, (7,)), (c2w, torch.float32, (3, 4)), (z, torch.float64, (n, S)),
+                       (rd, torch.float32, (n, 3)), (out, torch.float32, (7,)), (ws, torch.float64, (384,)),
+                       (ticket, torch.int32, (1,))) + tuple((g, torch.float64, (n * S, 3)) for g in g_pts):
+        if t.dtype != dt or tuple(t.shape) != shp or not t.is_contiguous():
+            raise ValueError(f"cam_grad_parts: expected contiguous {dt} {shp}, got {t.dtype} {tuple(t.shape)}")
+    bufs = (ctypes.c_void_p * len(g_pts))(*[ptr(g) for g in g_pts])
+    with _span("cam_grad"):
+        rc = lib().nslam_cam_grad_parts(ptr(cam), ptr(c2w), bufs, len(g_pts), ptr(z), ptr(rd), n, S, ptr(out), ptr(ws),
+                                        ptr(ticket), stream_ptr(cam.device))
+    check(rc, "nslam_cam_grad_parts")
+    return out
+
+
 def render_loss(raw, z, gt_depth, gt_color, keep=None, mode="mapper", use_color=True, handle_dynamic=False,
                 w_color=0.2, want_grad=True, occ_add=None):
     """Mapper/Tracker rendering loss fused with compositing and its backward (see nslam.h).

@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_strerror(pkg):
     L = pkg._lib.lib()
-    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 14
+    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 15
     assert L.nslam_strerror(0) == b"ok"
     assert b"invalid" in L.nslam_strerror(-1)
 
@@ -193,3 +193,17 @@ def test_v13_query_fwd_parts_validates_without_gpu(pkg):
     assert L.nslam_query_fwd_parts(ctypes.byref(cfg), None, 10, None, None, 0, 3, None) == -1    # bad stage
     ok = pkg._lib.NslamQueryCfg()
     assert L.nslam_query_fwd_parts(ctypes.byref(ok), None, 10, None, None, 0, 3, None) < 0      # incomplete cfg
+
+
+def test_v15_cam_grad_parts_validates_without_gpu(pkg):
+    """nslam_cam_grad_parts rejects missing buffers, bad part counts and oversized point counts."""
+    L = pkg._lib.lib()
+    bufs = (ctypes.c_void_p * 4)(64, 64, 64, 64)
+    assert L.nslam_cam_grad_parts(64, 64, bufs, 3, 64, 64, 10, 48, 64, None, 64, None) == -1       # no ws
+    assert L.nslam_cam_grad_parts(64, 64, bufs, 3, 64, 64, 10, 48, 64, 64, None, None) == -1       # no ticket
+    assert L.nslam_cam_grad_parts(64, 64, bufs, 0, 64, 64, 10, 48, 64, 64, 64, None) == -1         # no parts
+    assert L.nslam_cam_grad_parts(64, 64, bufs, 5, 64, 64, 10, 48, 64, 64, 64, None) == -1         # too many
+    bufs[1] = None
+    assert L.nslam_cam_grad_parts(64, 64, bufs, 3, 64, 64, 10, 48, 64, 64, 64, None) == -1         # a NULL part
+    bufs[1] = 64
+    assert L.nslam_cam_grad_parts(64, 64, bufs, 3, 64, 64, (1 << 31) // 3 // 48 + 1, 48, 64, 64, 64, None) == -2

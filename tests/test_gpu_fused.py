@@ -522,6 +522,34 @@ def test_tracking_engine_matches_oracle(tiny):
     assert rel_l2(cam.detach().cpu() - cam0.cpu(), camo.detach() - cam0.cpu()) < 1e-2
 
 
+def test_cam_grad_parts_matches_single_workgroup(tiny):
+    """ABI v15 nslam_cam_grad_parts (decoder d/dpts shares summed in the kernel, several workgroups
+    meeting through a ticket) == the torch adds + single-workgroup nslam_cam_grad, up to the order of
+    the float64 partial sums; repeated calls reuse the re-armed ticket."""
+    import copy
+    sc = Scene(tiny)
+    slam = sc.slam(base_cfg())
+    cam0 = P.common.get_tensor_from_camera(sc.c2w).cuda()
+    pix = torch.randint(400, (200,), generator=torch.Generator().manual_seed(9))
+    out = {}
+    for parts in (True, False):
+        te = P.engine.TrackingEngine(copy.deepcopy(slam.shared_decoders), slam.shared_c, sc.bound, 32, 16,
+                                     (sc.H, sc.W), (sc.fx, sc.fy, sc.cx, sc.cy), ignore_edge=(20, 20), w_color=0.5,
+                                     handle_dynamic=True, use_color=True, device=DEV)
+        te.cam_parts = parts
+        cam = cam0.clone().requires_grad_(True)
+        opt = P.ops.FusedAdam([{"params": [cam], "lr": 0.0}])
+        gs = []
+        for _ in range(3):  # lr 0: the same pose, the same draws -> the same gradient every call
+            te.iteration(cam, sc.depth.cuda(), sc.color.cuda(), (pix % te.n_window()).cuda(), opt)
+            gs.append(cam.grad.detach().clone())
+        out[parts] = gs
+    assert float(out[False][0].abs().sum()) > 0
+    for a, b in zip(out[True], out[False]):
+        assert rel_l2(a, b) < 1e-6
+    assert torch.equal(out[True][0], out[True][1]) and torch.equal(out[True][1], out[True][2])
+
+
 def test_tracker_track_frame_fused_matches_loop(tiny):
     """Tracker.track_frame on the TrackingEngine == the reference loop over optimize_cam_in_batch
     (same generator ⇒ same pixel draws; device-side best-pose selection vs loss.item())."""
