@@ -332,13 +332,14 @@ class MappingEngine:
                                 else:
                                     rc = lib().nslam_color_wgrad(ctypes.byref(cfg), n, ptr(ws), wsb, st.cuda_stream)
                                     check(rc, "nslam_color_wgrad")
-                                    on_branch(names, part="decoders")
                             else:
                                 rc = lib().nslam_query_bwd_decoder(ctypes.byref(cfg), d, 0, None, n, ptr(g_raw),
                                                                    ptr(gp[decs.index(name)]) if pts_grad else None,
                                                                    ptr(ws), wsb, st.cuda_stream)
                                 check(rc, "nslam_query_bwd_decoder")
                         if fused:
+                            if not self.fuse_adam:  # the decoder's Adam (outside the backward's span)
+                                on_branch(names, part="decoders")
                             continue
                     if on_branch is not None:
                         if cgrid_ev is not None and len(names) > 1:  # + the colour grid, once its lean chain is done
