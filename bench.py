@@ -689,8 +689,8 @@ def graph_time(scene, fn, reps):
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
-    try:
-        g, mode = capture_step_graphs(fn, sync=scene.flip_parity, tail=scene.join)
+    try:  # 50-iteration graph blocks, as the headline leg
+        g, mode = capture_step_graphs(fn, block=50, sync=scene.flip_parity, tail=scene.join)
         run = g.run
     except Exception:  # pragma: no cover - eager fallback
         g, mode = None, "eager"
