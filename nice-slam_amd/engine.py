@@ -316,22 +316,28 @@ class MappingEngine:
                         # the colour grid's Adam beside the weight gradients, in the frozen branch's Adam
                         cside = tape_bwd and self.cgrid_side and any(len(u) > 1 for u in units) and concurrent
                         fused = tape_bwd and (self.fuse_adam or cside)
-                        with ops._span("query_bwd." + name):  # this branch alone, on its own stream
+                        # (the split colour backward is timed as its two kernels: the lean chain and the
+                        # weight-gradient reduction have different bounds)
+                        with ops._span("query_bwd." + name) if not fused else ops._NOSPAN:
                             if fused:  # lean chain, then weight gradients (+ the colour Adam in the reduction)
-                                rc = lib().nslam_query_bwd_decoders(ctypes.byref(cfg), (1 << d) | _lib.BWD_DEFER_WGRAD,
-                                                                    None, n, ptr(g_raw), (ctypes.c_void_p * 4)(),
-                                                                    ptr(ws), wsb, st.cuda_stream)
+                                with ops._span("query_bwd.color_lean"):
+                                    rc = lib().nslam_query_bwd_decoders(ctypes.byref(cfg),
+                                                                        (1 << d) | _lib.BWD_DEFER_WGRAD, None, n,
+                                                                        ptr(g_raw), (ctypes.c_void_p * 4)(), ptr(ws),
+                                                                        wsb, st.cuda_stream)
                                 check(rc, "nslam_query_bwd_decoders(colour lean)")
                                 if cside:
                                     if self._lean_ev is None:  # one persistent event (never destroyed mid-capture)
                                         self._lean_ev = torch.cuda.Event()
                                     self._lean_ev.record(st)
                                     cgrid_ev = self._lean_ev
-                                if self.fuse_adam:
-                                    on_branch.color_wgrad(cfg, n, ws, wsb, st, grids=not cside)
-                                else:
-                                    rc = lib().nslam_color_wgrad(ctypes.byref(cfg), n, ptr(ws), wsb, st.cuda_stream)
-                                    check(rc, "nslam_color_wgrad")
+                                with ops._span("query_bwd.color_wgrad"):
+                                    if self.fuse_adam:
+                                        on_branch.color_wgrad(cfg, n, ws, wsb, st, grids=not cside)
+                                    else:
+                                        rc = lib().nslam_color_wgrad(ctypes.byref(cfg), n, ptr(ws), wsb,
+                                                                     st.cuda_stream)
+                                        check(rc, "nslam_color_wgrad")
                             else:
                                 rc = lib().nslam_query_bwd_decoder(ctypes.byref(cfg), d, 0, None, n, ptr(g_raw),
                                                                    ptr(gp[decs.index(name)]) if pts_grad else None,
