@@ -86,6 +86,9 @@ KERNEL_WORK = {
 ATOMIC_SPANS = {"query_bwd.fine": 1024, "query_bwd.middle": 1024, "query_bwd.middle+fine": 2048,
                 "query_bwd.color_lean": 1024}
 ATOMIC_PEAK_GBS = 1300.0
+# plain-store bytes per ray-sample inside an atomic span's WRITE_SIZE (subtracted to get its atomic
+# bytes): the colour lean chain's cotangent tape, 12 images x 4 KiB + 1 KiB of x / g per 32-point tile
+PLAIN_WRITE_PER_SAMPLE = {"query_bwd.color_lean": (12 * 4096 + 1024) / 32}
 # rocprofv3 kernel names behind each span (for the PMC traffic of profiles/*traffic*.json)
 SPAN_KERNELS = {
     "query_fwd": ("k_query_fwd", "k_occ_combine"),
@@ -114,6 +117,19 @@ def pmc_traffic(span, path=None):
         return None
     pats = SPAN_KERNELS.get(span, (span,))
     hits = [v["hbm_bytes_per_launch"] for k, v in kern.items() if any(k.startswith(p) for p in pats)]
+    return sum(hits) if hits else None
+
+
+def pmc_write_bytes(span, path=None):
+    """WRITE_SIZE bytes per launch of `span` from the committed PMC summary (float atomics are
+    counted exactly by WRITE_SIZE, MI355X guide), or None."""
+    try:
+        with open(path or TRAFFIC_FILE) as f:
+            kern = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    pats = SPAN_KERNELS.get(span, (span,))
+    hits = [v["write_size_kib"] * 1024.0 for k, v in kern.items() if any(k.startswith(p) for p in pats)]
     return sum(hits) if hits else None
 
 
@@ -666,11 +682,19 @@ def kernel_roofline(name, avg_ms, pts, traffic_path=None):
     bound = "mfma" if mfma else "hbm"
     extra = {}
     if name in ATOMIC_SPANS:
-        bound, achieved, peak, unit = "atomic", pts * ATOMIC_SPANS[name] / t / 1e9, ATOMIC_PEAK_GBS, "GB/s"
-        extra = {"atomic_bytes_per_sample": ATOMIC_SPANS[name],
-                 "atomic_note": "float-atomic adds into the grid gradient (8 corners x 32 ch x 4 B per sample "
-                                "before the scatter walk merges runs) against ~1.3 TB/s of added bytes chip-wide "
-                                "(MI355X_MICROARCH.md atomics table); mfma_frac = input-gradient FLOPs vs fp32 peak",
+        # the atomic bytes the kernel really issues: PMC WRITE_SIZE (exact for float atomics) when the
+        # committed summary has it — the scatter walk merges runs of samples, so far fewer than the
+        # 1024 B per sample and grid before merging; else that algorithmic count
+        counted = pmc_write_bytes(name, traffic_path or TRAFFIC_FILE)
+        if counted:
+            counted = max(counted - pts * PLAIN_WRITE_PER_SAMPLE.get(name, 0.0), 0.0)
+        abytes = counted if counted else pts * ATOMIC_SPANS[name]
+        bound, achieved, peak, unit = "atomic", abytes / t / 1e9, ATOMIC_PEAK_GBS, "GB/s"
+        extra = {"atomic_bytes_per_sample_unmerged": ATOMIC_SPANS[name],
+                 "atomic_bytes_per_launch": abytes, "atomic_basis": "pmc WRITE_SIZE" if counted else "algorithmic",
+                 "atomic_note": "float-atomic adds into the grid gradient against ~1.3 TB/s of added bytes chip-wide "
+                                "(MI355X_MICROARCH.md atomics table); well under it, these mask-only kernels are "
+                                "latency-bound; mfma_frac = input-gradient FLOPs vs fp32 peak",
                  "mfma_frac": tflops / F32_PEAK_TFLOPS}
     tp = traffic_path or TRAFFIC_FILE
     return {"kernel": name, "bound": bound, "achieved": achieved, "peak": peak, "unit": unit,
