@@ -936,6 +936,38 @@ __device__ __forceinline__ void stage_walk_table(float* __restrict__ tab, const 
   }
 }
 
+// Step codes of the walk (NSLAM_WALK_CODES, default): every lane evaluates, in parallel before the
+// walk, what the step from point p-1's cell to point p's does — bit 8: the cell changes; bit 4 hh + j:
+// voxel (hh, j) of the previous cell is kept (a neighbouring-cell step).  The walk itself then
+// reads one code per point (v_readlane) instead of deriving the steps' axis deltas and parities on the
+// scalar unit point after point (~3k SALU instructions per tile, shared by the CU's waves).
+#ifndef NSLAM_WALK_CODES
+#define NSLAM_WALK_CODES 1
+#endif
+__device__ __forceinline__ int walk_code(int cellk, int lane) {
+  const int p = lane & 31;
+  const int prev = __shfl(cellk, (lane & 32) | ((p + 31) & 31), 64);  // point p - 1 (same half)
+  if (p == 0) return 0x100;        // the first point: nothing accumulated, nothing kept
+  if (prev == cellk) return 0;     // the same cell: no step
+  const int ax = (cellk & 1023) - (prev & 1023);
+  const int ay = ((cellk >> 10) & 1023) - ((prev >> 10) & 1023);
+  const int az = (cellk >> 20) - (prev >> 20);
+  const int px = prev & 1, py = (prev >> 10) & 1, pz = (prev >> 20) & 1;
+  int code = 0x100;
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    const bool kx = ax == 0 || (ax == 1 && (hh ^ px) == 1) || (ax == -1 && (hh ^ px) == 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int dy = (j & 1) ^ py, dz = (j >> 1) ^ pz;
+      const bool ky = ay == 0 || (ay == 1 && dy == 1) || (ay == -1 && dy == 0);
+      const bool kz = az == 0 || (az == 1 && dz == 1) || (az == -1 && dz == 0);
+      if (kx && ky && kz) code |= 1 << (4 * hh + j);
+    }
+  }
+  return code;
+}
+
 __device__ __forceinline__ void scatter_grid_grad_uniform(float* __restrict__ grad, const ScatterCorners& sc,
                                                           int cellk, const f32x16& dc, float* __restrict__ img,
                                                           float* __restrict__ tab, int lane) {
@@ -964,6 +996,31 @@ __device__ __forceinline__ void scatter_grid_grad_uniform(float* __restrict__ gr
     wsum[j] = 0.f;
     rows[j] = 0;
   }
+#if NSLAM_WALK_CODES
+  const int codes = walk_code(cellk, lane);
+#pragma unroll
+  for (int t = 0; t < 32; ++t) {
+    const int code = __builtin_amdgcn_readlane(codes, t);
+    const f32x4 w = wt[2 * t];
+    const i32x4 nr = rt[2 * t];
+    if (code & 0x100) {  // wave-uniform: the walk steps to another cell
+      const int kb = code >> (4 * h);  // this half's voxels of the previous cell that stay
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool keep = (kb >> j) & 1;
+        if (!keep && wsum[j] != 0.f) grid_add(grad + (size_t)rows[j] * NSLAM_C_DIM + ch, acc[j]);
+        acc[j] = keep ? acc[j] : 0.f;
+        wsum[j] = keep ? wsum[j] : 0.f;
+        rows[j] = nr[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc[j] += w[j] * vcol[t];
+      wsum[j] += w[j];
+    }
+  }
+#else
   int cur = -1;
 #pragma unroll
   for (int t = 0; t < 32; ++t) {
@@ -1002,6 +1059,7 @@ __device__ __forceinline__ void scatter_grid_grad_uniform(float* __restrict__ gr
       wsum[j] += w[j];
     }
   }
+#endif
 #pragma unroll
   for (int j = 0; j < 4; ++j)
     if (wsum[j] != 0.f) grid_add(grad + (size_t)rows[j] * NSLAM_C_DIM + ch, acc[j]);
