@@ -184,6 +184,11 @@ constexpr int kCotFloats = kCotXg + 32 * 8;
 // transpose.  The forward stores registers 4k..4k+3 of lane (p, h) — features 8k+4h..+3, i.e.
 // F(r, h) — as one 16-B store at [p][8k+4h].
 __device__ __forceinline__ void tape_store(float* __restrict__ t, int i, const f32x16& v, int lane) {
+#ifdef NSLAM_EXP_NOSTORE  // timing experiment only: the values are formed, not stored
+#pragma unroll
+  for (int r = 0; r < 16; ++r) asm volatile("" ::"v"(v[r]));
+  return;
+#endif
   const int p = lane & 31, h = lane >> 5;
   __attribute__((address_space(1))) f32x4* q =
       reinterpret_cast<__attribute__((address_space(1))) f32x4*>(as_global_w(t) + i * 1024 + p * 32 + 4 * h);
@@ -774,8 +779,13 @@ __device__ __forceinline__ void xyz_backward_saved(const float* __restrict__ pk,
           sn[e] = sv;
         }
         const int o = p * 32 + 8 * k + 4 * h;
+#ifdef NSLAM_EXP_NOSTORE
+        asm volatile("" ::"v"(gc[0]), "v"(gc[1]), "v"(gc[2]), "v"(gc[3]), "v"(sn[0]), "v"(sn[1]), "v"(sn[2]),
+                     "v"(sn[3]), "v"(o));
+#else
         *reinterpret_cast<__attribute__((address_space(1))) f32x4*>(ct + (kCotG + b) * 1024 + o) = gc;
         *reinterpret_cast<__attribute__((address_space(1))) f32x4*>(ct + (kCotS + b) * 1024 + o) = sn;
+#endif
       }
     }
   }
