@@ -314,7 +314,9 @@ class MappingEngine:
                                     and hasattr(on_branch, "color_wgrad") and self._tape is not None
                                     and self._saved is not None)
                         # the colour grid's Adam beside the weight gradients, in the frozen branch's Adam
-                        cside = tape_bwd and self.cgrid_side and any(len(u) > 1 for u in units) and concurrent
+                        # (the frozen unit must come after this one: it picks the colour grid's Adam up)
+                        cside = (tape_bwd and self.cgrid_side and any(len(u) > 1 for u in units) and concurrent
+                                 and not self.lean_first)
                         fused = tape_bwd and (self.fuse_adam or cside)
                         # (the split colour backward is timed as its two kernels: the lean chain and the
                         # weight-gradient reduction have different bounds)
