@@ -15,6 +15,9 @@
 // Everything lives in a named namespace: the per-decoder backward launchers are explicitly
 // instantiated in their own translation units (nslam_query_dec.hip, built once per decoder) so the
 // library compiles in parallel; the API translation unit (nslam_query.hip) only declares them.
+#ifndef NSLAM_LATE_TAPE
+#define NSLAM_LATE_TAPE 0  // measured within noise of the early stores (bench 212-213 vs 214-215 M/s; kernels -4 %)
+#endif
 namespace nslamq {
 
 struct QueryKArgs {
@@ -364,30 +367,37 @@ __device__ __forceinline__ f32x16 xyz_forward(const float* __restrict__ pk, cons
   }
   PHF_(5);
   m[0] = mask16(a);
+  // NSLAM_LATE_TAPE: a layer's tape store is issued after the next layer's GEMM (its fragment
+  // loads) — on gfx950 a store holds the wave's in-order vmcnt until it completes, so a fragment load
+  // issued after it waits for it (h stays live until the next layer reassigns it anyway)
   f32x16 h = relu16(a) + fc_branch<NC, VLDS>(pk, L, 0, cin, lane, vs);
   if (KEEP) hs[0] = h;
-  if (TAPE) tape_store(tape, 0, h, lane);
+  if (TAPE && !NSLAM_LATE_TAPE) tape_store(tape, 0, h, lane);
   a = vtile<VLDS>(vs + (L.Bias(1) - L.V()), lane);
   gemm_acc(a, pk + L.L1() * NSLAM_FRAG, h, lane);
+  if (TAPE && NSLAM_LATE_TAPE) tape_store(tape, 0, h, lane);
   m[1] = mask16(a);
   h = relu16(a) + fc_branch<NC, VLDS>(pk, L, 1, cin, lane, vs);
   if (KEEP) hs[1] = h;
-  if (TAPE) tape_store(tape, 1, h, lane);
+  if (TAPE && !NSLAM_LATE_TAPE) tape_store(tape, 1, h, lane);
   PHF_(6);
   a = vtile<VLDS>(vs + (L.Bias(2) - L.V()), lane);
   gemm_acc(a, pk + L.L2() * NSLAM_FRAG, h, lane);
+  if (TAPE && NSLAM_LATE_TAPE) tape_store(tape, 1, h, lane);
   m[2] = mask16(a);
   h = relu16(a) + fc_branch<NC, VLDS>(pk, L, 2, cin, lane, vs);
   if (KEEP) hs[2] = h;
-  if (TAPE) tape_store(tape, 2, h, lane);
+  if (TAPE && !NSLAM_LATE_TAPE) tape_store(tape, 2, h, lane);
   gemm_acc(a3, pk + (L.L3() + 3) * NSLAM_FRAG, h, lane);
+  if (TAPE && NSLAM_LATE_TAPE) tape_store(tape, 2, h, lane);
   m[3] = mask16(a3);
   h = relu16(a3) + fc_branch<NC, VLDS>(pk, L, 3, cin, lane, vs);
   if (KEEP) hs[3] = h;
-  if (TAPE) tape_store(tape, 3, h, lane);
+  if (TAPE && !NSLAM_LATE_TAPE) tape_store(tape, 3, h, lane);
   PHF_(7);
   a = vtile<VLDS>(vs + (L.Bias(4) - L.V()), lane);
   gemm_acc(a, pk + L.L4() * NSLAM_FRAG, h, lane);
+  if (TAPE && NSLAM_LATE_TAPE) tape_store(tape, 3, h, lane);
   m[4] = mask16(a);
   h = relu16(a) + fc_branch<NC, VLDS>(pk, L, 4, cin, lane, vs);
   if (TAPE) tape_store(tape, 4, h, lane);
@@ -729,29 +739,36 @@ __device__ __forceinline__ void xyz_backward_saved(const float* __restrict__ pk,
 #pragma unroll
     for (int r = 0; r < 16; ++r) dh[r] += w[r] * gall[GOFS + j];
   }
-  if (cot) tape_store(cot, 4, dh, lane);
+  // (NSLAM_LATE_TAPE: each cotangent tile is stored after the FCᵢᵀ GEMM that reads it, whose
+  // fragment loads then do not queue behind the store)
+  if (cot && !NSLAM_LATE_TAPE) tape_store(cot, 4, dh, lane);
   dc = zero16();
   gemm_acc(dc, pk + L.FCT(4) * NSLAM_FRAG, dh, lane);
+  if (cot && NSLAM_LATE_TAPE) tape_store(cot, 4, dh, lane);
   f32x16 da = apply_mask(dh, m[4]);
   dh = zero16();
   gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
-  if (cot) tape_store(cot, 3, dh, lane);
+  if (cot && !NSLAM_LATE_TAPE) tape_store(cot, 3, dh, lane);
   gemm_acc(dc, pk + L.FCT(3) * NSLAM_FRAG, dh, lane);
+  if (cot && NSLAM_LATE_TAPE) tape_store(cot, 3, dh, lane);
   const f32x16 da3 = apply_mask(dh, m[3]);
   dh = zero16();
   gemm_acc(dh, pk + (L.L3T() + 3) * NSLAM_FRAG, da3, lane);
-  if (cot) tape_store(cot, 2, dh, lane);
+  if (cot && !NSLAM_LATE_TAPE) tape_store(cot, 2, dh, lane);
   gemm_acc(dc, pk + L.FCT(2) * NSLAM_FRAG, dh, lane);
+  if (cot && NSLAM_LATE_TAPE) tape_store(cot, 2, dh, lane);
   da = apply_mask(dh, m[2]);
   dh = zero16();
   gemm_acc(dh, pk + L.L2T() * NSLAM_FRAG, da, lane);
-  if (cot) tape_store(cot, 1, dh, lane);
+  if (cot && !NSLAM_LATE_TAPE) tape_store(cot, 1, dh, lane);
   gemm_acc(dc, pk + L.FCT(1) * NSLAM_FRAG, dh, lane);
+  if (cot && NSLAM_LATE_TAPE) tape_store(cot, 1, dh, lane);
   da = apply_mask(dh, m[1]);
   dh = zero16();
   gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
-  if (cot) tape_store(cot, 0, dh, lane);
+  if (cot && !NSLAM_LATE_TAPE) tape_store(cot, 0, dh, lane);
   gemm_acc(dc, pk + L.FCT(0) * NSLAM_FRAG, dh, lane);
+  if (cot && NSLAM_LATE_TAPE) tape_store(cot, 0, dh, lane);
   gx[0] = gx[1] = gx[2] = 0.f;
   if (cot) {  // a colour weight-gradient backward's embedding operands: Gc_b and S_b
     const f32x16 da0 = apply_mask(dh, m[0]);
