@@ -29,9 +29,9 @@ sys.path.insert(0, REPO)
 # the next iteration's pixel gather + sampler run beside this iteration's render/backward
 # (engine.MappingEngine.iteration(prefetch=True)); --no-prefetch for the strictly serial step
 PREFETCH = True
-# cross-iteration pipelining of the colour stage (engine.MappingEngine.pipeline): the next iteration's
-# middle | fine forward overlaps this iteration's colour weight gradients (--pipeline to turn on)
-PIPELINE = False
+# iterations per captured hipGraph, whatever --steps is (a replay starts only after the previous one has
+# drained, ~20 us on MI355X: paid once per block), so runs of any length measure the same thing
+GRAPH_BLOCK = 10
 
 ROOM0 = {
     "bound": [[-2.9, 8.9], [-3.2, 5.5], [-3.5, 3.3]], "bound_divisible": 0.32,
@@ -64,43 +64,33 @@ HBM_PEAK_GBS = 8000.0
 # into its grid = 1024 B read + 1024 B written (float-atomic RMW).
 KERNEL_WORK = {
     "query_fwd": (FLOP_FWD_PER_SAMPLE, BYTES_FWD_PER_SAMPLE),
-    # the pipelined iteration's forward halves (ABI v13 nslam_query_fwd_parts): middle | fine
-    # (middle and fine MACs; middle lookup + fine's fine and middle lookups) and colour
-    "query_fwd.middle+fine": (2 * (15479 + 20599), 3 * 1024),
-    "query_fwd.color": (2 * 15575, 1024),
     "query_bwd.color": (2 * 2 * 15575, 2048),
-    # ABI v11 split: the colour decoder's lean chain (input gradients, grid scatter, cotangent tape)
-    # and its weight-gradient reduction (dW = Σ cotangent ⊗ input: one MAC per weight per sample)
-    "query_bwd.color_lean": (2 * 15575, 2048),
+    # ABI v16: the colour decoder's weight gradients (dW = Σ cotangent ⊗ input: one MAC per weight per
+    # sample; the recomputed cotangent chain, colour feature and Fourier terms are not counted)
     "query_bwd.color_wgrad": (2 * 15575, 0),
     "query_bwd.fine": (2 * 20599, 2048),
     "query_bwd.middle": (2 * 15479, 2048),
-    # the frozen decoders' mask-only backward as one launch (ABI v10 nslam_query_bwd_decoders)
+    # every decoder's mask-only backward (input gradients + grid scatter) as one launch (ABI v10
+    # nslam_query_bwd_decoders): the fine / middle stages and the colour stage
     "query_bwd.middle+fine": (2 * 15479 + 2 * 20599, 2 * 2048),
-    "query_bwd.color+middle+fine": (2 * 15479 + 2 * 20599 + 2 * 2 * 15575, 3 * 2048),
+    "query_bwd.middle+fine+color": (2 * 15479 + 2 * 20599 + 2 * 15575, 3 * 2048),
 }
 # The frozen decoders' mask-only backward launches are bound by their grid-gradient float atomics,
 # not by HBM or MFMA: 8 corners x 32 channels x 4 B = 1024 added bytes per ray-sample against the
 # chip-wide float-atomic rate of ~1.3 TB/s of added bytes (MI355X_MICROARCH.md, atomics table: every
 # CU issuing, any footprint or contention).  Their roofline is stated against that ceiling.
 ATOMIC_SPANS = {"query_bwd.fine": 1024, "query_bwd.middle": 1024, "query_bwd.middle+fine": 2048,
-                "query_bwd.color_lean": 1024}
+                "query_bwd.middle+fine+color": 3072}
 ATOMIC_PEAK_GBS = 1300.0
-# plain-store bytes per ray-sample inside an atomic span's WRITE_SIZE (subtracted to get its atomic
-# bytes): the colour lean chain's cotangent tape, 12 images x 4 KiB + 1 KiB of x / g per 32-point tile
-PLAIN_WRITE_PER_SAMPLE = {"query_bwd.color_lean": (12 * 4096 + 1024) / 32}
 # rocprofv3 kernel names behind each span (for the PMC traffic of profiles/*traffic*.json)
 SPAN_KERNELS = {
     "query_fwd": ("k_query_fwd", "k_occ_combine"),
-    "query_fwd.middle+fine": ("k_query_fwd_parts<3, 2, false, 1>",),
-    "query_fwd.color": ("k_query_fwd_parts<3, 1, true, 2>",),
     "query_bwd.color": ("k_dec_bwd<3,", "k_color_wgrad", "k_slab_reduce"),
-    "query_bwd.color_lean": ("k_dec_bwd<3,",),
     "query_bwd.color_wgrad": ("k_color_wgrad", "k_slab_reduce"),
     "query_bwd.fine": ("k_dec_bwd<2,",),
     "query_bwd.middle": ("k_dec_bwd<1,",),
-    "query_bwd.middle+fine": ("k_dec_bwd_multi<false, false>",),
-    "query_bwd.color+middle+fine": ("k_dec_bwd_multi<false, true>", "k_slab_reduce"),
+    "query_bwd.middle+fine": ("k_dec_bwd_multi<false>",),
+    "query_bwd.middle+fine+color": ("k_dec_bwd_multi<false>",),
 }
 TRAFFIC_FILE = os.path.join(REPO, "profiles", "r03_traffic.json")
 STRESS_TRAFFIC_FILE = os.path.join(REPO, "profiles", "r03_traffic_stress.json")
@@ -165,30 +155,24 @@ class StepGraphs:
     (one per ray-buffer parity of the prefetching engine) cover remainders.  run(k) executes exactly
     k iterations; finish() re-aligns the engine's host-side buffer parity (sync) with the device."""
 
-    def __init__(self, fn, block=10, sync=None, tail=None):
-        # tail(): joins streams an iteration may leave in flight (the pipelined engine's colour
-        # branch) into the capturing stream before a capture ends
-        tail = tail or (lambda: None)
+    def __init__(self, fn, block=GRAPH_BLOCK, sync=None):
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for _ in range(2):
                 fn()
-            tail()
         torch.cuda.current_stream().wait_stream(side)
         self.single = []
         for _ in range(2):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 fn()
-                tail()
             self.single.append(g)
         self.block = max(2, block - block % 2)
         self.blockg = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.blockg):
             for _ in range(self.block):
                 fn()
-            tail()
         self.par = 0  # device-side parity relative to the capture start
         self.sync = sync
 
@@ -209,9 +193,9 @@ class StepGraphs:
         self.par = 0
 
 
-def capture_step_graphs(fn, block=10, sync=None, tail=None):
+def capture_step_graphs(fn, block=GRAPH_BLOCK, sync=None):
     """(StepGraphs, "hipgraph") for fn = one mapping iteration."""
-    return StepGraphs(fn, block, sync, tail), "hipgraph"
+    return StepGraphs(fn, block, sync), "hipgraph"
 
 
 class Room0Scene:
@@ -294,7 +278,6 @@ class Room0Scene:
             # grid gradients accumulate only on the frustum-selected rows Adam optimises (compact)
             self.engine = P.engine.MappingEngine(self.nice, self.grids, self.bound, cfg["n_strat"], cfg["n_surf"],
                                                  w_color=cfg["w_color"], device=dev, rows=self.rows)
-            self.engine.pipeline = PIPELINE
             self.opt = P.ops.FusedAdam(
                 [{"params": [self.engine.decs["color"].param], "lr": cfg["lr"]["decoders"]}] +
                 ([{"params": [self.grids["grid_coarse"]], "lr": cfg["lr"]["middle"]}] if self.coarse else []) +
@@ -340,11 +323,6 @@ class Room0Scene:
             stage, self.frames, None, n, (H, W), (cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"]), self.opt,
             trainable_decoders=("color",), exchange=self.exchange if sharded else None, n_kept=self.kept,
             seed=1000, world=world, rank=self.rank if sharded else 0, prefetch=PREFETCH)
-
-    def join(self):
-        """Join a pipelined iteration's colour branch into the current stream."""
-        if self.path == "fused":
-            self.engine.join()
 
     def flip_parity(self):
         """The prefetching engine's host-side ray-buffer parity, after an odd number of replayed
@@ -501,7 +479,7 @@ def stress_iteration(dev, steps=10):
     if os.environ.get("NSLAM_BENCH_EAGER"):  # PMC passes (tools/gpu_traffic_stress.sh): per-dispatch counters
         g, mode = None, "eager"
     else:
-        g, mode = capture_step_graphs(scene.step, block=2, sync=scene.flip_parity, tail=scene.join)
+        g, mode = capture_step_graphs(scene.step, block=2, sync=scene.flip_parity)
         g.run(2)
     torch.cuda.synchronize()
     scene.kept.zero_()
@@ -686,8 +664,6 @@ def kernel_roofline(name, avg_ms, pts, traffic_path=None):
         # committed summary has it — the scatter walk merges runs of samples, so far fewer than the
         # 1024 B per sample and grid before merging; else that algorithmic count
         counted = pmc_write_bytes(name, traffic_path or TRAFFIC_FILE)
-        if counted:
-            counted = max(counted - pts * PLAIN_WRITE_PER_SAMPLE.get(name, 0.0), 0.0)
         abytes = counted if counted else pts * ATOMIC_SPANS[name]
         bound, achieved, peak, unit = "atomic", abytes / t / 1e9, ATOMIC_PEAK_GBS, "GB/s"
         extra = {"atomic_bytes_per_sample_unmerged": ATOMIC_SPANS[name],
@@ -713,8 +689,8 @@ def graph_time(scene, fn, reps):
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
-    try:  # 50-iteration graph blocks, as the headline leg
-        g, mode = capture_step_graphs(fn, block=50, sync=scene.flip_parity, tail=scene.join)
+    try:  # graph blocks of GRAPH_BLOCK iterations, as the headline leg
+        g, mode = capture_step_graphs(fn, sync=scene.flip_parity)
         run = g.run
     except Exception:  # pragma: no cover - eager fallback
         g, mode = None, "eager"
@@ -850,17 +826,13 @@ def main():
                     help="override mapping pixels per iteration (scaling studies; the metric uses room0's 1000)")
     ap.add_argument("--path", choices=("fused", "autograd"), default="fused",
                     help="fused engine (default) or the autograd drop-in path")
-    ap.add_argument("--pipeline", action="store_true",
-                    help="cross-iteration overlap of the colour branch with the next forward (experiment)")
-    ap.add_argument("--no-pipeline", action="store_true", help="(the default) no cross-iteration overlap")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="draw + sample each iteration's rays inside it (no overlap with the previous backward)")
     ap.add_argument("--leg", choices=("frames", "stress", "stress_iter", "bulk", "frame_io", "apartment"), default=None,
                     help="run one auxiliary measurement and print its JSON (bench.py spawns these itself)")
     args = ap.parse_args()
-    global PREFETCH, PIPELINE
+    global PREFETCH
     PREFETCH = not args.no_prefetch
-    PIPELINE = (args.pipeline or PIPELINE) and not args.no_pipeline
     if args.leg:
         return leg_main(args.leg)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -888,11 +860,9 @@ def main():
     if not args.eager and not (world > 1 and args.backend == "gloo"):
         try:  # whole mapping iterations as hipGraphs (removes per-op host launch cost); two of them,
             # replayed in turn, since the prefetching engine alternates its ray buffers
-            # blocks of up to 50 iterations per graph: a replay starts only after the previous one
-            # drained (~20 us), paid once per block (block 10 -> 50: ~1.6 us less per iteration)
-            block = 50 if args.steps >= 50 else 10
-            graph, mode = capture_step_graphs(lambda: scene.step(sharded=sharded), block=block,
-                                              sync=scene.flip_parity, tail=scene.join)
+            # blocks of GRAPH_BLOCK iterations per graph whatever --steps is (a replay starts only
+            # after the previous one drained, ~20 us, paid once per block)
+            graph, mode = capture_step_graphs(lambda: scene.step(sharded=sharded), sync=scene.flip_parity)
             graph.run(graph.block)
             torch.cuda.synchronize()
         except Exception as e:  # pragma: no cover - fall back to eager launches
@@ -956,7 +926,7 @@ def main():
             "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in timers.items()},
             "query_fwd_hbm_frac": (pts_per_step * BYTES_FWD_PER_SAMPLE / (qf["avg_ms"] * 1e-3) / 1e9) / HBM_PEAK_GBS
             if "query_fwd" in timers else None,
-            "pipeline": PIPELINE,
+            "graph_block": GRAPH_BLOCK,
             "query_bwd_ms": qb["avg_ms"],
         }
         if sharded and args.path == "fused":

@@ -146,13 +146,6 @@ size_t nslam_query_fwd_workspace_size(const nslam_query_cfg* cfg, int64_t n_pts)
 int nslam_query_bwd(const nslam_query_cfg* cfg, const double* pts, int64_t n_pts, const float* g_raw,
                     double* g_pts, void* ws, size_t ws_bytes, void* stream);
 size_t nslam_query_bwd_workspace_size(const nslam_query_cfg* cfg, int64_t n_pts);
-/* ABI v13: part of the colour stage's decoder-parallel forward, for callers that overlap the
- * parts with other work (cfg->defer_occ must be 1).  part_mask: 0b011 = the middle and fine
- * decoders (middle occupancy into ws, at least nslam_query_fwd_workspace_size bytes; fine occupancy
- * into raw[...,3]; their ReLU masks), 0b100 = the colour decoder (raw[...,0:3], its masks and the
- * activation tape), 0b111 = nslam_query_fwd_ws.  The two halves touch disjoint bytes. */
-int nslam_query_fwd_parts(const nslam_query_cfg* cfg, const double* pts, int64_t n_pts, float* raw, void* ws,
-                          size_t ws_bytes, int32_t part_mask, void* stream);
 /* One decoder's share of nslam_query_bwd (ABI v4): its grid gradient, its parameter gradients
  * and its d/dpts (written, or added when accumulate_pts).  Decoders whose gradients go to
  * different buffers may run concurrently on different streams (the mapping iteration does:
@@ -164,32 +157,26 @@ int nslam_query_bwd_decoder(const nslam_query_cfg* cfg, int32_t dec, int32_t acc
 size_t nslam_query_bwd_decoder_workspace_size(const nslam_query_cfg* cfg, int32_t dec, int64_t n_pts);
 size_t nslam_query_saved_size(int64_t n_pts);
 size_t nslam_query_tape_size(int64_t n_pts); /* ABI v9 */
-/* ABI v10: the backward of several decoders in ONE launch — the share of nslam_query_bwd_decoder of
- * every decoder d in dec_mask (bit d), their workgroups interleaved over the grid, so decoders
- * that would run as concurrent launches on separate streams need no cross-stream fork / join.
- * Requires cfg->saved_masks (the forward's ReLU masks).  Frozen decoders (dgrad[d].base == NULL):
- * mask-only backward; with cfg->need_pts_grad, g_pts[d] (a host array of 4 device pointers)
- * receives decoder d's d/dpts [M][3] float64 (written, not accumulated).  The colour decoder may
- * also carry weight gradients (dgrad[COLOR].base, cfg->act_tape, no need_pts_grad,
- * ws >= nslam_query_bwd_decoder_workspace_size(cfg, COLOR, M)); any other decoder with weight
- * gradients is NSLAM_EUNSUPPORTED.  dec_mask | NSLAM_BWD_SUM_PTS (frozen decoders, need_pts_grad):
- * g_pts[0] receives the SUM of the decoders' d/dpts, added in decoder order ((middle + fine) +
- * colour: the order of summing the per-decoder buffers).  Replaces the per-decoder loop of
+/* ABI v10 (v16 signature): the backward of several decoders in ONE launch — the grid gradient and
+ * d/dpts share of nslam_query_bwd_decoder of every decoder d in dec_mask (bit d), their workgroups
+ * interleaved over the grid, so decoders that would run as concurrent launches on separate streams
+ * need no cross-stream fork / join.  Requires cfg->saved_masks (the forward's ReLU masks): every
+ * decoder runs the mask-only backward.  No parameter gradients are formed here: a decoder in dec_mask
+ * with dgrad[d].base != NULL is NSLAM_EUNSUPPORTED (the colour decoder's come from nslam_color_wgrad).
+ * With cfg->need_pts_grad, g_pts[d] (a host array of 4 device pointers) receives decoder d's d/dpts
+ * [M][3] float64 (written, not accumulated).  Replaces the per-decoder loop of
  * Tracker.optimize_cam_in_batch's backward (Tracker.py:125) / Mapper.optimize_map's (Mapper.py:503). */
-#define NSLAM_BWD_SUM_PTS 0x100
-/* ABI v11: dec_mask | NSLAM_BWD_DEFER_WGRAD (the colour decoder with weight gradients in the call):
- * the call runs the colour decoder's lean chain only (its grid gradient, and its cotangent tape into
- * ws); nslam_color_wgrad, with the same cfg and ws, later forms its weight gradients — so a mapping
- * iteration can run the frozen decoders' backward beside that weight-gradient reduction. */
-#define NSLAM_BWD_DEFER_WGRAD 0x200
 int nslam_query_bwd_decoders(const nslam_query_cfg* cfg, int32_t dec_mask, const double* pts, int64_t n_pts,
-                             const float* g_raw, double* const* g_pts, void* ws, size_t ws_bytes, void* stream);
-/* ABI v11: the colour decoder's parameter gradients (into cfg->dgrad[COLOR], added) from the tapes a
- * nslam_query_bwd_decoders(... | NSLAM_BWD_DEFER_WGRAD) call left: the forward's activation tape and
- * ReLU masks (cfg->act_tape, cfg->saved_masks) and the cotangent tape in ws (unchanged since, at least
- * nslam_query_bwd_decoder_workspace_size(cfg, COLOR, n_pts) bytes).  Mapper.py:503 for
- * color_decoder.parameters(); split-K over the points, deterministic. */
-int nslam_color_wgrad(const nslam_query_cfg* cfg, int64_t n_pts, void* ws, size_t ws_bytes, void* stream);
+                             const float* g_raw, double* const* g_pts, void* stream);
+/* ABI v16: the colour decoder's parameter gradients of a colour-stage backward (added into
+ * cfg->dgrad[COLOR]; Mapper.py:503 for color_decoder.parameters(), decoder.py:177-203) from the
+ * forward's activation tape and ReLU masks (cfg->act_tape, cfg->saved_masks) and the cotangent
+ * g_raw[M][4] — the cotangent chain, the colour feature and the Fourier features are recomputed, so
+ * the call reads nothing the grid-gradient backward (nslam_query_bwd_decoders) writes and the two may
+ * run concurrently on different streams.  Split-K over the points, deterministic.
+ * ws >= nslam_query_bwd_decoder_workspace_size(cfg, NSLAM_DEC_COLOR, M) bytes. */
+int nslam_color_wgrad(const nslam_query_cfg* cfg, const double* pts, int64_t n_pts, const float* g_raw, void* ws,
+                      size_t ws_bytes, void* stream);
 
 /* ---- compositing: raw2outputs_nerf_color, src/common.py:204-245 (occupancy mode) ------------ */
 int nslam_composite_fwd(const float* raw, const double* z_vals, int64_t n_rays, int32_t n_samples,
@@ -318,16 +305,6 @@ typedef struct nslam_adam_seg {
  * may run concurrently (other streams, other processes) each pass their own. */
 int nslam_adam_step(const nslam_adam_seg* segs, int32_t n_segs, float beta1, float beta2, float eps,
                     int32_t zero_grad, uint32_t* ticket, void* stream);
-/* ABI v14 (v12 took one segment): nslam_color_wgrad followed by the Adam step (Mapper.py:504) of the
- * colour decoder and of up to 3 further segments inside the same slab-reduction launch: segs[0] is
- * the decoder's dense segment with segs[0].grad == cfg->dgrad[COLOR].base and segs[0].n == its count
- * (mirror allowed); segs[1..n_segs) are any segments nslam_adam_step takes (e.g. the colour grid's
- * frustum rows, whose gradient the lean chain completed).  The update, zero_grad and the ticket
- * (required) behave as nslam_adam_step's over those segments, bit for bit. */
-int nslam_color_wgrad_adam(const nslam_query_cfg* cfg, int64_t n_pts, void* ws, size_t ws_bytes,
-                           const nslam_adam_seg* segs, int32_t n_segs, float beta1, float beta2, float eps,
-                           int32_t zero_grad, uint32_t* ticket, void* stream);
-
 /* Sparse gradient exchange of a ray-sharded mapping iteration (ABI v5).  Only the frustum-
  * selected grid rows reach Adam (Mapper.py:314-333,394-401,504), so only they need summing across
  * ranks: nslam_rows_pack copies rows[i] (row_len floats each, row_len % 4 == 0, 16-byte aligned

@@ -14,9 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NSLAM_LIB") or os.path.join(_HERE, "libnslam.so")  # NSLAM_LIB: instrumented builds
 
 NSLAM_OK = 0
-ABI_VERSION = 15
-BWD_SUM_PTS = 0x100  # nslam.h NSLAM_BWD_SUM_PTS (nslam_query_bwd_decoders)
-BWD_DEFER_WGRAD = 0x200  # nslam.h NSLAM_BWD_DEFER_WGRAD (ABI v11; then nslam_color_wgrad)
+ABI_VERSION = 16
 STAGES = {"coarse": 0, "middle": 1, "fine": 2, "color": 3}
 DEC_COARSE, DEC_MIDDLE, DEC_FINE, DEC_COLOR = 0, 1, 2, 3
 
@@ -116,8 +114,7 @@ EXPORTS = (
     "nslam_workspace_size", "nslam_strerror", "nslam_abi_version", "nslam_gather_rays", "nslam_render_loss",
     "nslam_render_loss_workspace_size", "nslam_adam_step", "nslam_rows_pack", "nslam_rows_unpack",
     "nslam_query_fwd_ws", "nslam_query_fwd_workspace_size", "nslam_cam_grad", "nslam_cam_pose",
-    "nslam_query_tape_size", "nslam_color_wgrad", "nslam_color_wgrad_adam",
-    "nslam_query_fwd_parts", "nslam_cam_grad_parts",
+    "nslam_query_tape_size", "nslam_color_wgrad", "nslam_cam_grad_parts",
 )
 
 _lib = None
@@ -143,18 +140,14 @@ def lib():
         L.nslam_sample_rays.argtypes = [vp, vp, vp, vp, i64, dp, dp, vp, i32, vp, i32, i32, vp, vp, sz, vp]
         L.nslam_query_fwd.argtypes = [ctypes.POINTER(NslamQueryCfg), vp, i64, vp, vp]
         L.nslam_query_fwd_ws.argtypes = [ctypes.POINTER(NslamQueryCfg), vp, i64, vp, vp, sz, vp]
-        L.nslam_query_fwd_parts.argtypes = [ctypes.POINTER(NslamQueryCfg), vp, i64, vp, vp, sz, i32, vp]
         L.nslam_query_fwd_workspace_size.argtypes = [ctypes.POINTER(NslamQueryCfg), i64]
         L.nslam_query_fwd_workspace_size.restype = sz
         L.nslam_query_bwd.argtypes = [ctypes.POINTER(NslamQueryCfg), vp, i64, vp, vp, vp, sz, vp]
         L.nslam_query_bwd_workspace_size.argtypes = [ctypes.POINTER(NslamQueryCfg), i64]
         L.nslam_query_bwd_workspace_size.restype = sz
         L.nslam_query_bwd_decoder.argtypes = [ctypes.POINTER(NslamQueryCfg), i32, i32, vp, i64, vp, vp, vp, sz, vp]
-        L.nslam_query_bwd_decoders.argtypes = [ctypes.POINTER(NslamQueryCfg), i32, vp, i64, vp, ctypes.POINTER(vp), vp,
-                                               sz, vp]
-        L.nslam_color_wgrad.argtypes = [ctypes.POINTER(NslamQueryCfg), i64, vp, sz, vp]
-        L.nslam_color_wgrad_adam.argtypes = [ctypes.POINTER(NslamQueryCfg), i64, vp, sz, ctypes.POINTER(NslamAdamSeg),
-                                             i32, ctypes.c_float, ctypes.c_float, ctypes.c_float, i32, vp, vp]
+        L.nslam_query_bwd_decoders.argtypes = [ctypes.POINTER(NslamQueryCfg), i32, vp, i64, vp, ctypes.POINTER(vp), vp]
+        L.nslam_color_wgrad.argtypes = [ctypes.POINTER(NslamQueryCfg), vp, i64, vp, vp, sz, vp]
         L.nslam_query_bwd_decoder_workspace_size.argtypes = [ctypes.POINTER(NslamQueryCfg), i32, i64]
         L.nslam_query_bwd_decoder_workspace_size.restype = sz
         L.nslam_query_saved_size.argtypes = [i64]

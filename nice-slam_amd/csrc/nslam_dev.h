@@ -102,10 +102,6 @@ __device__ __forceinline__ f32x16 zero16() {
   return z;
 }
 
-#ifdef NSLAM_EXP_HOTFRAG  // timing experiment only: every fragment read hits one 4 KiB block
-__device__ float g_hot_frag[1024];
-#endif
-
 // Global-address-space view of a pointer into device memory.  A pointer read out of the kernel
 // argument struct by a runtime index, or laundered through an asm constraint, is generic to the
 // compiler, and a generic access is a flat_* instruction — which counts in LGKM_CNT as well as
@@ -126,9 +122,6 @@ __device__ __forceinline__ __attribute__((address_space(1))) T* as_global_w(T* p
 // acc += Wblock * X   (frag: packed [lane][16], global memory)
 __device__ __forceinline__ void gemm_acc(f32x16& acc, const float* __restrict__ frag, const f32x16& x,
                                          int lane) {
-#ifdef NSLAM_EXP_HOTFRAG
-  frag = g_hot_frag;
-#endif
   const gptr_t<f32x4> f = as_global(reinterpret_cast<const f32x4*>(frag)) + lane * 4;
   const f32x4 a0 = f[0], a1 = f[1], a2 = f[2], a3 = f[3];
   acc = mfma32(a0[0], x[0], acc);

@@ -82,39 +82,6 @@ extern "C" int nslam_query_fwd_ws(const nslam_query_cfg* cfg, const double* pts,
 }
 
 
-// ABI v13: a subset of the colour stage's decoder-parallel forward (part_mask: bit 0 middle, bit 1
-// fine, bit 2 colour; the masks 0b011 and 0b100, or all three = nslam_query_fwd_ws with deferred
-// occupancy).  The middle part writes the occupancy workspace (ws), fine raw[...,3], colour
-// raw[...,0:3] (+ its activation tape): launches of disjoint masks write disjoint bytes.
-extern "C" int nslam_query_fwd_parts(const nslam_query_cfg* cfg, const double* pts, int64_t n_pts, float* raw,
-                                     void* ws, size_t ws_bytes, int32_t part_mask, void* stream) {
-  const int rc = check_cfg(cfg, false);
-  if (rc) return rc;
-  if (cfg->stage != NSLAM_STAGE_COLOR || !cfg->defer_occ) return NSLAM_EUNSUPPORTED;
-  if (part_mask != 3 && part_mask != 4 && part_mask != 7) return NSLAM_EINVAL;
-  if (n_pts < 0 || ((!pts && !cfg->rays_o) || !raw || (((uintptr_t)raw) & 15))) return NSLAM_EINVAL;
-  if (cfg->rays_o && (n_pts >= (int64_t(1) << 31) || n_pts % cfg->n_samples)) return NSLAM_EINVAL;
-  if (part_mask & 1) {
-    if (!ws || ws_bytes < nslam_query_fwd_workspace_size(cfg, n_pts)) return NSLAM_EWORKSPACE;
-  }
-  if (part_mask == 7) return nslam_query_fwd_ws(cfg, pts, n_pts, raw, ws, ws_bytes, stream);
-  if (n_pts == 0) return NSLAM_OK;
-  QueryKArgs a{*cfg, pts, n_pts, raw, nullptr, nullptr};
-  const int64_t groups = ((n_pts + 31) / 32 + 3) / 4;
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  float* occ = reinterpret_cast<float*>(ws);
-  if (part_mask == 3)
-    hipLaunchKernelGGL((k_query_fwd_parts<NSLAM_STAGE_COLOR, 2, false, 1>), dim3((unsigned)(groups * 2)), dim3(256), 0,
-                       s, a, occ);
-  else if (cfg->act_tape)
-    hipLaunchKernelGGL((k_query_fwd_parts<NSLAM_STAGE_COLOR, 1, true, 2>), dim3((unsigned)groups), dim3(256), 0, s, a,
-                       occ);
-  else
-    hipLaunchKernelGGL((k_query_fwd_parts<NSLAM_STAGE_COLOR, 1, false, 2>), dim3((unsigned)groups), dim3(256), 0, s,
-                       a, occ);
-  return hip_status();
-}
-
 extern "C" int nslam_query_bwd_decoder(const nslam_query_cfg* cfg, int32_t dec, int32_t accumulate_pts,
                                        const double* pts, int64_t n_pts, const float* g_raw, double* g_pts, void* ws,
                                        size_t ws_bytes, void* stream) {

@@ -15,9 +15,6 @@
 // Everything lives in a named namespace: the per-decoder backward launchers are explicitly
 // instantiated in their own translation units (nslam_query_dec.hip, built once per decoder) so the
 // library compiles in parallel; the API translation unit (nslam_query.hip) only declares them.
-#ifndef NSLAM_LATE_TAPE
-#define NSLAM_LATE_TAPE 0  // measured within noise of the early stores (bench 212-213 vs 214-215 M/s; kernels -4 %)
-#endif
 namespace nslamq {
 
 struct QueryKArgs {
@@ -27,12 +24,6 @@ struct QueryKArgs {
   float* raw;          // fwd output [n][4]
   const float* g_raw;  // bwd input  [n][4]
   double* g_pts;       // bwd output [n][3]
-  // colour-decoder cotangent tape (workspace of a colour weight-gradient backward, NULL = none):
-  // the lean backward stores dh_0..dh_4 of every tile here for k_color_wgrad
-  float* cot = nullptr;
-  // ABI v11 NSLAM_BWD_DEFER_WGRAD: the colour tape backward stops after its lean chain (the
-  // cotangent tape in ws); nslam_color_wgrad forms the weight gradients later
-  bool defer_wgrad = false;
 };
 
 // ------------------------------------------------------------------------------------------
@@ -161,24 +152,6 @@ __device__ __forceinline__ void load_masks(const QueryKArgs& a, int dec, int64_t
 // post-ReLU hidden tiles h0..h4 of every tile (C layout) and the weight-gradient backward reads them
 // instead of recomputing the decoder (it needs them as the inputs of dW; Mapper.py:503).
 constexpr int kTapeFloats = 5 * 16 * 64;  // per tile: h0..h4
-// Cotangent tape of the colour decoder's weight-gradient backward, written by the lean chain, in the
-// activation tape's point-major layout ([32 points][32 features] per slot):
-//   slots 0-4  dh_0..dh_4, the cotangents of the five hidden layers before their ReLU masks
-//   slots 5-7  Gc_b = (L3_b^T da_3 + L0_b^T da_0) ⊙ cos(x B_b): the embedding cotangent times the
-//              sin derivative (dims 32b..32b+31, b = 0..2), the operand of dB
-//   slots 8-10 S_b = sin(x B_b), the embedding itself (the input of dW_0 and of dW_3's first 93
-//              columns): sin and cos by one range reduction, bit-identical to the forward's
-//   slot 11    the colour feature c (the fc_c weight gradients' input)
-// then a [32 points][8] block of x (float, 3 + pad) and the colour cotangent g (3 + pad): every
-// tile is 49 KiB of whole 1-KiB pieces (k_color_wgrad stages them by LDS-DMA).
-#ifndef NSLAM_CGATHER_NB
-#define NSLAM_CGATHER_NB 4  // corners in flight of the lean chain's colour-feature gather
-#endif
-constexpr int kCotG = 5;
-constexpr int kCotS = 8;
-constexpr int kCotC = 11;
-constexpr int kCotXg = 12 * 16 * 64;
-constexpr int kCotFloats = kCotXg + 32 * 8;
 // Layout [tile][layer][register r][64 lanes] float: every store / load instruction moves 256 B
 // contiguous, and no 4-register grouping of the tile is needed (a float4 layout cost the forward
 // ~30 VGPRs of copies).
@@ -187,54 +160,12 @@ constexpr int kCotFloats = kCotXg + 32 * 8;
 // transpose.  The forward stores registers 4k..4k+3 of lane (p, h) — features 8k+4h..+3, i.e.
 // F(r, h) — as one 16-B store at [p][8k+4h].
 __device__ __forceinline__ void tape_store(float* __restrict__ t, int i, const f32x16& v, int lane) {
-#ifdef NSLAM_EXP_NOSTORE  // timing experiment only: the values are formed, not stored
-#pragma unroll
-  for (int r = 0; r < 16; ++r) asm volatile("" ::"v"(v[r]));
-  return;
-#endif
   const int p = lane & 31, h = lane >> 5;
   __attribute__((address_space(1))) f32x4* q =
       reinterpret_cast<__attribute__((address_space(1))) f32x4*>(as_global_w(t) + i * 1024 + p * 32 + 4 * h);
 #pragma unroll
   for (int k = 0; k < 4; ++k) q[2 * k] = f32x4{v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]};
 }
-// tape_store with one 4-B store per register: no 4-register tuples (storing the colour feature
-// with 16-B stores right after the forward chain cost that kernel 52 VGPRs and half its occupancy)
-__device__ __forceinline__ void tape_store_dw(float* __restrict__ t, int i, const f32x16& v, int lane) {
-  const int p = lane & 31, h = lane >> 5;
-  __attribute__((address_space(1))) float* q = as_global_w(t) + i * 1024 + p * 32 + 4 * h;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) q[(r & 3) + 8 * (r >> 2)] = v[r];
-}
-// Layer i of the tape as an MFMA B-operand stream over the points: element s of lane (j, h) is
-// h_i[point 2s+h][feature j] (each load instruction reads two 128-B point rows).
-__device__ __forceinline__ f32x16 tape_bop(const float* __restrict__ t, int i, int lane) {
-  // laundered base: keeps the scheduler from hoisting all five tile loads (80 VGPRs) to the top
-  asm volatile("" : "+s"(t));
-  const gptr_t<float> p = as_global(t) + i * 1024 + (lane >> 5) * 32 + (lane & 31);
-  f32x16 v;
-#pragma unroll
-  for (int s = 0; s < 16; ++s) v[s] = p[s * 64];
-  return v;
-}
-
-// Layer i of a point-major tape back in the C layout (inverse of tape_store): lane (p, h) gets
-// features F(r, h) of point p.
-__device__ __forceinline__ f32x16 tape_cload(const float* __restrict__ t, int i, int lane) {
-  const int p = lane & 31, h = lane >> 5;
-  const gptr_t<f32x4> q = as_global(reinterpret_cast<const f32x4*>(t + i * 1024 + p * 32 + 4 * h));
-  f32x16 v;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const f32x4 w = q[2 * k];
-    v[4 * k] = w[0];
-    v[4 * k + 1] = w[1];
-    v[4 * k + 2] = w[2];
-    v[4 * k + 3] = w[3];
-  }
-  return v;
-}
-
 // Parameter-gradient slab of one wave, addressed as a raw buffer: every update is a buffer store
 // (or load + store) with the lane-dependent part of the offset in a VGPR and the uniform part
 // (parameter block, row) in soffset, so the ~350 updates per tile cost one address VGPR per block.
@@ -251,9 +182,6 @@ __device__ __forceinline__ Slab make_slab(float* base, int floats) {
 
 template <int WG>
 __device__ __forceinline__ void put(const Slab& A, int lane_off, int uni_off, float v) {
-#ifdef NSLAM_EXP_NOSLAB  // timing experiment only: no slab stores
-  if (lane_off >= 0) { asm volatile("" ::"v"(v)); return; }
-#endif
   // the b32 intrinsics move raw bits (unsigned): bit-cast, never convert
   if (WG == 2) v += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(A.r, lane_off * 4, uni_off * 4, 0));
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), A.r, lane_off * 4, uni_off * 4, 0);
@@ -367,37 +295,30 @@ __device__ __forceinline__ f32x16 xyz_forward(const float* __restrict__ pk, cons
   }
   PHF_(5);
   m[0] = mask16(a);
-  // NSLAM_LATE_TAPE: a layer's tape store is issued after the next layer's GEMM (its fragment
-  // loads) — on gfx950 a store holds the wave's in-order vmcnt until it completes, so a fragment load
-  // issued after it waits for it (h stays live until the next layer reassigns it anyway)
   f32x16 h = relu16(a) + fc_branch<NC, VLDS>(pk, L, 0, cin, lane, vs);
   if (KEEP) hs[0] = h;
-  if (TAPE && !NSLAM_LATE_TAPE) tape_store(tape, 0, h, lane);
+  if (TAPE) tape_store(tape, 0, h, lane);
   a = vtile<VLDS>(vs + (L.Bias(1) - L.V()), lane);
   gemm_acc(a, pk + L.L1() * NSLAM_FRAG, h, lane);
-  if (TAPE && NSLAM_LATE_TAPE) tape_store(tape, 0, h, lane);
   m[1] = mask16(a);
   h = relu16(a) + fc_branch<NC, VLDS>(pk, L, 1, cin, lane, vs);
   if (KEEP) hs[1] = h;
-  if (TAPE && !NSLAM_LATE_TAPE) tape_store(tape, 1, h, lane);
+  if (TAPE) tape_store(tape, 1, h, lane);
   PHF_(6);
   a = vtile<VLDS>(vs + (L.Bias(2) - L.V()), lane);
   gemm_acc(a, pk + L.L2() * NSLAM_FRAG, h, lane);
-  if (TAPE && NSLAM_LATE_TAPE) tape_store(tape, 1, h, lane);
   m[2] = mask16(a);
   h = relu16(a) + fc_branch<NC, VLDS>(pk, L, 2, cin, lane, vs);
   if (KEEP) hs[2] = h;
-  if (TAPE && !NSLAM_LATE_TAPE) tape_store(tape, 2, h, lane);
+  if (TAPE) tape_store(tape, 2, h, lane);
   gemm_acc(a3, pk + (L.L3() + 3) * NSLAM_FRAG, h, lane);
-  if (TAPE && NSLAM_LATE_TAPE) tape_store(tape, 2, h, lane);
   m[3] = mask16(a3);
   h = relu16(a3) + fc_branch<NC, VLDS>(pk, L, 3, cin, lane, vs);
   if (KEEP) hs[3] = h;
-  if (TAPE && !NSLAM_LATE_TAPE) tape_store(tape, 3, h, lane);
+  if (TAPE) tape_store(tape, 3, h, lane);
   PHF_(7);
   a = vtile<VLDS>(vs + (L.Bias(4) - L.V()), lane);
   gemm_acc(a, pk + L.L4() * NSLAM_FRAG, h, lane);
-  if (TAPE && NSLAM_LATE_TAPE) tape_store(tape, 3, h, lane);
   m[4] = mask16(a);
   h = relu16(a) + fc_branch<NC, VLDS>(pk, L, 4, cin, lane, vs);
   if (TAPE) tape_store(tape, 4, h, lane);
@@ -724,12 +645,10 @@ __device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, con
 // dh_{i-1} = L_iT mask_i(dh_i) (layer 3 through its hidden block); EMBG adds d/dx through the
 // Fourier features from mask_3(dh_3) and mask_0(dh_0).
 // ------------------------------------------------------------------------------------------
-// cot (colour weight-gradient backward, else NULL): the tile's cotangent tape — dh_4..dh_0 are
-// stored there as they are formed, for k_color_wgrad.
 template <int NC, int NOUT, int GOFS, bool EMBG>
 __device__ __forceinline__ void xyz_backward_saved(const float* __restrict__ pk, const uint32_t m[5],
                                                    const float x[3], const float (&gall)[4], int lane, f32x16& dc,
-                                                   float gx[3], float* __restrict__ cot = nullptr) {
+                                                   float gx[3]) {
   const XyzPack L{NC};
   const int h = lane >> 5;
   f32x16 dh = zero16();
@@ -739,73 +658,25 @@ __device__ __forceinline__ void xyz_backward_saved(const float* __restrict__ pk,
 #pragma unroll
     for (int r = 0; r < 16; ++r) dh[r] += w[r] * gall[GOFS + j];
   }
-  // (NSLAM_LATE_TAPE: each cotangent tile is stored after the FCᵢᵀ GEMM that reads it, whose
-  // fragment loads then do not queue behind the store)
-  if (cot && !NSLAM_LATE_TAPE) tape_store(cot, 4, dh, lane);
   dc = zero16();
   gemm_acc(dc, pk + L.FCT(4) * NSLAM_FRAG, dh, lane);
-  if (cot && NSLAM_LATE_TAPE) tape_store(cot, 4, dh, lane);
   f32x16 da = apply_mask(dh, m[4]);
   dh = zero16();
   gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
-  if (cot && !NSLAM_LATE_TAPE) tape_store(cot, 3, dh, lane);
   gemm_acc(dc, pk + L.FCT(3) * NSLAM_FRAG, dh, lane);
-  if (cot && NSLAM_LATE_TAPE) tape_store(cot, 3, dh, lane);
   const f32x16 da3 = apply_mask(dh, m[3]);
   dh = zero16();
   gemm_acc(dh, pk + (L.L3T() + 3) * NSLAM_FRAG, da3, lane);
-  if (cot && !NSLAM_LATE_TAPE) tape_store(cot, 2, dh, lane);
   gemm_acc(dc, pk + L.FCT(2) * NSLAM_FRAG, dh, lane);
-  if (cot && NSLAM_LATE_TAPE) tape_store(cot, 2, dh, lane);
   da = apply_mask(dh, m[2]);
   dh = zero16();
   gemm_acc(dh, pk + L.L2T() * NSLAM_FRAG, da, lane);
-  if (cot && !NSLAM_LATE_TAPE) tape_store(cot, 1, dh, lane);
   gemm_acc(dc, pk + L.FCT(1) * NSLAM_FRAG, dh, lane);
-  if (cot && NSLAM_LATE_TAPE) tape_store(cot, 1, dh, lane);
   da = apply_mask(dh, m[1]);
   dh = zero16();
   gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
-  if (cot && !NSLAM_LATE_TAPE) tape_store(cot, 0, dh, lane);
   gemm_acc(dc, pk + L.FCT(0) * NSLAM_FRAG, dh, lane);
-  if (cot && NSLAM_LATE_TAPE) tape_store(cot, 0, dh, lane);
   gx[0] = gx[1] = gx[2] = 0.f;
-  if (cot) {  // a colour weight-gradient backward's embedding operands: Gc_b and S_b
-    const f32x16 da0 = apply_mask(dh, m[0]);
-    const float* FB = pk + L.FB();
-    const int p = lane & 31;
-    __attribute__((address_space(1))) float* ct = as_global_w(cot);
-#pragma unroll
-    for (int b = 0; b < 3; ++b) {
-      f32x16 de = zero16();
-      gemm_acc(de, pk + (L.L3T() + b) * NSLAM_FRAG, da3, lane);
-      gemm_acc(de, pk + (L.L0T() + b) * NSLAM_FRAG, da0, lane);
-      // registers 4k..4k+3 of lane (p, h) are dims 32b + 8k + 4h + 0..3 of point p (tape_store's layout)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int kd = 32 * b + 8 * k + 4 * h;
-        const f32x4 B0 = *as_global(reinterpret_cast<const f32x4*>(FB + kd));
-        const f32x4 B1 = *as_global(reinterpret_cast<const f32x4*>(FB + 96 + kd));
-        const f32x4 B2 = *as_global(reinterpret_cast<const f32x4*>(FB + 192 + kd));
-        f32x4 gc, sn;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float sv, cv;
-          fsincos(fourier_arg(x, B0[e], B1[e], B2[e]), sv, cv);  // decoder.py:29-30
-          gc[e] = de[4 * k + e] * cv;
-          sn[e] = sv;
-        }
-        const int o = p * 32 + 8 * k + 4 * h;
-#ifdef NSLAM_EXP_NOSTORE
-        asm volatile("" ::"v"(gc[0]), "v"(gc[1]), "v"(gc[2]), "v"(gc[3]), "v"(sn[0]), "v"(sn[1]), "v"(sn[2]),
-                     "v"(sn[3]), "v"(o));
-#else
-        *reinterpret_cast<__attribute__((address_space(1))) f32x4*>(ct + (kCotG + b) * 1024 + o) = gc;
-        *reinterpret_cast<__attribute__((address_space(1))) f32x4*>(ct + (kCotS + b) * 1024 + o) = sn;
-#endif
-      }
-    }
-  }
   if (EMBG) {
     da = apply_mask(dh, m[0]);
     const float* FB = pk + L.FB();
@@ -893,19 +764,8 @@ __device__ __forceinline__ void stage_corners(const Corners& cr, const int32_t* 
 }
 
 
-// grid-gradient add of one lane's channel (timing experiments swap the atomic for a plain store
-// or nothing; the product build is the float atomic)
-__device__ __forceinline__ void grid_add(float* p, float v) {
-#if defined(NSLAM_EXP_NOATOMIC)
-  asm volatile("" ::"v"(v), "v"(p));
-#elif defined(NSLAM_EXP_HALFATOMIC)  // every other grid row only: sensitivity to the atomic count
-  if (((reinterpret_cast<uintptr_t>(p) >> 7) & 1) == 0) unsafeAtomicAdd(p, v);
-#elif defined(NSLAM_EXP_STOREATOMIC)
-  __builtin_nontemporal_store(v, p);
-#else
-  unsafeAtomicAdd(p, v);
-#endif
-}
+// grid-gradient add of one lane's channel
+__device__ __forceinline__ void grid_add(float* p, float v) { unsafeAtomicAdd(p, v); }
 
 __device__ __forceinline__ float rdlane(float v, int l) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
@@ -1320,15 +1180,9 @@ __device__ __forceinline__ void fwd_part_color(const QueryKArgs& a, const Pt& q,
 #define NSLAM_FWD_LB 2  // min waves per SIMD (experiments: 3..5 trade VGPRs for occupancy)
 #endif
 constexpr int kVecFloats = 744;  // XyzPack vector section (740) rounded to float4s
-// PSET (ABI v13 nslam_query_fwd_parts, colour stage): 0 = the whole forward as above; 1 = only the
-// middle | fine parts (NPARTS 2: part 0 middle, part 1 fine writing raw[p][3]); 2 = only the colour
-// part (NPARTS 1) — so a pipelined mapping loop can start the next iteration's middle and fine
-// decoders (which read neither the colour grid nor the colour decoder) while this iteration's colour
-// weight gradients and colour Adam step are still running.
-template <int STAGE, int NPARTS, bool TAPE, int PSET = 0>
+template <int STAGE, int NPARTS, bool TAPE>
 __global__ __launch_bounds__(256, NSLAM_FWD_LB) void k_query_fwd_parts(QueryKArgs a, float* __restrict__ occ_mid) {
-  static_assert(PSET == 0 || (STAGE == NSLAM_STAGE_COLOR && NPARTS == (PSET == 1 ? 2 : 1)), "part set");
-  const int part = PSET == 2 ? 2 : (int)(blockIdx.x % NPARTS);
+  const int part = (int)(blockIdx.x % NPARTS);
   const int lane = threadIdx.x & 63;
   // The part's decoder vector sections (biases, output rows, Fourier B: ~3 KiB each) are read by
   // every layer of every wave: an LDS copy per workgroup turns ~90 global loads per wave into
@@ -1338,7 +1192,7 @@ __global__ __launch_bounds__(256, NSLAM_FWD_LB) void k_query_fwd_parts(QueryKArg
     const int d0 = part == 0 ? NSLAM_DEC_MIDDLE : part == 1 ? NSLAM_DEC_FINE : NSLAM_DEC_COLOR;
     const int nc0 = d0 == NSLAM_DEC_FINE ? 2 : 1;
     const float* src0 = a.c.packed[d0] + XyzPack{nc0}.V();
-    const bool two = PSET == 0 && NPARTS == 2 && STAGE == NSLAM_STAGE_COLOR && part == 0;
+    const bool two = NPARTS == 2 && STAGE == NSLAM_STAGE_COLOR && part == 0;
     const float* src1 = two ? a.c.packed[NSLAM_DEC_COLOR] + XyzPack{1}.V() : nullptr;
     for (int i = threadIdx.x; i < 740; i += 256) {
       vsec[0][i] = src0[i];
@@ -1352,7 +1206,7 @@ __global__ __launch_bounds__(256, NSLAM_FWD_LB) void k_query_fwd_parts(QueryKArg
   PHASE(0, 0);
   const Pt q = load_point(a, idx);
   PHASE(0, 1);
-  if (PSET == 0 && NPARTS == 2 && STAGE == NSLAM_STAGE_COLOR) {
+  if (NPARTS == 2 && STAGE == NSLAM_STAGE_COLOR) {
     if (part == 0) {
       fwd_part_middle(a, q, tile, idx, lane, occ_mid, vsec[0]);
       fwd_part_color<TAPE>(a, q, tile, idx, lane, vsec[1]);
@@ -1387,13 +1241,10 @@ constexpr int kScratchFloats = 2 * TILE_FLOATS + 32 * 4 + 32 * 3 + 32 * 8 * 2 + 
 constexpr int kWavesBwd = 4;
 constexpr int kMaxSlabs = 4096;  // WG == 2 above this many tiles
 
-// COT: the colour tile may store the cotangent tape (a.cot) of a colour weight-gradient backward (a
-// compile-time switch: the tape path's registers would otherwise be every caller's)
-template <int DEC, int WG, bool PG, bool FIRST, bool SAVED, bool COT = true>
+template <int DEC, int WG, bool PG, bool FIRST, bool SAVED>
 __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, const Slab& A, const Scratch& S,
                                              int lane, double* __restrict__ gpts, int64_t gbase = 0) {
   // gpts: d/dpts of point idx at gpts[(idx - gbase) * 3 + k] (gbase: a tile's LDS staging rows)
-  float* const cot = COT ? a.cot : nullptr;
   // Every scratch / slab address is a function of the lane only, i.e. invariant across the tile
   // loop; letting LICM hoist the ~300 of them pins (and spills) the register file.  Re-derive
   // them per tile.
@@ -1435,21 +1286,14 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
   float gx[3] = {0.f, 0.f, 0.f};
   static_assert(!(SAVED && WG), "weight gradients from saved masks run as k_color_wgrad");
   if (SAVED) {  // masks from the forward: no recompute (the mask-only chain)
-    if (DEC == NSLAM_DEC_COLOR && cot)  // the colour feature: the fc_c weight gradients' input
-      tape_store(cot + tile * kCotFloats, kCotC, gather_tile_batched<NSLAM_CGATHER_NB>(gr.data, cr, lane), lane);
     uint32_t m[5];
     load_masks(a, DEC, tile, m, lane);
     if (DEC == NSLAM_DEC_COARSE) {
       noxyz_backward_saved(pk, m, g[3], lane, dc);
     } else if (DEC == NSLAM_DEC_FINE) {
       xyz_backward_saved<2, 1, 3, PG>(pk, m, q.x, g, lane, dc, gx);
-    } else if (DEC == NSLAM_DEC_COLOR) {  // + the cotangent tape of a colour weight-gradient backward
-      xyz_backward_saved<1, 3, 0, PG>(pk, m, q.x, g, lane, dc, gx, cot ? cot + tile * kCotFloats : nullptr);
-      if (cot) {  // x (half 0) and g (half 1) of point p (g is 0 past the end)
-        const f32x4 v = h == 0 ? f32x4{q.x[0], q.x[1], q.x[2], 0.f} : f32x4{g[0], g[1], g[2], 0.f};
-        *reinterpret_cast<__attribute__((address_space(1))) f32x4*>(as_global_w(cot) + tile * kCotFloats + kCotXg +
-                                                                    p * 8 + 4 * h) = v;
-      }
+    } else if (DEC == NSLAM_DEC_COLOR) {
+      xyz_backward_saved<1, 3, 0, PG>(pk, m, q.x, g, lane, dc, gx);
     } else {
       xyz_backward_saved<1, 1, 3, PG>(pk, m, q.x, g, lane, dc, gx);
     }
@@ -1471,11 +1315,7 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
       xyz_backward<1, 1, 3, WG, PG || WG>(pk, c, q.x, g, dg, A, S, lane, dc, gx);
   }
   PHASE(DEC, 12);
-#ifdef NSLAM_EXP_NOSCATTER  // timing experiment only: no grid-gradient atomics
-  if (false) {
-#else
   if (gr.grad) {
-#endif
     if (WG) {
       scatter_grid_grad_halves(gr.grad, gr.slot, cr, dc, q.valid, S, lane);
     } else {  // walk table: the lean kernels' slot after the transpose image
@@ -1559,14 +1399,10 @@ struct MultiDecArgs {
   int dec[4];
   double* gp[4];
 };
-// The colour decoder may be a part WITH weight gradients: its tiles run the same mask-only chain
-// and store their cotangents in a.cot (k_color_wgrad, launched after this kernel, forms the
-// weight gradients), so every part is lean and the launch keeps the lean kernels' occupancy.
-#ifndef NSLAM_MULTI_COT_LB
-#define NSLAM_MULTI_COT_LB 2  // min workgroups per CU of the all-decoder lean launch with the colour tape
-#endif
-template <bool PG, bool COT>
-__global__ __launch_bounds__(64 * kWavesBwd, COT ? NSLAM_MULTI_COT_LB : 2) void k_dec_bwd_multi(QueryKArgs a, MultiDecArgs m) {
+// (a colour decoder with weight gradients runs here as its lean chain too: grid gradient, d/dpts;
+// its parameter gradients come from k_color_wgrad, nslam_color_wgrad.hip)
+template <bool PG>
+__global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd_multi(QueryKArgs a, MultiDecArgs m) {
   constexpr int kScr = TILE_FLOATS + kWalkFloats;
   __shared__ __attribute__((aligned(16))) float lds[kWavesBwd * kScr];
   const int lane = threadIdx.x & 63, wave = wave_id();
@@ -1586,47 +1422,7 @@ __global__ __launch_bounds__(64 * kWavesBwd, COT ? NSLAM_MULTI_COT_LB : 2) void 
     case NSLAM_DEC_COARSE: dec_bwd_tile<NSLAM_DEC_COARSE, 0, PG, true, true>(a, w, A, S, lane, gp); break;
     case NSLAM_DEC_MIDDLE: dec_bwd_tile<NSLAM_DEC_MIDDLE, 0, PG, true, true>(a, w, A, S, lane, gp); break;
     case NSLAM_DEC_FINE: dec_bwd_tile<NSLAM_DEC_FINE, 0, PG, true, true>(a, w, A, S, lane, gp); break;
-    default: dec_bwd_tile<NSLAM_DEC_COLOR, 0, PG, true, true, COT>(a, w, A, S, lane, gp); break;
-  }
-}
-
-// Mask-only backward of several frozen decoders with their d/dpts SUMMED (ABI v10,
-// NSLAM_BWD_SUM_PTS): one workgroup per tile, wave i evaluates decoder part i and stages its
-// d/dpts in LDS; after a barrier the parts are added in decoder order ((middle + fine) + colour,
-// the order of the per-decoder buffers' sum) and written once — no separate add kernels.
-template <bool PG_UNUSED = true>
-__global__ __launch_bounds__(256, 2) void k_dec_bwd_multi_sum(QueryKArgs a, MultiDecArgs m, double* __restrict__ out) {
-  constexpr int kScr = TILE_FLOATS + kWalkFloats;
-  __shared__ __attribute__((aligned(16))) float lds[4 * kScr];
-  __shared__ double stage[4][32 * 3];
-  const int lane = threadIdx.x & 63, part = wave_id();
-  const int64_t tile = blockIdx.x;
-  Scratch S;
-  S.sA = lds + part * kScr;
-  S.sX = S.gtab = S.xtab = S.cw = nullptr;
-  S.crow = S.ccell = nullptr;
-  for (int i = lane; i < 96; i += 64) stage[part][i] = 0.0;
-  __syncthreads();
-  const int dec = part == 0 ? m.dec[0] : part == 1 ? m.dec[1] : part == 2 ? m.dec[2] : m.dec[3];
-  const Slab A = make_slab(nullptr, 0);
-  double* st = &stage[part][0];
-  const int64_t gb = tile * 32;
-  switch (dec) {
-    case NSLAM_DEC_COARSE: dec_bwd_tile<NSLAM_DEC_COARSE, 0, true, true, true>(a, tile, A, S, lane, st, gb); break;
-    case NSLAM_DEC_MIDDLE: dec_bwd_tile<NSLAM_DEC_MIDDLE, 0, true, true, true>(a, tile, A, S, lane, st, gb); break;
-    case NSLAM_DEC_FINE: dec_bwd_tile<NSLAM_DEC_FINE, 0, true, true, true>(a, tile, A, S, lane, st, gb); break;
-    default: dec_bwd_tile<NSLAM_DEC_COLOR, 0, true, true, true, false>(a, tile, A, S, lane, st, gb); break;
-  }
-  __syncthreads();
-  if (part == 0) {
-    for (int i = lane; i < 96; i += 64) {
-      const int64_t idx = gb + i / 3;
-      if (idx < a.n) {
-        double v = stage[0][i];
-        for (int d = 1; d < m.ndec; ++d) v = v + stage[d][i];
-        out[gb * 3 + i] = v;
-      }
-    }
+    default: dec_bwd_tile<NSLAM_DEC_COLOR, 0, PG, true, true>(a, w, A, S, lane, gp); break;
   }
 }
 
@@ -1634,95 +1430,33 @@ __global__ __launch_bounds__(256, 2) void k_dec_bwd_multi_sum(QueryKArgs a, Mult
 // float4 c of slab r of every 64th slab group, so the 16 waves x 4 lane rows keep 64 slab streams
 // in flight per workgroup (~count/64 workgroups fill the chip; a wave load is 4 x 256-B
 // segments).  The 64 partials are combined in LDS in a fixed order: deterministic.
-// Optional Adam epilogue (ABI v12 nslam_color_wgrad_adam): the reduced gradient g = base + sum is
-// consumed at once by the same element update as k_adam (seg: the decoder's dense segment, its grad
-// == base) — param, exp_avg, exp_avg_sq and the packed mirror are written, base is left g (or 0 with
-// zero_grad), and the last workgroup advances the step count by the ticket (k_adam's protocol), so a
-// mapping iteration's decoder update needs no separate launch after its weight-gradient reduction.
-// ABI v14: further segments (the colour grid's frustum rows) ride in the same launch as workgroups
-// past the reduction's, each running k_adam's segment update (adam_segment_block).
-constexpr int kSlabAdamExtra = 3;
-struct SlabAdam {
-  nslam_adam_seg seg;
-  float b1, b2, eps;
-  int32_t zero_grad;
-  uint32_t* ticket;
-  int32_t on;
-  int32_t n_extra;
-  nslam_adam_seg extra[kSlabAdamExtra];
-  int64_t extra_blk0[kSlabAdamExtra + 1];  // first workgroup of each extra segment, past the reduction's
-};
 constexpr int kReduceWaves = 16;
 static __global__ __launch_bounds__(64 * kReduceWaves) void k_slab_reduce(const float* __restrict__ slab, int64_t nslab,
                                                                    int acc_floats, int count,
-                                                                   float* __restrict__ base, SlabAdam ad) {
+                                                                   float* __restrict__ base) {
   __shared__ f32x4 part[kReduceWaves * 4][16];
-  if (ad.on && (int64_t)blockIdx.x >= ad.extra_blk0[0]) {  // an extra segment's Adam workgroup
-    const int64_t b = blockIdx.x;
-    int s = 0;
-    while (s + 1 < ad.n_extra && b >= ad.extra_blk0[s + 1]) ++s;
-    const nslam_adam_seg& sg = ad.extra[s];
-    const AdamCoef co = adam_coef(ad.b1, ad.b2, ad.eps, sg.lr, *sg.step);
-    adam_segment_block(sg, co, b - ad.extra_blk0[s], ad.zero_grad, (int)threadIdx.x, 64 * kReduceWaves);
-  } else {  // the reduction (+ the decoder's Adam)
-    const int lane = threadIdx.x & 63, wave = wave_id();
-    const int c = lane & 15, r = wave * 4 + (lane >> 4);  // r: slab stream 0..63
-    const int j = (blockIdx.x * 16 + c) * 4;
-    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
-    if (j < count) {
-      const float* p = slab + j;
-      int64_t b = r;
-      for (; b + 64 < nslab; b += 128) {
-        s0 += *reinterpret_cast<const f32x4*>(p + b * acc_floats);
-        s1 += *reinterpret_cast<const f32x4*>(p + (b + 64) * acc_floats);
-      }
-      if (b < nslab) s0 += *reinterpret_cast<const f32x4*>(p + b * acc_floats);
+  const int lane = threadIdx.x & 63, wave = wave_id();
+  const int c = lane & 15, r = wave * 4 + (lane >> 4);  // r: slab stream 0..63
+  const int j = (blockIdx.x * 16 + c) * 4;
+  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
+  if (j < count) {
+    const float* p = slab + j;
+    int64_t b = r;
+    for (; b + 64 < nslab; b += 128) {
+      s0 += *reinterpret_cast<const f32x4*>(p + b * acc_floats);
+      s1 += *reinterpret_cast<const f32x4*>(p + (b + 64) * acc_floats);
     }
-    part[r][c] = s0 + s1;
-    __syncthreads();
-    if (threadIdx.x < 16 && j < count) {
-      f32x4 t = part[0][c];
-#pragma unroll 8
-      for (int k = 1; k < kReduceWaves * 4; ++k) t += part[k][c];
-      if (!ad.on) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (j + e < count) base[j + e] += t[e];
-      } else {
-        const nslam_adam_seg& sg = ad.seg;
-        const AdamCoef co = adam_coef(ad.b1, ad.b2, ad.eps, sg.lr, *sg.step);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int64_t i = j + e;
-          if (i < count) {
-            const float g = base[i] + t[e];
-            float p = sg.param[i], m = sg.exp_avg[i], v = sg.exp_avg_sq[i];
-            adam_one(p, g, m, v, co);
-            sg.param[i] = p;
-            sg.exp_avg[i] = m;
-            sg.exp_avg_sq[i] = v;
-            base[i] = ad.zero_grad ? 0.f : g;
-            if (sg.mirror) {
-              const int i0 = sg.mirror_idx[2 * i], i1 = sg.mirror_idx[2 * i + 1];
-              if (i0 >= 0) sg.mirror[i0] = p;
-              if (i1 >= 0) sg.mirror[i1] = p;
-            }
-          }
-        }
-      }
-    }
-  
+    if (b < nslab) s0 += *reinterpret_cast<const f32x4*>(p + b * acc_floats);
   }
-  if (ad.on) {  // every workgroup has read its step count: the last one advances them (k_adam's ticket)
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const uint32_t tk = __hip_atomic_fetch_add(ad.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (tk == gridDim.x - 1) {
-        *ad.seg.step += 1.f;
-        for (int k = 0; k < ad.n_extra; ++k) *ad.extra[k].step += 1.f;
-        __hip_atomic_store(ad.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
+  part[r][c] = s0 + s1;
+  __syncthreads();
+  if (threadIdx.x < 16 && j < count) {
+    f32x4 t = part[0][c];
+#pragma unroll 8
+    for (int k = 1; k < kReduceWaves * 4; ++k) t += part[k][c];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (j + e < count) base[j + e] += t[e];
   }
 }
 
@@ -1756,31 +1490,28 @@ inline int hip_status() {
 
 inline int acc_floats_of(const nslam_dec_grad& dg) { return (int)((dg.count + 3) & ~int64_t(3)); }
 
-// ---- the colour decoder's weight gradients from the tapes (k_color_wgrad, nslam_color_wgrad.hip) --
-// With the forward's activation tape and ReLU masks, the colour decoder's backward is two launches:
-// the lean mask-only chain (grid gradient; it also stores the cotangent tape) and k_color_wgrad, a
-// split-K reduction over tile chunks of every weight block (one 8-wave workgroup per chunk, the
-// tiles staged through LDS; each chunk's partial sums fill one slab), then k_slab_reduce over the
-// chunks.  Workspace: [cotangent tape | chunk slabs].
-constexpr int kCwTargetChunks = 256;  // one workgroup per CU (its LDS holds two staged tiles)
+// ---- the colour decoder's weight gradients (k_color_wgrad, nslam_color_wgrad.hip) ----------------
+// With the forward's activation tape and ReLU masks, the colour decoder's backward is two launches that
+// need not wait for each other: the lean mask-only chain (grid gradient, d/dpts) and k_color_wgrad, a
+// split-K reduction over tile chunks of every weight block (one 8-wave workgroup per chunk; each
+// chunk's partial sums fill one slab), then k_slab_reduce over the chunks.  Workspace: the chunk slabs.
+constexpr int kCwTargetChunks = 256;  // one workgroup per CU
 struct CwPlan {
   int64_t chunk_tiles;
   int nchunks;
-  size_t cot_bytes, slab_bytes;
+  size_t slab_bytes;
 };
 inline CwPlan cw_plan(const nslam_dec_grad& dg, int64_t n_pts) {
   CwPlan p;
   const int64_t tiles = (n_pts + 31) / 32;
   p.chunk_tiles = (tiles + kCwTargetChunks - 1) / kCwTargetChunks;
   p.nchunks = (int)((tiles + p.chunk_tiles - 1) / p.chunk_tiles);
-  p.cot_bytes = ((size_t)tiles * kCotFloats * sizeof(float) + 255) & ~(size_t)255;
   p.slab_bytes = (size_t)p.nchunks * acc_floats_of(dg) * sizeof(float);
   return p;
 }
 inline bool cw_tape_path(const nslam_query_cfg* c) { return c->act_tape != nullptr && c->saved_masks != nullptr; }
-// k_color_wgrad + k_slab_reduce into a.c.dgrad[COLOR] after the lean chain has filled the cotangent
-// tape at ws (a.cot is set from ws); nslam_color_wgrad.hip
-int launch_color_wgrad(const QueryKArgs& a, float* ws, hipStream_t s, const SlabAdam* adam = nullptr);
+// k_color_wgrad + k_slab_reduce into a.c.dgrad[COLOR] (a.g_raw: the cotangent; ws: the chunk slabs)
+int launch_color_wgrad(const QueryKArgs& a, float* ws, hipStream_t s);
 
 // Slab cap: kMaxSlabs, or NSLAM_MAX_SLABS from the environment (tests use it to reach the
 // multi-tile read-modify-write mode at small sizes).
@@ -1806,21 +1537,12 @@ int launch_one(const QueryKArgs& a, float* slab, int acc, int64_t blocks, hipStr
 
 // WG == 1 launches leave one folded slab per workgroup (stride kWavesBwd slabs); WG == 2 one per wave
 inline int slab_reduce(const nslam_dec_grad& dg, float* slab, bool folded, int64_t nslab, int64_t blocks, int acc,
-                       hipStream_t s, const SlabAdam* adam = nullptr) {
+                       hipStream_t s) {
   const int64_t n = folded ? blocks : nslab;
   const int stride = folded ? acc * kWavesBwd : acc;
-  SlabAdam ad{};
-  int64_t nblk = (dg.count + 63) / 64;  // the reduction's workgroups, then the extra segments'
-  if (adam) {
-    ad = *adam;
-    for (int k = 0; k < ad.n_extra; ++k) {
-      ad.extra_blk0[k] = nblk;
-      nblk += adam_segment_blocks(ad.extra[k], 64 * kReduceWaves);
-    }
-    ad.extra_blk0[ad.n_extra] = nblk;
-  }
-  hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)nblk), dim3(64 * kReduceWaves), 0, s, slab, n,
-                     stride, (int)dg.count, dg.base, ad);
+  const int64_t nblk = (dg.count + 63) / 64;
+  hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)nblk), dim3(64 * kReduceWaves), 0, s, slab, n, stride,
+                     (int)dg.count, dg.base);
   return hip_status();
 }
 
@@ -1839,16 +1561,14 @@ int launch_dec_bwd(const QueryKArgs& a, bool first, float* slab, hipStream_t s) 
   const int acc = acc_floats_of(dg);
   const int64_t nslab = n_slabs(tiles);
   const int64_t blocks = (nslab + kWavesBwd - 1) / kWavesBwd;
-  // the colour decoder's weight gradients read the forward's activation tape when it is there:
-  // the lean chain (+ cotangent tape) then k_color_wgrad
+  // the colour decoder's weight gradients from the forward's activation tape when it is there: the
+  // lean chain (grid gradient), then k_color_wgrad (which does not read anything the chain wrote)
   constexpr bool kTapeable = DEC == NSLAM_DEC_COLOR && !PG;
   int rc;
   if constexpr (kTapeable) {
     if (cw_tape_path(&a.c)) {
-      QueryKArgs b = a;
-      b.cot = slab;
-      rc = launch_one<DEC, 0, false, true, true>(b, nullptr, 0, (tiles + kWavesBwd - 1) / kWavesBwd, s);
-      return rc || a.defer_wgrad ? rc : launch_color_wgrad(a, slab, s);
+      rc = launch_one<DEC, 0, false, true, true>(a, nullptr, 0, (tiles + kWavesBwd - 1) / kWavesBwd, s);
+      return rc ? rc : launch_color_wgrad(a, slab, s);
     }
   }
   if (tiles > max_slabs() && hipMemsetAsync(slab, 0, (size_t)nslab * acc * sizeof(float), s) != hipSuccess)
@@ -1888,8 +1608,7 @@ inline size_t dec_ws_bytes(const nslam_query_cfg* cfg, int dec, int64_t n_pts) {
   const nslam_dec_grad& dg = cfg->dgrad[dec];
   if (!dg.base || dg.count <= 0) return 0;
   if (dec == NSLAM_DEC_COLOR && cw_tape_path(cfg)) {
-    const CwPlan p = cw_plan(dg, n_pts);
-    return p.cot_bytes + p.slab_bytes;
+    return cw_plan(dg, n_pts).slab_bytes;
   }
   return (size_t)n_slabs((n_pts + 31) / 32) * acc_floats_of(dg) * sizeof(float);
 }

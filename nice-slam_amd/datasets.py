@@ -27,7 +27,7 @@ import torch.nn.functional as F
 def _read_color(path):
     from PIL import Image
     with Image.open(path) as im:
-        return np.asarray(im.convert("RGB"))  # == cv2.imread + COLOR_BGR2RGB (datasets.py:80,90)
+        return np.array(im.convert("RGB"))  # == cv2.imread + COLOR_BGR2RGB (datasets.py:80,90); writable
 
 
 def _read_depth(path):

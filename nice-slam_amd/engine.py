@@ -21,8 +21,9 @@ the frustum-selected voxels in place instead of through masked copies (Mapper.py
 from __future__ import annotations
 
 import ctypes
-import os
 import math
+import os
+import weakref
 
 import numpy as np
 import torch
@@ -99,47 +100,12 @@ class MappingEngine:
         self._pre_stream = None
         self._side = []     # side streams of the concurrent decoder backward
         self.concurrent = True
-        self.priority = False  # concurrent: run the weight-gradient branch on a high-priority stream
-        self.all_side = False  # concurrent: every branch on a side stream (main only forks / joins)
-        self.lean_first = False  # concurrent: enqueue the frozen decoders' branches before the weight-gradient one
-        # frozen decoders' mask-only backward as one launch (ABI v10) whenever there are several
-        # (tracking: 0.199 -> 0.117 ms per iteration; mapping, beside the colour branch's lean chain +
-        # k_color_wgrad: 205-208 vs 195-197 M ray-samples/s, profiles/r03_knobs.txt); False = one
-        # launch per decoder; "all": every decoder, the colour weight gradients included, in one
-        # launch (experiment)
-        self.merge_frozen = True
-        # ABI v11 split: the colour lean chain alone first, then its weight-gradient reduction beside
-        # the frozen decoders' backward (wgrad_side: which of the two forks off).  Measured slower
-        # (182 vs 199 M ray-samples/s, profiles/r03_knobs.txt): the lean kernels are latency-bound at
-        # the colour chain's 1500 waves (60 us alone vs 76 us for all three decoders together).
-        self.split_wgrad = False
-        self.wgrad_side = True
-        # merged d/dpts summed inside the launch (NSLAM_BWD_SUM_PTS, one workgroup per tile): measured
-        # 0.109 vs 0.102 ms per tracking iteration for per-decoder buffers + two adds — kept off
-        self.sum_pts = False
-        # ABI v14: with per-branch Adam the colour branch may fold the colour decoder's and colour
-        # grid's Adam step into the weight-gradient slab reduction (nslam_color_wgrad_adam) — one
-        # launch fewer.  Measured 199-203 vs 206-208 M ray-samples/s for the separate Adam launch in
-        # the hipGraph'd room0 iteration (the fused reduction takes 16.7 us against 8.8 + 9.7): off.
-        self.fuse_adam = os.environ.get("NSLAM_FUSE_ADAM", "0") == "1"
-        # the colour grid's Adam in the frozen branch's Adam call (that stream waits for the colour
-        # lean chain), off the colour branch's critical path: lean -> weight gradients -> decoder Adam
-        self.cgrid_side = os.environ.get("NSLAM_CGRID_SIDE", "1") == "1"
-        self._lean_ev = None
-        # Cross-iteration pipelining (colour stage, one rank, per-branch Adam; experiment, off: measured
-        # 181-185 vs 206-208 M ray-samples/s — the two forward halves side by side take 100 us against
-        # the single decoder-parallel launch's 91 us, which the overlap does not win back): the colour
-        # branch (lean chain -> weight gradients with the colour decoder's and grid's Adam, ABI v14)
-        # stays on its own stream past the end of iteration(), and the next iteration's forward is
-        # split (ABI v13 nslam_query_fwd_parts): its middle | fine parts — which read neither the
-        # colour grid nor the colour decoder — start as soon as the frozen branch's grid Adam is done,
-        # its colour part queues behind the colour branch.  Every iteration still sees the map its predecessor
-        # left (the same dependencies as the serial loop).  Callers join() before reading the colour
-        # decoder / grid or ending a graph capture.
-        self.pipeline = False
-        self._col_pending = False
-        self._col_stream = None   # the colour branch (+ the next forward's colour part)
-        self._hi = None
+        # concurrent backward: enqueue the colour weight-gradient branch before the grid-gradient one
+        # (its workgroups are dispatched first and hold one slot per CU; the lean launch fills the rest)
+        self.wgrad_first = os.environ.get("NSLAM_WGRAD_FIRST", "1") == "1"
+        # every mask-only decoder backward as ONE launch (ABI v10); False: one nslam_query_bwd_decoder
+        # launch per decoder (the library then runs a colour tape backward's two kernels in sequence)
+        self.merge = True
         for k, v in c.items():
             if not v.is_contiguous(memory_format=torch.channels_last_3d):
                 raise ValueError(f"{k} must be channels-last (ops.channels_last)")
@@ -224,278 +190,110 @@ class MappingEngine:
 
     def query_bwd(self, stage, ro, rd, z, g_raw, grid_grads, dec_grads, concurrent=None, pts_grad=False,
                   on_branch=None, pts_parts=False):
-        """Backward into the engine's gradient buffers.  The decoders write disjoint buffers, so
-        each runs as its own launch; with `concurrent` the frozen decoders (mask-only backward,
-        atomics-heavy) run on side streams beside the one with weight gradients (MFMA-heavy) —
-        parallel branches when captured in a hipGraph.
+        """Backward into the engine's gradient buffers, as independent launches ("branches") that write
+        disjoint buffers:
+          lean     every decoder's grid gradient (and d/dpts) from the forward's ReLU masks, ONE launch
+                   (ABI v10 nslam_query_bwd_decoders; the trainable colour decoder included);
+          wgrad    the colour decoder's parameter gradients (ABI v16 nslam_color_wgrad), which reads only
+                   the forward's tapes and g_raw — so it runs beside the lean launch;
+          others   a decoder with parameter gradients and no tape path (nslam_query_bwd_decoder each).
+        With `concurrent` the branches run on separate streams (parallel branches of a captured hipGraph).
 
         pts_grad: also return d loss / d pts [N*S, 3] float64 (tracking, bundle adjustment): every
-        decoder writes its share into its own buffer (so the branches stay independent) and the
-        shares are summed afterwards.
-        on_branch(names): called on each launch's stream right after it, with the decoders it covered
-        (the per-branch Adam of the mapping iteration: a grid's rows depend on its branch alone)."""
+        decoder writes its share into its own buffer and the shares are summed afterwards (or returned
+        as a list with pts_parts).
+        on_branch(names, part): called on each branch's stream right after it ("grids": the grids of
+        the decoders the lean launch covered; "decoders": a decoder's parameters) — the per-branch Adam
+        of the mapping iteration (a grid's rows, or a decoder, depend on that branch alone)."""
         n = z.numel()
         self._clean = False
         concurrent = self.concurrent if concurrent is None else concurrent
         cfg = self._cfg(stage, ro, rd, z, grid_grads, dec_grads)
         cfg.need_pts_grad = int(bool(pts_grad))
-        decs = sorted(ops._DEC_FOR_STAGE[stage], key=lambda d: d not in dec_grads)  # weight-grad one first
-        frozen = [d for d in decs if d not in dec_grads]
-        if (self.split_wgrad and concurrent and not pts_grad and list(dec_grads) == ["color"] and frozen
-                and self._tape is not None and self._saved is not None and n > 0):
-            return self._query_bwd_split(cfg, n, z, g_raw, frozen, on_branch)
-        gp = [torch.empty(n, 3, dtype=torch.float64, device=z.device) for _ in decs] if pts_grad else None
-        # units of work: (decoder names, stream index); the frozen decoders' mask-only backward is one
-        # launch (ABI v10 nslam_query_bwd_decoders) — no fork / join between their streams
-        merge = self.merge_frozen
+        decs = list(ops._DEC_FOR_STAGE[stage])
         wgt = [d for d in decs if d in dec_grads]
-        if (merge == "all" and self._saved is not None and not pts_grad and wgt == ["color"]
-                and self._tape is not None):
-            units = [list(decs)]  # every decoder, the colour weight gradients included: one launch
-        elif merge and len(frozen) > 1 and self._saved is not None:
-            units = [[d] for d in wgt] + [frozen]
-        else:
-            units = [[d] for d in decs]
+        masks = self._saved is not None
+        tape_color = "color" in wgt and masks and self._tape is not None
+        lean = [d for d in decs if self.merge and masks and (d not in wgt or (d == "color" and tape_color))]
+        others = [d for d in decs if d not in lean]
+        gp = {d: torch.empty(n, 3, dtype=torch.float64, device=z.device) for d in decs} if pts_grad else None
+        # units: (kind, decoder names) in enqueue order
+        units = []
+        if "color" in lean and "color" in wgt and n > 0:
+            units.append(("wgrad", ["color"]))
+        if lean:
+            units.append(("lean", lean))
+        units += [("one", [d]) for d in others]
+        if not self.wgrad_first:
+            units.sort(key=lambda u: u[0] == "wgrad")
         main = torch.cuda.current_stream(z.device)
+        par = concurrent and len(units) > 1
         streams = [main]
-        if concurrent and len(units) > 1:
-            while len(self._side) < len(units):
+        if par:
+            while len(self._side) < len(units) - 1:
                 self._side.append(torch.cuda.Stream(z.device))
-            if self.priority:  # the critical (MFMA-heavy) branch gets its waves dispatched first
-                if self._hi is None:
-                    self._hi = torch.cuda.Stream(z.device, priority=-1)
-                streams = [self._hi]
-            elif self.all_side:
-                streams = [self._side[len(units) - 1]]
             streams += self._side[:len(units) - 1]
-        used = [st for st in streams if st is not main]
-        cgrid_ev = None  # the colour lean chain's completion, when the colour grid's Adam joins the frozen branch
-        summed = False
+        used = streams[1:]
         with ops._span("query_bwd"):
             for st in used:  # fork: every branch starts from the same point of the main stream
                 st.wait_stream(main)
                 for t in (ro, rd, z, g_raw, self._saved, self._tape):
                     if t is not None:
                         t.record_stream(st)
-            order = list(enumerate(units))
-            if concurrent and self.lean_first:
-                order = order[1:] + order[:1]
-            for i, names in order:
-                st = streams[i] if (concurrent and len(units) > 1) else main
+            for i, (kind, names) in enumerate(units):
+                st = streams[i] if par else main
                 with torch.cuda.stream(st):
-                    if len(names) > 1:
-                        mask = 0
+                    if kind == "wgrad":
+                        wsb = lib().nslam_query_bwd_decoder_workspace_size(ctypes.byref(cfg), _lib.DEC_COLOR, n)
+                        ws = torch.empty(wsb, dtype=torch.uint8, device=z.device)
+                        with ops._span("query_bwd.color_wgrad"):
+                            rc = lib().nslam_color_wgrad(ctypes.byref(cfg), None, n, ptr(g_raw), ptr(ws), wsb,
+                                                         st.cuda_stream)
+                        check(rc, "nslam_color_wgrad")
+                        if on_branch is not None:
+                            on_branch(names, part="decoders")
+                    elif kind == "lean":
+                        lc = _lib.NslamQueryCfg.from_buffer_copy(cfg)  # grids (and d/dpts) only
                         gps = (ctypes.c_void_p * 4)()
+                        mask = 0
                         for name in names:
                             d = ops._DEC_ID[name]
                             mask |= 1 << d
+                            lc.dgrad[d] = _lib.NslamDecGrad()
                             if pts_grad:
-                                gps[d] = ptr(gp[decs.index(name)])
-                        if pts_grad and names == decs and self.sum_pts:
-                            # every decoder in this launch: their d/dpts summed in the kernel, in decoder
-                            # order (what the loop below would add), into the first buffer
-                            mask |= _lib.BWD_SUM_PTS
-                            gps[0] = ptr(gp[0])
-                            summed = True
-                        wsb = 0
-                        if "color" in names and "color" in dec_grads:
-                            wsb = lib().nslam_query_bwd_decoder_workspace_size(ctypes.byref(cfg), ops._DEC_ID["color"], n)
-                        ws = torch.empty(wsb, dtype=torch.uint8, device=z.device) if wsb else None
+                                gps[d] = ptr(gp[name])
                         with ops._span("query_bwd." + "+".join(names)):
-                            rc = lib().nslam_query_bwd_decoders(ctypes.byref(cfg), mask, None, n, ptr(g_raw), gps,
-                                                                ptr(ws), wsb, st.cuda_stream)
+                            rc = lib().nslam_query_bwd_decoders(ctypes.byref(lc), mask, None, n, ptr(g_raw), gps,
+                                                                st.cuda_stream)
                         check(rc, "nslam_query_bwd_decoders")
+                        if on_branch is not None:
+                            on_branch(names, part="grids")
                     else:
                         name = names[0]
                         d = ops._DEC_ID[name]
                         wsb = lib().nslam_query_bwd_decoder_workspace_size(ctypes.byref(cfg), d, n)
                         ws = torch.empty(wsb, dtype=torch.uint8, device=z.device) if wsb else None
-                        tape_bwd = (name == "color" and name in dec_grads and not pts_grad and on_branch is not None
-                                    and hasattr(on_branch, "color_wgrad") and self._tape is not None
-                                    and self._saved is not None)
-                        # the colour grid's Adam beside the weight gradients, in the frozen branch's Adam
-                        # (the frozen unit must come after this one: it picks the colour grid's Adam up)
-                        cside = (tape_bwd and self.cgrid_side and any(len(u) > 1 for u in units) and concurrent
-                                 and not self.lean_first)
-                        fused = tape_bwd and (self.fuse_adam or cside)
-                        # (the split colour backward is timed as its two kernels: the lean chain and the
-                        # weight-gradient reduction have different bounds)
-                        with ops._span("query_bwd." + name) if not fused else ops._NOSPAN:
-                            if fused:  # lean chain, then weight gradients (+ the colour Adam in the reduction)
-                                with ops._span("query_bwd.color_lean"):
-                                    rc = lib().nslam_query_bwd_decoders(ctypes.byref(cfg),
-                                                                        (1 << d) | _lib.BWD_DEFER_WGRAD, None, n,
-                                                                        ptr(g_raw), (ctypes.c_void_p * 4)(), ptr(ws),
-                                                                        wsb, st.cuda_stream)
-                                check(rc, "nslam_query_bwd_decoders(colour lean)")
-                                if cside:
-                                    if self._lean_ev is None:  # one persistent event (never destroyed mid-capture)
-                                        self._lean_ev = torch.cuda.Event()
-                                    self._lean_ev.record(st)
-                                    cgrid_ev = self._lean_ev
-                                with ops._span("query_bwd.color_wgrad"):
-                                    if self.fuse_adam:
-                                        on_branch.color_wgrad(cfg, n, ws, wsb, st, grids=not cside)
-                                    else:
-                                        rc = lib().nslam_color_wgrad(ctypes.byref(cfg), n, ptr(ws), wsb,
-                                                                     st.cuda_stream)
-                                        check(rc, "nslam_color_wgrad")
-                            else:
-                                rc = lib().nslam_query_bwd_decoder(ctypes.byref(cfg), d, 0, None, n, ptr(g_raw),
-                                                                   ptr(gp[decs.index(name)]) if pts_grad else None,
-                                                                   ptr(ws), wsb, st.cuda_stream)
-                                check(rc, "nslam_query_bwd_decoder")
-                        if fused:
-                            if not self.fuse_adam:  # the decoder's Adam (outside the backward's span)
-                                on_branch(names, part="decoders")
-                            continue
-                    if on_branch is not None:
-                        if cgrid_ev is not None and len(names) > 1:  # + the colour grid, once its lean chain is done
-                            st.wait_event(cgrid_ev)
-                            on_branch(list(names) + ["color"], part="grids")
-                            cgrid_ev = None
-                        else:
+                        with ops._span("query_bwd." + name):
+                            rc = lib().nslam_query_bwd_decoder(ctypes.byref(cfg), d, 0, None, n, ptr(g_raw),
+                                                               ptr(gp[name]) if pts_grad else None, ptr(ws), wsb,
+                                                               st.cuda_stream)
+                        check(rc, "nslam_query_bwd_decoder")
+                        if on_branch is not None:
                             on_branch(names)
                 if pts_grad and st is not main:
                     for name in names:
-                        gp[decs.index(name)].record_stream(st)
+                        gp[name].record_stream(st)
             for st in used:
                 main.wait_stream(st)
-        if pts_grad and summed:
-            return gp[0]
-        if pts_grad and pts_parts:  # the per-decoder shares, for a consumer that sums them itself
-            return gp
-        if pts_grad:
-            out = gp[0]
-            for g in gp[1:]:
-                out += g
-            return out
-        return None
-
-    def _query_bwd_split(self, cfg, n, z, g_raw, frozen, on_branch):
-        """The mapping iteration's backward with the colour decoder's weight gradients split off
-        (ABI v11): the colour lean chain first (its grid gradient and cotangent tape), then its
-        weight-gradient reduction (MFMA / LDS bound) on one stream beside the frozen decoders'
-        mask-only backward (float-atomic bound) on the other, so the two kinds of work overlap."""
-        main = torch.cuda.current_stream(z.device)
-        if not self._side:
-            self._side.append(torch.cuda.Stream(z.device))
-        side = self._side[0]
-        dcol = ops._DEC_ID["color"]
-        wsb = lib().nslam_query_bwd_decoder_workspace_size(ctypes.byref(cfg), dcol, n)
-        ws = torch.empty(wsb, dtype=torch.uint8, device=z.device)
-        gps = (ctypes.c_void_p * 4)()
-        with ops._span("query_bwd"):
-            with ops._span("query_bwd.color_lean"):
-                rc = lib().nslam_query_bwd_decoders(ctypes.byref(cfg), (1 << dcol) | _lib.BWD_DEFER_WGRAD, None, n,
-                                                    ptr(g_raw), gps, ptr(ws), wsb, main.cuda_stream)
-            check(rc, "nslam_query_bwd_decoders(colour lean)")
-            side.wait_stream(main)
-            for t in (z, g_raw, self._saved, self._tape, ws):
-                t.record_stream(side)
-            wst, fst = (side, main) if self.wgrad_side else (main, side)
-            with torch.cuda.stream(wst):
-                with ops._span("query_bwd.color_wgrad"):
-                    rc = lib().nslam_color_wgrad(ctypes.byref(cfg), n, ptr(ws), wsb, wst.cuda_stream)
-                check(rc, "nslam_color_wgrad")
-                if on_branch is not None:
-                    on_branch(["color"])
-            with torch.cuda.stream(fst):
-                mask = 0
-                for name in frozen:
-                    mask |= 1 << ops._DEC_ID[name]
-                with ops._span("query_bwd." + "+".join(frozen)):
-                    rc = lib().nslam_query_bwd_decoders(ctypes.byref(cfg), mask, None, n, ptr(g_raw), gps, None, 0,
-                                                        fst.cuda_stream)
-                check(rc, "nslam_query_bwd_decoders")
-                if on_branch is not None:
-                    on_branch(frozen)
-            main.wait_stream(side)
-        return None
-
-    # -- cross-iteration pipelining (self.pipeline) ------------------------------------------------
-    def join(self):
-        """Make the current stream wait for a pipelined colour branch still in flight (call before
-        reading the colour decoder / colour grid, or before ending a graph capture)."""
-        if self._col_stream is not None:
-            torch.cuda.current_stream(self.device).wait_stream(self._col_stream)
-        self._col_pending = False
-
-    def _pipe_streams(self):
-        if self._col_stream is None:
-            self._col_stream = torch.cuda.Stream(self.device)
-        return self._col_stream
-
-    def _query_fwd_pipelined(self, ro, rd, z):
-        """Colour-stage forward as two launches: middle | fine on the current stream, colour on the
-        colour stream (behind the previous iteration's colour branch); returns raw (occupancy of the
-        middle decoder deferred into self.occ_add, as query_fwd(defer_occ=True))."""
-        main = torch.cuda.current_stream(self.device)
-        sc = self._pipe_streams()
-        n = z.numel()
-        raw = torch.empty(n, 4, dtype=torch.float32, device=z.device)
-        self._saved = torch.empty(lib().nslam_query_saved_size(n), dtype=torch.uint8, device=z.device)
-        self._tape = torch.empty(lib().nslam_query_tape_size(n) // 4, dtype=torch.float32, device=z.device)
-        cfg = self._cfg("color", ro, rd, z, (), ())
-        cfg.defer_occ = 1
-        wsb = lib().nslam_query_fwd_workspace_size(ctypes.byref(cfg), n)
-        ws = torch.empty(wsb, dtype=torch.uint8, device=z.device)
-        # fork BEFORE the middle | fine launch: the colour half needs the rays and the buffers just
-        # allocated on main, and (in stream order on sc) the previous iteration's colour branch
-        sc.wait_stream(main)
-        with ops._span("query_fwd.middle+fine"):
-            rc = lib().nslam_query_fwd_parts(ctypes.byref(cfg), None, n, ptr(raw), ptr(ws), wsb, 3, main.cuda_stream)
-        check(rc, "nslam_query_fwd_parts(middle | fine)")
-        with torch.cuda.stream(sc):
-            with ops._span("query_fwd.color"):
-                rc = lib().nslam_query_fwd_parts(ctypes.byref(cfg), None, n, ptr(raw), ptr(ws), wsb, 4,
-                                                 sc.cuda_stream)
-        check(rc, "nslam_query_fwd_parts(colour)")
-        main.wait_stream(sc)
-        self.occ_add = ws[:n * 4].view(torch.float32)
-        return raw
-
-    def _query_bwd_pipelined(self, ro, rd, z, g_raw, keys, frozen, on_branch):
-        """The colour stage's backward with per-branch Adam: the colour stream runs the colour lean
-        chain, then the weight gradients with the colour decoder's and colour grid's Adam in the
-        reduction (ABI v14), and is NOT joined into the current stream (the next iteration's colour
-        forward queues behind it); the current stream runs the frozen decoders' merged mask-only
-        launch and the middle / fine grids' Adam.  So the next forward's middle | fine half (which
-        reads neither the colour grid nor the colour decoder) does not wait for the colour branch.
-        (Stream topology chosen for hipGraph capture on this stack: a stream forked off the colour
-        stream and joined back into it crashes hipStreamEndCapture, tools/probes/capture_topology.py
-        pattern t3.)"""
-        main = torch.cuda.current_stream(self.device)
-        sc = self._pipe_streams()
-        n = z.numel()
-        cfg = self._cfg("color", ro, rd, z, keys, ("color",))
-        cfg.need_pts_grad = 0
-        self._clean = False
-        dcol = ops._DEC_ID["color"]
-        # the colour workspace is allocated on the current stream (inside a graph capture the caching
-        # allocator serves the capturing stream's pool)
-        wsb = lib().nslam_query_bwd_decoder_workspace_size(ctypes.byref(cfg), dcol, n)
-        ws = torch.empty(wsb, dtype=torch.uint8, device=z.device)
-        mask = 0
-        for name in frozen:
-            mask |= 1 << ops._DEC_ID[name]
-        with ops._span("query_bwd"):
-            sc.wait_stream(main)
-            for t in (ro, rd, z, g_raw, self._saved, self._tape, ws):
-                t.record_stream(sc)
-            with torch.cuda.stream(sc):
-                with ops._span("query_bwd.color"):
-                    rc = lib().nslam_query_bwd_decoders(ctypes.byref(cfg), (1 << dcol) | _lib.BWD_DEFER_WGRAD, None, n,
-                                                        ptr(g_raw), (ctypes.c_void_p * 4)(), ptr(ws), wsb,
-                                                        sc.cuda_stream)
-                    check(rc, "nslam_query_bwd_decoders(colour lean)")
-                    on_branch.color_wgrad(cfg, n, ws, wsb, sc)  # (+ the colour decoder's and grid's Adam)
-            with ops._span("query_bwd." + "+".join(frozen)):
-                rc = lib().nslam_query_bwd_decoders(ctypes.byref(cfg), mask, None, n, ptr(g_raw),
-                                                    (ctypes.c_void_p * 4)(), None, 0, main.cuda_stream)
-            check(rc, "nslam_query_bwd_decoders")
-            on_branch(frozen)
-            self._col_pending = True  # the next prefetch reuses this batch's rays: it waits for sc
+        if not pts_grad:
+            return None
+        parts = [gp[d] for d in decs]
+        if pts_parts:  # the per-decoder shares, for a consumer that sums them itself
+            return parts
+        out = parts[0]
+        for g in parts[1:]:
+            out += g
+        return out
 
     # -- one iteration ---------------------------------------------------------------------------
     def grads_for(self, stage, trainable_decoders):
@@ -564,23 +362,25 @@ class MappingEngine:
         prefetch = prefetch and pix is None
         side = None
         if prefetch:
-            # the frames' identity and version counters: a prefetched batch is only valid for the very
-            # frames (images and poses, unmodified) it was gathered from
-            fkey = tuple((t.data_ptr(), t._version) for f in frames for t in f)
-            pkey = (stage, fkey, n_per, hw, use_gt_in_sampler, seed, world, rank)
-            if self._pre is None or self._pre[0] != pkey:
+            # A prefetched batch is only valid for the very frames (images and poses, unmodified) it was
+            # gathered from: held by weak reference (identity — a new tensor that reuses a freed one's
+            # address is not the same frame) and version counter.
+            ftens = [t for f in frames for t in f]
+            pkey = (stage, n_per, hw, use_gt_in_sampler, seed, world, rank)
+            valid = (self._pre is not None and self._pre[0] == pkey and len(self._pre[1]) == len(ftens)
+                     and all(r() is t and v == t._version for (r, v), t in zip(self._pre[1], ftens)))
+            if not valid:
                 first = rays()  # first call: this iteration's batch (set 0), then a same-shaped set 1
-                self._pre = (pkey, [first, [torch.empty_like(t) for t in first]])
+                self._pre = (pkey, [(weakref.ref(t), t._version) for t in ftens],
+                             [first, [torch.empty_like(t) for t in first]])
                 self._parity = 0
-            cur, nxt = self._pre[1][self._parity], self._pre[1][1 - self._parity]
+            cur, nxt = self._pre[2][self._parity], self._pre[2][1 - self._parity]
             self._parity ^= 1
             main = torch.cuda.current_stream(self.device)
             if self._pre_stream is None:
                 self._pre_stream = torch.cuda.Stream(self.device)
             side = self._pre_stream
             side.wait_stream(main)  # the previous iteration's backward has released `nxt`
-            if self._col_pending and self._col_stream is not None:
-                side.wait_stream(self._col_stream)  # (a pipelined colour lean chain reads `nxt` too)
             with torch.cuda.stream(side):
                 rays(out=nxt)  # the next iteration's batch, beside this iteration's render + backward
             ro, rd, gd, gc, keep, z = cur
@@ -588,18 +388,10 @@ class MappingEngine:
             ro, rd, gd, gc, keep, z = rays()
         keys, dnames = self.grads_for(stage, trainable_decoders)
         mirror = hasattr(optimizer, "set_mirror")
-        pipe = (self.pipeline and stage == "color" and tuple(dnames) == ("color",)
-                and exchange is None and allreduce is None and mirror and hasattr(optimizer, "color_wgrad_step"))
-        if not pipe:
-            self.join()  # a pipelined predecessor's colour branch must finish before a serial iteration
-        if pipe:
-            raw = self._query_fwd_pipelined(ro, rd, z)
-        else:
-            raw = self.query_fwd(stage, ro, rd, z, defer_occ=True, tape="color" in dnames)
+        raw = self.query_fwd(stage, ro, rd, z, defer_occ=True, tape="color" in dnames)
         _, _, _, ray_loss, g_raw = ops.render_loss(raw, z, gd, gc, keep, mode="mapper", use_color=stage == "color",
                                                    w_color=self.w_color, occ_add=self.occ_add)
         if not self._clean:
-            self.join()  # (a pipelined colour branch may still be writing the decoder gradient)
             self.gall.zero_()  # grid and decoder gradients: one memset
         # Adam resets every gradient entry it reads.  With compact gradients for every grid of the
         # stage that is every entry the backward wrote, so the next iteration needs no memsets.
@@ -612,9 +404,9 @@ class MappingEngine:
         grads = self.adam_grads(stage, trainable_decoders)
         on_branch = None
         if exchange is None and allreduce is None and mirror:
-            # one rank: each decoder branch updates its own grid's rows (+ the trainable decoder's
-            # parameters, after its slab reduction) on its own stream — the update of a grid needs
-            # that branch's gradients alone, so no branch waits for the others before its Adam
+            # one rank: each backward branch updates what it alone completes on its own stream — the
+            # lean launch its decoders' grid rows, the weight-gradient branch the colour decoder — so
+            # no branch waits for the others before its Adam
             def on_branch(names, part=None):  # the decoders of one launch: one Adam call for their grids
                 sub = {}                         # (part "grids" / "decoders": only those)
                 for name in names:
@@ -625,18 +417,7 @@ class MappingEngine:
                 if sub:
                     optimizer.step(grads=sub, zero_grad=clean)
 
-            if hasattr(optimizer, "color_wgrad_step"):
-                def color_wgrad(cfg, n, ws, wsb, st, grids=True):  # weight gradients + the colour Adam, one reduction
-                    p = self.decs["color"].param
-                    extra = {self.c[k]: grads[self.c[k]] for k in ("grid_color",) if k in keys and grids}
-                    optimizer.color_wgrad_step(cfg, n, ws, wsb, p, grads[p], extra=extra, zero_grad=clean, stream=st)
-
-                on_branch.color_wgrad = color_wgrad
-        if pipe:
-            self._query_bwd_pipelined(ro, rd, z, g_raw, keys, [d for d in ops._DEC_FOR_STAGE[stage] if d != "color"],
-                                      on_branch)
-        else:
-            self.query_bwd(stage, ro, rd, z, g_raw, keys, dnames, on_branch=on_branch)
+        self.query_bwd(stage, ro, rd, z, g_raw, keys, dnames, on_branch=on_branch)
         if exchange is not None:  # frustum-compacted all-reduce (distributed.SparseGradExchange)
             exchange(keys, dnames)
         elif allreduce is not None:  # the grid gradients as one flat buffer, plus the decoder gradients

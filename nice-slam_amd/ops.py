@@ -825,33 +825,6 @@ class FusedAdam:
                                        stream_ptr(self.device))
         check(rc, "nslam_adam_step")
 
-    @torch.no_grad()
-    def color_wgrad_step(self, cfg, n, ws, ws_bytes, p, grad, extra=None, zero_grad=False, stream=None):
-        """The colour decoder's weight gradients from its tapes (the lean chain ran with
-        NSLAM_BWD_DEFER_WGRAD into `ws`) with this optimiser's Adam step for `p` (its flat parameter,
-        gradient `grad` = cfg.dgrad[COLOR].base) — and for the parameters in `extra` ({param: grad},
-        e.g. the colour grid's frustum rows) — applied inside the slab-reduction launch: ABI v14
-        nslam_color_wgrad_adam, the same update as step(grads={p: grad, **extra}), bit for bit."""
-        segs = self.segments({p: grad})
-        if len(segs) != 1:
-            raise ValueError("color_wgrad_step: p is not a parameter of this optimiser")
-        segs += self.segments(extra) if extra else []
-        if len(segs) > 1 + 3:
-            raise ValueError("color_wgrad_step: at most 3 extra segments")
-        key = ("color_wgrad",) + tuple(id(q) for _, q, _ in segs)
-        ticket = self._tickets.get(key)
-        if ticket is None:
-            if torch.cuda.is_current_stream_capturing():
-                raise RuntimeError("FusedAdam: first colour weight-gradient step inside graph capture; "
-                                   "run one eager step first")
-            ticket = self._tickets[key] = torch.zeros(1, dtype=torch.int32, device=self.device)
-        arr = (_lib.NslamAdamSeg * len(segs))(*[s for s, _, _ in segs])
-        b1, b2 = self.betas
-        st = stream if stream is not None else torch.cuda.current_stream(self.device)
-        rc = lib().nslam_color_wgrad_adam(ctypes.byref(cfg), n, ptr(ws), ws_bytes, arr, len(segs), b1, b2, self.eps,
-                                          int(bool(zero_grad)), ptr(ticket), st.cuda_stream)
-        check(rc, "nslam_color_wgrad_adam")
-
     def zero_grad(self, set_to_none=True):
         for g in self.param_groups:
             for p in g["params"]:

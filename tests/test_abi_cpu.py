@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_strerror(pkg):
     L = pkg._lib.lib()
-    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 15
+    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 16
     assert L.nslam_strerror(0) == b"ok"
     assert b"invalid" in L.nslam_strerror(-1)
 
@@ -140,59 +140,71 @@ def test_v8_cam_pose_validates_without_gpu(pkg):
     assert L.nslam_cam_pose(64, None, None) == -1
 
 
-def test_v10_bwd_decoders_validates_without_gpu(pkg):
-    """nslam_query_bwd_decoders rejects bad configs, masks and missing buffers before any launch."""
-    L = pkg._lib.lib()
+def _colour_cfg(pkg):
+    """A colour-stage config with fake (aligned, never dereferenced) device pointers: the entry points
+    below must reject or accept it from the arguments alone, before any launch."""
     cfg = pkg._lib.NslamQueryCfg()
-    cfg.stage = 7
-    gps = (ctypes.c_void_p * 4)()
-    assert L.nslam_query_bwd_decoders(ctypes.byref(cfg), 0b0110, None, 10, None, gps, None, 0, None) == -1  # stage
-    ok = pkg._lib.NslamQueryCfg()
-    rc = L.nslam_query_bwd_decoders(ctypes.byref(ok), 0, None, 0, None, gps, None, 0, None)
-    assert rc < 0  # an empty decoder mask (or an otherwise incomplete config) is never launched
-
-
-def test_v11_color_wgrad_validates_without_gpu(pkg):
-    """nslam_color_wgrad and NSLAM_BWD_DEFER_WGRAD reject configs without a colour weight-gradient
-    tape backward before any launch."""
-    L = pkg._lib.lib()
-    cfg = pkg._lib.NslamQueryCfg()
-    cfg.stage = 7
-    assert L.nslam_color_wgrad(ctypes.byref(cfg), 10, None, 0, None) == -1            # bad stage
-    cfg.stage = pkg._lib.STAGES["middle"]
-    assert L.nslam_color_wgrad(ctypes.byref(cfg), 10, None, 0, None) < 0              # not the colour stage
-    gps = (ctypes.c_void_p * 4)()
-    mask = (1 << pkg._lib.DEC_MIDDLE) | pkg._lib.BWD_DEFER_WGRAD                       # nothing to defer
-    assert L.nslam_query_bwd_decoders(ctypes.byref(cfg), mask, None, 0, None, gps, None, 0, None) < 0
-
-
-def test_v12_color_wgrad_adam_validates_without_gpu(pkg):
-    """nslam_color_wgrad_adam rejects a missing segment / ticket, a segment that is not the colour
-    decoder's gradient, and non-colour stages before any launch."""
-    L = pkg._lib.lib()
-    cfg = pkg._lib.NslamQueryCfg()
-    seg = pkg._lib.NslamAdamSeg()
-    cfg.stage = 7
-    assert L.nslam_color_wgrad_adam(ctypes.byref(cfg), 10, None, 0, ctypes.byref(seg), 1, 0.9, 0.999, 1e-8, 0, None,
-                                    None) == -1                                          # bad stage
-    cfg.stage = pkg._lib.STAGES["middle"]
-    assert L.nslam_color_wgrad_adam(ctypes.byref(cfg), 10, None, 0, ctypes.byref(seg), 1, 0.9, 0.999, 1e-8, 0, None,
-                                    None) < 0                                            # not the colour stage
     cfg.stage = pkg._lib.STAGES["color"]
-    assert L.nslam_color_wgrad_adam(ctypes.byref(cfg), 10, None, 0, None, 1, 0.9, 0.999, 1e-8, 0, None, None) < 0
-    assert L.nslam_color_wgrad_adam(ctypes.byref(cfg), 10, None, 0, ctypes.byref(seg), 5, 0.9, 0.999, 1e-8, 0, None,
-                                    None) < 0                                            # too many segments
+    for d in range(4):
+        cfg.grid[d].data = 4096
+        cfg.grid[d].dims[0] = cfg.grid[d].dims[1] = cfg.grid[d].dims[2] = 8
+        cfg.packed[d] = 4096
+    return cfg
 
 
-def test_v13_query_fwd_parts_validates_without_gpu(pkg):
-    """nslam_query_fwd_parts takes only the colour stage with deferred occupancy and the part masks
-    0b011 / 0b100 / 0b111, checked before any launch."""
+def test_v16_bwd_decoders_validates_without_gpu(pkg):
+    """nslam_query_bwd_decoders rejects bad configs, masks and parameter gradients before any launch."""
     L = pkg._lib.lib()
     cfg = pkg._lib.NslamQueryCfg()
     cfg.stage = 7
-    assert L.nslam_query_fwd_parts(ctypes.byref(cfg), None, 10, None, None, 0, 3, None) == -1    # bad stage
+    gps = (ctypes.c_void_p * 4)()
+    assert L.nslam_query_bwd_decoders(ctypes.byref(cfg), 0b0110, None, 10, None, gps, None) == -1  # stage
     ok = pkg._lib.NslamQueryCfg()
-    assert L.nslam_query_fwd_parts(ctypes.byref(ok), None, 10, None, None, 0, 3, None) < 0      # incomplete cfg
+    rc = L.nslam_query_bwd_decoders(ctypes.byref(ok), 0, None, 0, None, gps, None)
+    assert rc < 0  # an empty decoder mask (or an otherwise incomplete config) is never launched
+    c = _colour_cfg(pkg)
+    c.dgrad[pkg._lib.DEC_COLOR].base = 4096
+    c.dgrad[pkg._lib.DEC_COLOR].count = 100
+    colour = 1 << pkg._lib.DEC_COLOR
+    # no parameter gradients in the lean launch (v16: the colour decoder's come from nslam_color_wgrad)
+    assert L.nslam_query_bwd_decoders(ctypes.byref(c), colour, 4096, 10, 4096, gps, None) == -2
+    c.dgrad[pkg._lib.DEC_COLOR].base = None
+    assert L.nslam_query_bwd_decoders(ctypes.byref(c), colour, 4096, 10, 4096, gps, None) == -2  # no saved masks
+    assert L.nslam_query_bwd_decoders(ctypes.byref(c), 1 << pkg._lib.DEC_COARSE, 4096, 10, 4096, gps, None) == -1
+
+
+def test_v16_color_wgrad_validates_without_gpu(pkg):
+    """nslam_color_wgrad rejects configs without a colour weight-gradient tape backward, a missing
+    cotangent and a short workspace before any launch; an empty batch is a no-op."""
+    L = pkg._lib.lib()
+    cfg = pkg._lib.NslamQueryCfg()
+    cfg.stage = 7
+    assert L.nslam_color_wgrad(ctypes.byref(cfg), None, 10, None, None, 0, None) == -1            # bad stage
+    c = _colour_cfg(pkg)
+    c.stage = pkg._lib.STAGES["middle"]
+    assert L.nslam_color_wgrad(ctypes.byref(c), 4096, 10, 4096, 4096, 1 << 20, None) == -1        # not colour
+    c.stage = pkg._lib.STAGES["color"]
+    assert L.nslam_color_wgrad(ctypes.byref(c), 4096, 10, 4096, 4096, 1 << 20, None) == -2        # no dgrad
+    c.dgrad[pkg._lib.DEC_COLOR].base = 4096
+    c.dgrad[pkg._lib.DEC_COLOR].count = 15575
+    assert L.nslam_color_wgrad(ctypes.byref(c), 4096, 10, 4096, 4096, 1 << 20, None) == -2        # no tapes
+    c.act_tape = 4096
+    c.saved_masks = 4096
+    assert L.nslam_color_wgrad(ctypes.byref(c), 4096, 10, None, 4096, 1 << 20, None) == -1        # no g_raw
+    assert L.nslam_color_wgrad(ctypes.byref(c), None, 10, 4096, 4096, 1 << 20, None) == -1        # no points
+    need = L.nslam_query_bwd_decoder_workspace_size(ctypes.byref(c), pkg._lib.DEC_COLOR, 10)
+    assert need > 0
+    assert L.nslam_color_wgrad(ctypes.byref(c), 4096, 10, 4096, 4096, need - 1, None) == -3       # short ws
+    assert L.nslam_color_wgrad(ctypes.byref(c), 4096, 10, 4096, None, need, None) == -3           # no ws
+    assert L.nslam_color_wgrad(ctypes.byref(c), None, 0, None, None, 0, None) == 0                # empty batch
+
+
+def test_v16_removed_entry_points(pkg):
+    """ABI v16 dropped the options measured neutral or slower in round 3 (the fused colour Adam, the
+    part-wise forward of the pipelined loop): they are no longer exported."""
+    L = pkg._lib.lib()
+    for name in ("nslam_color_wgrad_adam", "nslam_query_fwd_parts"):
+        assert not hasattr(L, name), name
 
 
 def test_v15_cam_grad_parts_validates_without_gpu(pkg):

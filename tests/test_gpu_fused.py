@@ -8,6 +8,7 @@ and torch on the same inputs:
   nslam_adam_step    vs torch.optim.Adam(foreach=False) (dense, row-masked, per-parameter steps)
   MappingEngine      vs the autograd path (one iteration's gradients; loss decreases over 5)
 """
+import ctypes
 import importlib
 
 import numpy as np
@@ -322,95 +323,81 @@ def test_engine_per_branch_adam_matches_single_adam(tiny):
     assert sorted(out[True][2].values()) == sorted(out[False][2].values()) == [3.0] * 4
 
 
-def test_engine_fused_colour_adam_matches_separate_adam(tiny):
-    """ABI v12: the colour decoder's Adam step inside the weight-gradient slab reduction
-    (nslam_color_wgrad_adam, the colour grid's Adam forked beside it) == the separate reduction then
-    nslam_adam_step — bit for bit after one iteration (decoder parameters, Adam state, packed copy),
-    and the same map after three."""
+def test_engine_branch_order_and_concurrency_keep_the_map(tiny):
+    """ABI v16: the colour decoder's weight gradients (nslam_color_wgrad) run beside the lean backward
+    of every decoder.  Enqueued first or second, on concurrent streams or one: three iterations give
+    the same map, decoder, packed copy and Adam steps (grid atomics order aside)."""
     sc, frames = _frames(tiny)
     out = {}
-    for fuse in (True, False):
+    for variant in ("first", "second", "serial"):
         nice, c = _nice(sc)
         eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV)
-        eng.fuse_adam = fuse
+        eng.wgrad_first = variant != "second"
+        eng.concurrent = variant != "serial"
         opt = P.ops.FusedAdam([{"params": [eng.decs["color"].param], "lr": 0.005}] +
                               [{"params": [c[k]], "lr": 0.005} for k in ("grid_middle", "grid_fine", "grid_color")])
-        pix = torch.randint(96 * 128, (3 * 150,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(12))
-        snaps = []
-        for _ in range(3):
-            eng.iteration("color", frames, pix, 150, (96, 128), (sc.fx, sc.fy, sc.cx, sc.cy), opt)
-            torch.cuda.synchronize()
-            p = eng.decs["color"].param
-            st = opt.state[p]
-            snaps.append((p.detach().clone(), st["exp_avg"].clone(), st["exp_avg_sq"].clone(), float(st["step"]),
-                          eng.decs["color"].packed.clone(), eng.decs["color"].grad.clone(),
-                          {k: v.detach().clone() for k, v in c.items()}))
-        out[fuse] = snaps
-    a, b = out[True][0], out[False][0]
-    for i in range(5):
-        assert torch.equal(a[i], b[i]) if i != 3 else a[i] == b[i] == 1.0, i
-    # the reduced gradient is left in the buffer (no rows: the engine zeroes it with a memset next time)
-    assert torch.equal(a[5], b[5]) and float(a[5].abs().sum()) > 0
-    a, b = out[True][2], out[False][2]
-    assert a[3] == b[3] == 3.0
-    assert rel_l2(a[0], b[0]) < 1e-5
-    for k in a[6]:
-        assert rel_l2(a[6][k], b[6][k]) < 1e-5, k
-
-
-def test_query_fwd_parts_match_whole_forward(tiny):
-    """ABI v13: the colour stage's forward as its middle | fine half and its colour half (two
-    launches, the halves on separate streams) == nslam_query_fwd_ws with deferred occupancy, bit for
-    bit: raw, the middle occupancy, the saved ReLU masks and the colour activation tape."""
-    sc, frames = _frames(tiny)
-    nice, c = _nice(sc)
-    eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV)
-    pix = torch.randint(96 * 128, (3 * 150,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(3))
-    ro, rd, gd, gc, keep = P.ops.gather_rays(frames, pix, 150, 96, 128, (0, 96, 0, 128), sc.fx, sc.fy, sc.cx, sc.cy)
-    z = P.ops.sample_z(ro, rd, gd, sc.bound, 32, 16)
-    raw0 = eng.query_fwd("color", ro, rd, z, defer_occ=True, tape=True)
-    ref = (raw0.clone(), eng.occ_add.clone(), eng._saved.clone(), eng._tape.clone())
-    raw1 = eng._query_fwd_pipelined(ro, rd, z)
-    torch.cuda.synchronize()
-    got = (raw1, eng.occ_add, eng._saved, eng._tape)
-    tiles = (z.numel() + 31) // 32
-    for i, (a, b) in enumerate(zip(got, ref)):
-        if i == 2:  # masks [decoder][tile][layer][64] u16: the colour stage writes decoders 1..3 (no coarse)
-            a, b = (t.view(torch.int16).view(4, tiles, 5, 64)[1:] for t in (a, b))
-        assert torch.equal(a, b), i
-
-
-def test_engine_pipelined_matches_serial(tiny):
-    """Cross-iteration pipelining (the next iteration's middle | fine forward beside this one's
-    colour weight gradients and Adam) keeps every dependency of the serial loop: three iterations
-    give the same map, decoder and Adam steps (grid atomics order aside)."""
-    sc, frames = _frames(tiny)
-    out = {}
-    for pipe in (True, False):
-        nice, c = _nice(sc)
-        eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV)
-        eng.pipeline = pipe
-        opt = P.ops.FusedAdam([{"params": [eng.decs["color"].param], "lr": 0.005}] +
-                              [{"params": [c[k]], "lr": 0.005} for k in ("grid_middle", "grid_fine", "grid_color")])
-        losses = []
         for it in range(3):
             pix = torch.randint(96 * 128, (3 * 150,), device=DEV,
                                 generator=torch.Generator(device=DEV).manual_seed(20 + it))
-            loss, _ = eng.iteration("color", frames, pix, 150, (96, 128), (sc.fx, sc.fy, sc.cx, sc.cy), opt)
-            losses.append(loss.sum())
-        eng.join()
+            eng.iteration("color", frames, pix, 150, (96, 128), (sc.fx, sc.fy, sc.cx, sc.cy), opt)
         torch.cuda.synchronize()
-        out[pipe] = ({k: v.detach().clone() for k, v in c.items()}, eng.decs["color"].param.detach().clone(),
-                     eng.decs["color"].packed.clone(), [float(x) for x in losses],
-                     sorted(float(st["step"]) for st in opt.state.values()))
-    a, b = out[True], out[False]
-    for k in a[0]:
-        assert rel_l2(a[0][k], b[0][k]) < 1e-5, k
-    assert rel_l2(a[1], b[1]) < 1e-5 and rel_l2(a[2], b[2]) < 1e-5
-    assert abs(a[3][0] - b[3][0]) <= 1e-9 * abs(b[3][0])  # the first iteration's loss: same map, same rays
-    for x, y in zip(a[3][1:], b[3][1:]):
-        assert abs(x - y) <= 1e-4 * abs(y)
-    assert a[4] == b[4] == [3.0] * 4
+        out[variant] = ({k: v.detach().clone() for k, v in c.items()}, eng.decs["color"].param.detach().clone(),
+                        eng.decs["color"].packed.clone(), sorted(float(st["step"]) for st in opt.state.values()))
+    b = out["serial"]
+    for v in ("first", "second"):
+        a = out[v]
+        for k in a[0]:
+            assert rel_l2(a[0][k], b[0][k]) < 1e-5, (v, k)
+        assert rel_l2(a[1], b[1]) < 1e-5 and rel_l2(a[2], b[2]) < 1e-5, v
+        assert a[3] == b[3] == [3.0] * 4, v
+
+
+@pytest.mark.parametrize("n_rays", [150, 1000, 3333])
+def test_color_wgrad_matches_recompute_backward(tiny, n_rays):
+    """k_color_wgrad (the split-K weight gradients from the activation tape, ABI v16) vs the colour
+    decoder's recompute backward (k_dec_bwd with weight gradients: forward recomputed, LDS transposes,
+    per-tile slabs) on the same rays and cotangent, ELEMENTWISE over every colour-decoder parameter —
+    the two share no weight-gradient code.  Ragged batches (n not a multiple of 32), one and several
+    tiles per chunk (150 rays: 1 tile per chunk; 3333 rays x 48: 5 tiles per chunk)."""
+    sc, frames = _frames(tiny)
+    nice, c = _nice(sc)
+    eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV)
+    g = torch.Generator(device=DEV).manual_seed(30 + n_rays)
+    pix = torch.randint(96 * 128, (n_rays,), device=DEV, generator=g)
+    ro, rd, gd, gc, keep = P.ops.gather_rays(frames[:1], pix, n_rays, 96, 128, (0, 96, 0, 128), sc.fx, sc.fy, sc.cx,
+                                             sc.cy)
+    z = P.ops.sample_z(ro, rd, gd, sc.bound, 32, 16)
+    n = z.numel()
+    eng.query_fwd("color", ro, rd, z, tape=True)
+    g_raw = torch.randn(n, 4, device=DEV, generator=g)
+    cfg = eng._cfg("color", ro, rd, z, (), ("color",))
+    dgrad = eng.decs["color"].grad
+    res = {}
+    for path in ("tape", "recompute"):
+        dgrad.zero_()
+        cfg.act_tape = eng._tape.data_ptr() if path == "tape" else None
+        cfg.saved_masks = eng._saved.data_ptr() if path == "tape" else None
+        wsb = P._lib.lib().nslam_query_bwd_decoder_workspace_size(ctypes.byref(cfg), P._lib.DEC_COLOR, n)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=DEV)
+        if path == "tape":
+            rc = P._lib.lib().nslam_color_wgrad(ctypes.byref(cfg), None, n, g_raw.data_ptr(), ws.data_ptr(), wsb,
+                                                torch.cuda.current_stream().cuda_stream)
+        else:
+            rc = P._lib.lib().nslam_query_bwd_decoder(ctypes.byref(cfg), P._lib.DEC_COLOR, 0, None, n,
+                                                      g_raw.data_ptr(), None, ws.data_ptr(), wsb,
+                                                      torch.cuda.current_stream().cuda_stream)
+        assert rc == 0, (path, rc)
+        torch.cuda.synchronize()
+        res[path] = dgrad.clone()
+    a, b = res["tape"], res["recompute"]
+    assert float(b.abs().sum()) > 0
+    assert rel_l2(a, b) < 1e-5
+    # elementwise, on every parameter tensor (a mis-placed block would show as a large local error)
+    for name, t_a, t_b in zip(eng.decs["color"].packer.names, eng.decs["color"].packer.split_grad(a),
+                              eng.decs["color"].packer.split_grad(b)):
+        scale = float(t_b.abs().max()) + 1e-30
+        err = float((t_a - t_b).abs().max()) / scale
+        assert err < 1e-4, (name, err)
 
 
 def test_rows_pack_unpack_bitexact():
@@ -714,23 +701,23 @@ def test_cam_pose_kernel_matches_get_camera_from_tensor():
 
 
 @pytest.mark.gpu
-def test_merged_frozen_backward_matches_per_decoder_launches(tiny):
-    """ABI v10 nslam_query_bwd_decoders (the frozen decoders' mask-only backward as ONE launch) ==
-    one nslam_query_bwd_decoder launch per decoder: mapping grid gradients (float atomics: up to
-    summation order) and the tracking camera gradient (per-decoder d/dpts buffers: bit-exact)."""
+def test_merged_backward_matches_per_decoder_launches(tiny):
+    """ABI v10/v16: every decoder's mask-only backward as ONE launch beside the colour weight
+    gradients (nslam_query_bwd_decoders + nslam_color_wgrad, the engine's two branches) == one
+    nslam_query_bwd_decoder launch per decoder (the library running the colour tape backward's two
+    kernels in sequence): mapping grid gradients (float atomics: up to summation order), the colour
+    decoder's gradient (the same kernels: bit-exact) and the tracking camera gradient (per-decoder
+    d/dpts buffers: bit-exact)."""
     import copy
 
     sc, frames = _frames(tiny)
     keys = ("grid_middle", "grid_fine", "grid_color")
     pix = torch.randint(96 * 128, (3 * 150,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(21))
     out = {}
-    # "all": the colour weight-gradient backward joins the launch; "split": ABI v11, the colour lean
-    # chain first, then nslam_color_wgrad beside the frozen decoders' launch
-    for merge in (False, True, "all", "split"):
+    for merge in (False, True):
         nice, c = _nice(sc)
         eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV)
-        eng.merge_frozen = True if merge == "split" else merge
-        eng.split_wgrad = merge == "split"
+        eng.merge = merge
         opt = P.ops.FusedAdam([{"params": [eng.decs["color"].param], "lr": 0.0}] +
                               [{"params": [c[k]], "lr": 0.0} for k in keys])
         gr = {}
@@ -742,30 +729,27 @@ def test_merged_frozen_backward_matches_per_decoder_launches(tiny):
 
         eng.iteration("color", frames, pix, 150, (96, 128), (sc.fx, sc.fy, sc.cx, sc.cy), opt, exchange=snapshot)
         out[merge] = gr
-    for merge in (True, "all", "split"):
-        for k in keys:
-            assert float(out[False][k].abs().sum()) > 0, k
-            assert rel_l2(out[merge][k], out[False][k]) < 1e-6, (merge, k)
-        assert torch.equal(out[merge]["dec"], out[False]["dec"]), merge
+    for k in keys:
+        assert float(out[False][k].abs().sum()) > 0, k
+        assert rel_l2(out[True][k], out[False][k]) < 1e-6, k
+    assert torch.equal(out[True]["dec"], out[False]["dec"])
     # tracking: middle, fine and colour frozen, d/dpts per decoder
     scn = Scene(tiny)
     slam = scn.slam(base_cfg())
     cam0 = P.common.get_tensor_from_camera(scn.c2w).cuda()
     pixs = torch.randint(400, (200,), generator=torch.Generator().manual_seed(5))
     grads = {}
-    for merge in (False, True, "nosum"):  # "nosum": merged launch, per-decoder d/dpts buffers added in torch
+    for merge in (False, True):
         te = P.engine.TrackingEngine(copy.deepcopy(slam.shared_decoders), slam.shared_c, scn.bound, 32, 16,
                                      (scn.H, scn.W), (scn.fx, scn.fy, scn.cx, scn.cy), ignore_edge=(20, 20),
                                      w_color=0.5, handle_dynamic=True, use_color=True, device=DEV)
-        te.eng.merge_frozen = bool(merge)  # (the default, True, merges the frozen decoders)
-        te.eng.sum_pts = merge is True  # in-kernel sum of the decoders' d/dpts (NSLAM_BWD_SUM_PTS)
+        te.eng.merge = merge
         cam = cam0.clone().requires_grad_(True)
         opt = P.ops.FusedAdam([{"params": [cam], "lr": 0.0}])
         te.iteration(cam, scn.depth.cuda(), scn.color.cuda(), (pixs % te.n_window()).cuda(), opt)
         grads[merge] = cam.grad.detach().clone()
     assert float(grads[False].abs().sum()) > 0
     assert torch.equal(grads[True], grads[False])
-    assert torch.equal(grads["nosum"], grads[False])
 
 
 def test_engine_prefetch_discards_batch_of_other_frames(tiny):
@@ -782,11 +766,11 @@ def test_engine_prefetch_discards_batch_of_other_frames(tiny):
     for f, (_, _, m) in enumerate(moved):
         m[:3, 3] += 0.05 * (f + 1)
     eng.iteration("color", moved, *args, seed=11, prefetch=True)   # another window: fresh batch (set 0)
-    ro = eng._pre[1][0][0].view(len(moved), 150, 3)
+    ro = eng._pre[2][0][0].view(len(moved), 150, 3)
     for f, (_, _, m) in enumerate(moved):
         assert torch.equal(ro[f], m[:3, 3].expand(150, 3)), f
     with torch.no_grad():
         moved[0][2][:3, 3] += 0.01                                     # a pose updated in place
     eng.iteration("color", moved, *args, seed=11, prefetch=True)
-    ro = eng._pre[1][0][0].view(len(moved), 150, 3)
+    ro = eng._pre[2][0][0].view(len(moved), 150, 3)
     assert torch.equal(ro[0], moved[0][2][:3, 3].expand(150, 3))

@@ -26,7 +26,7 @@ def main():
     P = bench.pkg()
     scene = bench.Room0Scene(dev, 0, path="fused")
     scene.engine.concurrent = False
-    scene.engine.merge_frozen = False  # one kernel per decoder: wave index = tile in every phase slot
+    scene.engine.merge = False  # one kernel per decoder: wave index = tile in every phase slot
     for _ in range(4):
         scene.step()
     torch.cuda.synchronize()
