@@ -32,6 +32,9 @@ PREFETCH = True
 # iterations per captured hipGraph, whatever --steps is (a replay starts only after the previous one has
 # drained, ~20 us on MI355X: paid once per block), so runs of any length measure the same thing
 GRAPH_BLOCK = 10
+# gradient exchange of a ray-sharded run (N > 1): "sharded" (reduce-scatter, Adam on the rank's
+# shard, all-gather: distributed.ShardedAdamExchange) or "allreduce" (SparseGradExchange, replicated Adam)
+EXCHANGE = "sharded"
 
 ROOM0 = {
     "bound": [[-2.9, 8.9], [-3.2, 5.5], [-3.5, 3.3]], "bound_divisible": 0.32,
@@ -283,8 +286,14 @@ class Room0Scene:
                 ([{"params": [self.grids["grid_coarse"]], "lr": cfg["lr"]["middle"]}] if self.coarse else []) +
                 [{"params": [self.grids[k]], "lr": cfg["lr"][k[5:]], "rows": self.rows[k]}
                  for k in ("grid_middle", "grid_fine", "grid_color")])
-            # ray-sharded: all-reduce only the frustum rows Adam reads (+ colour-decoder grads)
-            self.exchange = P.distributed.SparseGradExchange(self.engine, self.rows)
+            # ray-sharded: exchange only the frustum rows Adam reads (+ colour-decoder grads) — by default
+            # reduce-scatter, Adam on this rank's shard, all-gather, per backward branch
+            # (distributed.ShardedAdamExchange); --exchange allreduce: one all-reduce, replicated Adam
+            world = int(os.environ.get("WORLD_SIZE", "1"))
+            if world > 1 and EXCHANGE == "sharded":
+                self.exchange = P.distributed.ShardedAdamExchange(self.engine, self.opt)
+            else:
+                self.exchange = P.distributed.SparseGradExchange(self.engine, self.rows)
         else:
             params = [{"params": list(self.nice.color_decoder.parameters()), "lr": cfg["lr"]["decoders"]},
                       {"params": [self.grids["grid_middle"]], "lr": cfg["lr"]["middle"]},
@@ -826,13 +835,16 @@ def main():
                     help="override mapping pixels per iteration (scaling studies; the metric uses room0's 1000)")
     ap.add_argument("--path", choices=("fused", "autograd"), default="fused",
                     help="fused engine (default) or the autograd drop-in path")
+    ap.add_argument("--exchange", choices=("sharded", "allreduce"), default="sharded",
+                    help="N>1 gradient exchange: sharded Adam (default) or all-reduce + replicated Adam")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="draw + sample each iteration's rays inside it (no overlap with the previous backward)")
     ap.add_argument("--leg", choices=("frames", "stress", "stress_iter", "bulk", "frame_io", "apartment"), default=None,
                     help="run one auxiliary measurement and print its JSON (bench.py spawns these itself)")
     args = ap.parse_args()
-    global PREFETCH
+    global PREFETCH, EXCHANGE
     PREFETCH = not args.no_prefetch
+    EXCHANGE = args.exchange
     if args.leg:
         return leg_main(args.leg)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -932,6 +944,7 @@ def main():
         if sharded and args.path == "fused":
             keys, dn = scene.engine.grads_for("color", ("color",))
             out["exchange_bytes_per_step"] = scene.exchange.payload_bytes(keys, dn)
+            out["exchange"] = EXCHANGE
             out["dense_grad_bytes_per_step"] = sum(v.numel() for v in scene.grids.values()) * 4
         # the auxiliary measurements run as child processes: a failure there (one run on a fresh
         # box ended in a host heap abort inside a later leg) cannot take the headline line with it

@@ -140,5 +140,171 @@ class SparseGradExchange:
             self.unpack(buf[off:off + g.numel()], None, None, g.reshape(-1))
 
 
+def _storage(t):
+    """A dense tensor's elements in storage order, as a view (a channels-last grid's [Z][Y][X][C])."""
+    if t.dim() == 5 and not t.is_contiguous():
+        return t.permute(0, 2, 3, 4, 1).reshape(-1)
+    return t.reshape(-1)
+
+
+class ShardedAdamExchange:
+    """The ray-sharded mapping iteration's gradient exchange with the optimiser step sharded across
+    ranks (ZeRO-1 style; SURVEY §8(e), Mapper.py:503-504 on the summed gradients):
+
+        reduce-scatter  the branch's compact gradient span (frustum rows of its grids, or a decoder's
+                        gradient): rank r receives the summed shard r            (in place)
+        Adam            on shard r only: this rank's slices of the row-masked grid segments / of the
+                        decoder (nslam_adam_step over explicit sub-segments; its Adam state is only
+                        ever touched there, the rest stays zero)
+        all-gather      the updated values of every shard (rows gathered from the grids, decoder
+                        parameters), then written back (nslam_rows_unpack)    (in place)
+
+    The bytes on the wire are an all-reduce's (a reduce-scatter plus an all-gather of the same span)
+    and each rank runs 1/N of the Adam work, which the replicated design ran N times.  It runs per
+    backward BRANCH (engine.MappingEngine.iteration calls branch() on the branch's stream right after
+    it): the grids' exchange starts when the lean backward launch completes, while the colour decoder's
+    weight gradients are still running; the decoder's exchange follows them on their own stream, over a
+    second process group (two communicators: collectives from two streams never share one).
+
+    The engine's compact gradients are padded to whole shards (engine.set_rows(pad_rows=world)); the
+    exchange zeroes every gradient entry it consumed, so the next iteration needs no memset.
+    pack / unpack / adam_slices default to the HIP entry points and are injectable for CPU tests."""
+
+    leaves_clean = True
+
+    def __init__(self, engine, optimizer, group=None, group_dec=None, pack=None, unpack=None, adam_slices=None):
+        from . import ops
+        self.engine, self.opt, self.group = engine, optimizer, group
+        init = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if init else 1
+        self.rank = dist.get_rank(group) if init else 0
+        if group_dec is None and self.world > 1:
+            group_dec = dist.new_group(dist.get_process_group_ranks(group) if group is not None else None)
+        self.group_dec = group_dec
+        self.pack = pack or ops.rows_pack
+        self.unpack = unpack or ops.rows_unpack
+        self.adam_slices = adam_slices or self._adam_hip
+        if engine.pad_rows != self.world:
+            engine.set_rows(engine.rows, pad_rows=self.world)
+        self._plans = {}
+
+    # -- layout ---------------------------------------------------------------------------------
+    def _span(self, pieces):
+        """The contiguous view over `pieces` (tensors adjacent in the engine's flat buffer, in order)."""
+        for a, b in zip(pieces, pieces[1:]):
+            if a.data_ptr() + a.numel() * 4 != b.data_ptr():
+                raise ValueError("ShardedAdamExchange: the branch's gradients are not one contiguous span")
+        return pieces[0].as_strided((sum(p.numel() for p in pieces),), (1,))
+
+    def _plan(self, gkeys, dnames):
+        """(gradient span, value buffer, [(param, rows or None, n valid, offset in span, decoder)], chunk)
+        over the grids `gkeys` then the decoders `dnames` (adjacent in the engine's flat buffer)."""
+        key = (gkeys, dnames)
+        if key not in self._plans:
+            eng = self.engine
+            pieces = [eng.ggrad_pad[k] for k in gkeys] + [eng.dgrad_pad[n] for n in dnames]
+            segs = [(eng.c[k], eng.rows.get(k), eng.ggrad[k].numel(), None) for k in gkeys]
+            segs += [(eng.decs[n].param, None, eng.decs[n].param.numel(), n) for n in dnames]
+            span = self._span(pieces)
+            if span.numel() % (self.world * 32):
+                raise ValueError("ShardedAdamExchange: span not padded to whole shards")
+            chunk = span.numel() // self.world
+            vals = torch.empty_like(span)
+            off, placed = 0, []
+            for (p, rows, n, dec), piece in zip(segs, pieces):
+                placed.append((p, rows, n, off, dec))
+                off += piece.numel()
+            self._plans[key] = (span, vals, placed, chunk)
+        return self._plans[key]
+
+    # -- collectives (gloo has no in-place reduce-scatter of device tensors: all-reduce, same shard) --
+    def _reduce_scatter(self, span, chunk, group):
+        own = span[self.rank * chunk:(self.rank + 1) * chunk]
+        if self.world == 1:
+            return own
+        if dist.get_backend(group) == "gloo":
+            dist.all_reduce(span, group=group)
+        else:
+            dist.reduce_scatter_tensor(own, span, group=group)
+        return own
+
+    def _all_gather(self, vals, chunk, group):
+        if self.world == 1:
+            return
+        own = vals[self.rank * chunk:(self.rank + 1) * chunk]
+        if dist.get_backend(group) == "gloo":
+            parts = list(vals.split(chunk))
+            dist.all_gather(parts, own.clone(), group=group)
+        else:
+            dist.all_gather_into_tensor(vals, own, group=group)
+
+    # -- one branch -----------------------------------------------------------------------------
+    def branch(self, names, part, keys, dnames):
+        """One backward branch's exchange + sharded Adam (engine.MappingEngine.query_bwd's on_branch):
+        part "grids" (the lean launch: its grids, over `group`) or "all" (the weight-gradient branch:
+        the colour grid and decoder, one span, over `group_dec`)."""
+        if part not in ("grids", "all"):
+            raise ValueError("ShardedAdamExchange: every weight-gradient decoder must have the tape path "
+                             "(its grids in the lean launch, its parameters in nslam_color_wgrad)")
+        gk = tuple(k for k in ("grid_" + n for n in names) if k in keys)
+        dk = tuple(n for n in names if n in dnames) if part == "all" else ()
+        if not gk and not dk:
+            return
+        group = self.group if part == "grids" else self.group_dec
+        span, vals, placed, chunk = self._plan(gk, dk)
+        own0, own1 = self.rank * chunk, (self.rank + 1) * chunk
+        self._reduce_scatter(span, chunk, group)
+        # Adam on this rank's shard: the sub-segment of every piece that overlaps [own0, own1)
+        slices = []
+        for p, rows, n, off, dec in placed:
+            a, b = max(own0, off), min(own1, off + n)  # (the piece's padding is never stepped)
+            if a < b:
+                slices.append((p, rows, a - off, b - off, a))
+        self.adam_slices(slices, span, ("sharded",) + gk + dk)
+        span.zero_()  # every entry consumed (the next iteration accumulates into zeros)
+        # the shard's updated values, all-gathered, written back on every rank
+        for p, rows, a0, b0, a in slices:
+            if rows is not None:
+                self.pack(_storage(p.data), rows[a0 // 32:b0 // 32], None, vals[a:a + (b0 - a0)])
+            else:
+                vals[a:a + (b0 - a0)].copy_(_storage(p.data)[a0:b0])
+        self._all_gather(vals, chunk, group)
+        for p, rows, n, off, dec in placed:
+            if rows is not None:
+                self.unpack(vals[off:off + n], rows, _storage(p.data), None)
+            else:
+                _storage(p.data).copy_(vals[off:off + n])
+                if dec is not None:
+                    self.engine.decs[dec].repack()  # the MFMA-packed copy of the updated decoder
+
+    def _adam_hip(self, slices, span, key):
+        """nslam_adam_step over this rank's slices: a row-masked grid segment takes whole rows a0/32 ..
+        b0/32 of its row list (compact gradient in the span, its compact Adam state from a0); a dense
+        one (a decoder, or a dense channels-last grid) elements a0 .. b0 of its storage."""
+        from . import _lib
+        from ._lib import ptr
+        segs = []
+        for p, rows, a0, b0, a in slices:
+            ex, ex2, step = self.opt.state_of(p)
+            s = _lib.NslamAdamSeg()
+            s.grad = ptr(span) + a * 4
+            s.exp_avg, s.exp_avg_sq, s.step = ptr(ex) + a0 * 4, ptr(ex2) + a0 * 4, ptr(step)
+            s.lr = float(self.opt.group_of(p)["lr"])
+            if rows is not None:
+                s.param, s.rows, s.n, s.row_len, s.grad_rows = ptr(p.data), ptr(rows) + (a0 // 32) * 4, (b0 - a0) // 32, 32, 1
+            else:
+                s.param, s.rows, s.n, s.row_len = ptr(p.data) + a0 * 4, None, b0 - a0, 0
+            segs.append(s)
+        self.opt.step_segments(segs, key)
+
+    def payload_bytes(self, keys, dnames):
+        """Bytes each rank sends + receives per iteration ~ 2 (N-1)/N of these (reduce-scatter and
+        all-gather of the padded spans)."""
+        eng = self.engine
+        g = sum(eng.ggrad_pad[k].numel() for k in keys if k in eng.ggrad_pad)
+        d = sum(eng.dgrad_pad[n].numel() for n in dnames)
+        return (g + d) * 4
+
+
 def optimizer_params(opt):
     return [p for grp in opt.param_groups for p in grp["params"]]

@@ -106,41 +106,52 @@ class MappingEngine:
         # every mask-only decoder backward as ONE launch (ABI v10); False: one nslam_query_bwd_decoder
         # launch per decoder (the library then runs a colour tape backward's two kernels in sequence)
         self.merge = True
+        self._lean_ev = None
         for k, v in c.items():
             if not v.is_contiguous(memory_format=torch.channels_last_3d):
                 raise ValueError(f"{k} must be channels-last (ops.channels_last)")
         self.grid_grads = grid_grads
         self.set_rows(rows)
 
-    def set_rows(self, rows):
+    def set_rows(self, rows, pad_rows=1):
         """Grid-gradient layout.  rows=None: dense gradients (one flat buffer for every grid, so
         zeroing is a single memset).  rows={grid key: int32 voxel rows} (the frustum selection of
         Mapper.py:314-333, the FusedAdam group "rows"): those grids accumulate a COMPACT gradient
         [n_rows][32] in row-list order through a voxel→slot map (ABI v6 nslam_grid.slot); the
         scatter skips every other voxel, whose gradient the reference never forms (it optimises
         the masked vector, Mapper.py:394-401).  Adam then reads the compact rows directly and the
-        ray-sharded exchange all-reduces them as they are."""
+        ray-sharded exchange sums them as they are.
+        pad_rows: every compact grid's rows and every decoder's gradient are padded (with entries
+        nothing writes) to a multiple of pad_rows rows / elements, so a stage's gradient span splits
+        into equal whole-row shards (distributed.ShardedAdamExchange: pad_rows = world size)."""
         c = self.c
+        pad = max(1, int(pad_rows))
+        rup = lambda n: -(-n // pad) * pad  # noqa: E731
+        drup = lambda n: -(-n // (32 * pad)) * 32 * pad  # noqa: E731  (decoders: whole rows per shard too)
         self.rows = dict(rows) if rows else {}
+        self.pad_rows = pad
         self.slot = {}
         sizes = {}
         for k, v in c.items():
-            sizes[k] = 0 if not self.grid_grads else (self.rows[k].numel() * 32 if k in self.rows else v.numel())
+            n = self.rows[k].numel() if k in self.rows else v.numel() // 32  # rows (voxels)
+            sizes[k] = 0 if not self.grid_grads else rup(n) * 32
         # one flat gradient buffer: the grids (c order), then the decoders' gradients (colour first, so
         # the colour stage's whole exchange payload — middle/fine/colour rows + colour decoder — is
         # one contiguous span of it: all-reduced in place, distributed.SparseGradExchange)
         dorder = [n for n in ("color", "fine", "middle", "coarse") if n in self.decs]
         gsum = sum(sizes.values())
-        self.gall = torch.zeros(gsum + sum(self.decs[n].param.numel() for n in dorder), dtype=torch.float32,
+        self.gall = torch.zeros(gsum + sum(drup(self.decs[n].param.numel()) for n in dorder), dtype=torch.float32,
                                 device=self.device)
         self.gbuf = self.gall[:gsum]
         off = gsum
+        self.dgrad_pad = {}  # decoder -> its gradient with the padding
         for n in dorder:
             k = self.decs[n].param.numel()
             self.decs[n].grad = self.gall[off:off + k]
-            off += k
+            self.dgrad_pad[n] = self.gall[off:off + drup(k)]
+            off += drup(k)
         self._clean = False  # every gradient the next iteration accumulates into is known zero
-        self.ggrad, off = {}, 0
+        self.ggrad, self.ggrad_pad, off = {}, {}, 0  # ggrad_pad: flat, with the padding
         for k, v in c.items():
             if not self.grid_grads:  # tracking: grids are constants (Tracker.py:138-141)
                 continue
@@ -150,9 +161,10 @@ class MappingEngine:
                 slot = torch.full((Z * Y * X,), -1, dtype=torch.int32, device=self.device)
                 slot[r.long()] = torch.arange(r.numel(), dtype=torch.int32, device=self.device)
                 self.slot[k] = slot
-                self.ggrad[k] = self.gbuf[off:off + sizes[k]].view(-1, 32)
+                self.ggrad[k] = self.gbuf[off:off + r.numel() * 32].view(-1, 32)
             else:
-                self.ggrad[k] = self.gbuf[off:off + sizes[k]].view(1, Z, Y, X, 32).permute(0, 4, 1, 2, 3)
+                self.ggrad[k] = self.gbuf[off:off + v.numel()].view(1, Z, Y, X, 32).permute(0, 4, 1, 2, 3)
+            self.ggrad_pad[k] = self.gbuf[off:off + sizes[k]]
             off += sizes[k]
 
     # -- query in ray form ---------------------------------------------------------------------
@@ -202,9 +214,11 @@ class MappingEngine:
         pts_grad: also return d loss / d pts [N*S, 3] float64 (tracking, bundle adjustment): every
         decoder writes its share into its own buffer and the shares are summed afterwards (or returned
         as a list with pts_parts).
-        on_branch(names, part): called on each branch's stream right after it ("grids": the grids of
-        the decoders the lean launch covered; "decoders": a decoder's parameters) — the per-branch Adam
-        of the mapping iteration (a grid's rows, or a decoder, depend on that branch alone)."""
+        on_branch(names, part): called on a branch's stream once what it updates is complete — "grids":
+        the grids of the lean launch's decoders but the colour one; "all": the colour grid and the
+        colour decoder, on the weight-gradient branch after it AND the lean launch (k_color_wgrad reads
+        the colour grid: it is not rewritten before that kernel is done); "unit": a per-decoder launch's
+        grid and parameters — the per-branch Adam of the mapping iteration."""
         n = z.numel()
         self._clean = False
         concurrent = self.concurrent if concurrent is None else concurrent
@@ -226,6 +240,8 @@ class MappingEngine:
         units += [("one", [d]) for d in others]
         if not self.wgrad_first:
             units.sort(key=lambda u: u[0] == "wgrad")
+        has_wgrad = any(u[0] == "wgrad" for u in units)
+        wgrad_st = None
         main = torch.cuda.current_stream(z.device)
         par = concurrent and len(units) > 1
         streams = [main]
@@ -250,8 +266,7 @@ class MappingEngine:
                             rc = lib().nslam_color_wgrad(ctypes.byref(cfg), None, n, ptr(g_raw), ptr(ws), wsb,
                                                          st.cuda_stream)
                         check(rc, "nslam_color_wgrad")
-                        if on_branch is not None:
-                            on_branch(names, part="decoders")
+                        wgrad_st = st  # (its update waits for the lean launch: see below)
                     elif kind == "lean":
                         lc = _lib.NslamQueryCfg.from_buffer_copy(cfg)  # grids (and d/dpts) only
                         gps = (ctypes.c_void_p * 4)()
@@ -266,8 +281,16 @@ class MappingEngine:
                             rc = lib().nslam_query_bwd_decoders(ctypes.byref(lc), mask, None, n, ptr(g_raw), gps,
                                                                 st.cuda_stream)
                         check(rc, "nslam_query_bwd_decoders")
+                        if has_wgrad:
+                            if self._lean_ev is None:  # one persistent event (never destroyed mid-capture)
+                                self._lean_ev = torch.cuda.Event()
+                            self._lean_ev.record(st)
                         if on_branch is not None:
-                            on_branch(names, part="grids")
+                            # the grids of this launch — but the colour grid, which k_color_wgrad reads (its
+                            # colour feature) and which is updated on that branch once both are done
+                            own = [d for d in names if not (d == "color" and has_wgrad)]
+                            if own:
+                                on_branch(own, part="grids")
                     else:
                         name = names[0]
                         d = ops._DEC_ID[name]
@@ -279,10 +302,17 @@ class MappingEngine:
                                                                st.cuda_stream)
                         check(rc, "nslam_query_bwd_decoder")
                         if on_branch is not None:
-                            on_branch(names)
+                            on_branch(names, part="unit")
                 if pts_grad and st is not main:
                     for name in names:
                         gp[name].record_stream(st)
+            if has_wgrad and on_branch is not None:
+                # the colour grid and the colour decoder, on the weight-gradient branch after its kernel
+                # and after the lean launch (the colour grid's gradient; and no Adam may rewrite the grid
+                # while k_color_wgrad still gathers from it)
+                with torch.cuda.stream(wgrad_st):
+                    wgrad_st.wait_event(self._lean_ev)
+                    on_branch(["color"], part="all")
             for st in used:
                 main.wait_stream(st)
         if not pts_grad:
@@ -303,6 +333,7 @@ class MappingEngine:
         return keys, tuple(n for n in decs if n in trainable_decoders)
 
     def adam_grads(self, stage, trainable_decoders):
+        """{parameter: its gradient buffer} of the stage (compact grids: [n_rows, 32], no padding)."""
         keys, dnames = self.grads_for(stage, trainable_decoders)
         g = {self.c[k]: self.ggrad[k] for k in keys}
         g.update({self.decs[n].param: self.decs[n].grad for n in dnames})
@@ -403,10 +434,17 @@ class MappingEngine:
                     optimizer.set_mirror(d.param, d.mirror_idx, d.packed)
         grads = self.adam_grads(stage, trainable_decoders)
         on_branch = None
-        if exchange is None and allreduce is None and mirror:
-            # one rank: each backward branch updates what it alone completes on its own stream — the
-            # lean launch its decoders' grid rows, the weight-gradient branch the colour decoder — so
-            # no branch waits for the others before its Adam
+        sharded = exchange is not None and hasattr(exchange, "branch")
+        if sharded:
+            # ZeRO-style exchange (distributed.ShardedAdamExchange): each backward branch's gradients are
+            # reduce-scattered, this rank's shard stepped by Adam and the updated values all-gathered,
+            # on that branch's stream as soon as it finishes — the exchange does the optimiser step
+            def on_branch(names, part=None):
+                exchange.branch(names, part, keys, dnames)
+        elif exchange is None and allreduce is None and mirror:
+            # one rank: each backward branch updates what it completes on its own stream — the lean
+            # launch the middle / fine grid rows, the weight-gradient branch (once the lean launch is
+            # done too) the colour grid and the colour decoder — so no Adam waits for the whole backward
             def on_branch(names, part=None):  # the decoders of one launch: one Adam call for their grids
                 sub = {}                         # (part "grids" / "decoders": only those)
                 for name in names:
@@ -418,7 +456,9 @@ class MappingEngine:
                     optimizer.step(grads=sub, zero_grad=clean)
 
         self.query_bwd(stage, ro, rd, z, g_raw, keys, dnames, on_branch=on_branch)
-        if exchange is not None:  # frustum-compacted all-reduce (distributed.SparseGradExchange)
+        if sharded:
+            pass
+        elif exchange is not None:  # frustum-compacted all-reduce (distributed.SparseGradExchange)
             exchange(keys, dnames)
         elif allreduce is not None:  # the grid gradients as one flat buffer, plus the decoder gradients
             allreduce([self.gbuf] + [self.decs[n].grad for n in dnames])
@@ -426,7 +466,7 @@ class MappingEngine:
             main.wait_stream(side)
         if on_branch is None:
             optimizer.step(grads=grads, zero_grad=clean)
-        self._clean = clean
+        self._clean = clean and (not sharded or exchange.leaves_clean)
         if not mirror:
             for n in dnames:
                 self.decs[n].repack()

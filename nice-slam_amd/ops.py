@@ -825,6 +825,41 @@ class FusedAdam:
                                        stream_ptr(self.device))
         check(rc, "nslam_adam_step")
 
+    def group_of(self, p):
+        """The parameter group holding p."""
+        for g in self.param_groups:
+            if any(q is p for q in g["params"]):
+                return g
+        raise KeyError("not a parameter of this optimiser")
+
+    def state_of(self, p):
+        """(exp_avg, exp_avg_sq, step) of p, created on first use (dense, or [n_rows * row_len] for a
+        row-masked group, as step() keeps them)."""
+        st = self._st(p, self.group_of(p).get("rows"))
+        return st["exp_avg"], st["exp_avg_sq"], st["step"]
+
+    @torch.no_grad()
+    def step_segments(self, segs, key, zero_grad=False):
+        """nslam_adam_step over explicit segments (NslamAdamSeg structs built by the caller — e.g. one
+        rank's slices of the parameters, distributed.ShardedAdamExchange), with this optimiser's
+        betas / eps and a ticket of its own per `key`.  A parameter's step count must appear in at
+        most one segment of the call."""
+        if not segs:
+            return
+        if len(segs) > _lib.ADAM_MAX_SEGS:
+            raise ValueError(f"at most {_lib.ADAM_MAX_SEGS} segments per step")
+        ticket = self._tickets.get(key)
+        if ticket is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("FusedAdam: first step of a segment set inside graph capture; run one eager step")
+            ticket = self._tickets[key] = torch.zeros(1, dtype=torch.int32, device=self.device)
+        arr = (_lib.NslamAdamSeg * len(segs))(*segs)
+        b1, b2 = self.betas
+        with _span("adam"):
+            rc = lib().nslam_adam_step(arr, len(segs), b1, b2, self.eps, int(bool(zero_grad)), ptr(ticket),
+                                       stream_ptr(self.device))
+        check(rc, "nslam_adam_step")
+
     def zero_grad(self, set_to_none=True):
         for g in self.param_groups:
             for p in g["params"]:

@@ -4,9 +4,11 @@ Two gloo ranks (processes made by mp.spawn: fresh interpreters, no exec of a GPU
 the one GPU of the box.  Each runs 3 colour-stage MappingEngine iterations with in-kernel pixel
 draws sliced from a global batch (PixelDraws world=2: same seed, rank r gathers its slots and the
 global batch's max(gt_depth) — Renderer.py:107-111,144), frustum-compacted gradients and the
-SparseGradExchange all-reduce before a replicated Adam.  Checks:
+SparseGradExchange all-reduce before a replicated Adam — or (ABI v16 round) the ShardedAdamExchange:
+reduce-scatter, Adam on the rank's own slices of the frustum rows / colour decoder, all-gather of the
+updated values, per backward branch.  Checks:
   * both ranks end with bit-identical maps (grids and colour decoder): replicated Adam on the
-    same summed gradients;
+    same summed gradients, or every rank's slices all-gathered;
   * those maps equal a world = 1 run of the same engine on the whole global batch (float-atomic
     summation order aside) — Mapper.py:503-504 on the full batch.
 """
@@ -34,7 +36,7 @@ def _free_port():
     return p
 
 
-def _run(world, rank, group=None):
+def _run(world, rank, group=None, mode="allreduce"):
     """The mapping loop of one rank on cuda:0; returns CPU copies of the final map."""
     import importlib
     sys.path.insert(0, REPO)
@@ -67,7 +69,12 @@ def _run(world, rank, group=None):
     opt = P.ops.FusedAdam([{"params": [eng.decs["color"].param], "lr": 0.005}] +
                           [{"params": [c[k]], "lr": 0.005, "rows": rows[k]} for k in c])
     dec0 = eng.decs["color"].param.detach().cpu().clone()
-    ex = P.distributed.SparseGradExchange(eng, rows, group=group) if world > 1 else None
+    if world == 1:
+        ex = None
+    elif mode == "sharded":
+        ex = P.distributed.ShardedAdamExchange(eng, opt, group=group)
+    else:
+        ex = P.distributed.SparseGradExchange(eng, rows, group=group)
     losses = []
     for _ in range(ITERS):
         rl, _ = eng.iteration("color", frames, None, N_PER * (2 // world), (cam["H"], cam["W"]),
@@ -81,27 +88,28 @@ def _run(world, rank, group=None):
     return out
 
 
-def _worker(rank, world, port, path):
+def _worker(rank, world, port, path, mode):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        res = _run(world, rank)
+        res = _run(world, rank, mode=mode)
         torch.save(res, os.path.join(path, f"rank{rank}.pt"))
         dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
-def test_two_rank_sharded_engine_matches_single_rank(tmp_path):
+@pytest.mark.parametrize("mode", ["allreduce", "sharded"])
+def test_two_rank_sharded_engine_matches_single_rank(tmp_path, mode):
     port = _free_port()
-    mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, port, str(tmp_path), mode), nprocs=2, join=True)
     r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
     r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
     for k in r0:
         if k != "losses":
-            assert torch.equal(r0[k], r1[k]), k   # replicated Adam on identical all-reduced gradients
+            assert torch.equal(r0[k], r1[k]), k   # identical summed gradients / all-gathered updates
     full = _run(1, 0)
     with np.load(os.path.join(GOLDEN, "tiny_scene.npz")) as z:
         start = {k: torch.from_numpy(z[k]) for k in ("grid_middle", "grid_fine", "grid_color")}
