@@ -738,6 +738,8 @@ def apartment_iterations(dev, reps=50):
         out["ray_samples_per_s"]["map_" + stage] = int(scene.kept) * spr / (ms * 1e-3)
     out["launch_mode"] = mode
     out["grids"] = {k: list(v.shape) for k, v in scene.grids.items()}
+    # the frustum rows Adam reads = the per-iteration exchange payload of a ray-sharded job
+    out["frustum_rows"] = {k: int(v.numel()) for k, v in scene.rows.items()}
     out["workload"] = ("configs[3] Apartment, 1 GPU: 5000 pixels (5 frames x 1000) per iteration; coarse 32 samples "
                        "(no gt), middle/fine/colour 48 samples, frustum-masked Adam (coarse grid dense)")
     del scene

@@ -219,20 +219,6 @@ __device__ __forceinline__ void pin16(f32x16& v) {
                "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15]));
 }
 
-// A weight fragment (16 floats per lane, nslam_dev.h) held in registers, so the next GEMM's fragment
-// can be in flight while the current GEMM runs
-struct Frag {
-  f32x4 q[4];
-};
-__device__ __forceinline__ Frag load_frag(const float* __restrict__ frag, int lane) {
-  const gptr_t<f32x4> f = as_global(reinterpret_cast<const f32x4*>(frag)) + lane * 4;
-  return Frag{{f[0], f[1], f[2], f[3]}};
-}
-__device__ __forceinline__ void gemm_frag(f32x16& acc, const Frag& f, const f32x16& x) {
-#pragma unroll
-  for (int s = 0; s < 16; ++s) acc = mfma32(f.q[s >> 2][s & 3], x[s], acc);
-}
-
 // Wave 7, the cotangent chain of tile t into buf: the ReLU masks, the g half of the x | g table and
 // dh4..dh0 of xyz_backward_saved (the colour decoder's outputs 0-2, decoder.py:198-203; the 4th row is
 // the stage combiner's, decoder.py:341) without its feature-gradient GEMMs.  Each GEMM's weight

@@ -142,6 +142,39 @@ __device__ __forceinline__ void gemm_acc(f32x16& acc, const float* __restrict__ 
   acc = mfma32(a3[3], x[15], acc);
 }
 
+// A weight fragment (16 floats per lane) held in registers, so a GEMM's fragment can be in flight
+// while the previous GEMM runs
+struct Frag {
+  f32x4 q[4];
+};
+__device__ __forceinline__ Frag load_frag(const float* __restrict__ frag, int lane) {
+  const gptr_t<f32x4> f = as_global(reinterpret_cast<const f32x4*>(frag)) + lane * 4;
+  return Frag{{f[0], f[1], f[2], f[3]}};
+}
+// acc += W X from a loaded fragment (gemm_acc's MFMA chain)
+__device__ __forceinline__ void gemm_frag(f32x16& acc, const Frag& f, const f32x16& x) {
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc = mfma32(f.q[s >> 2][s & 3], x[s], acc);
+}
+// A fixed sequence of GEMMs over one decoder's packed fragments with each fragment loaded one GEMM
+// ahead: gemm(acc, x, next) runs acc += W_cur X while the fragment of block `next` (< 0: none) loads.
+// The fence after the load keeps the compiler from sinking it to its use (the MFMAs of the current
+// GEMM wait only for the current fragment: vmcnt counts in order, the younger load stays in flight).
+struct FragPipe {
+  const float* pk;
+  int lane;
+  Frag cur;
+  __device__ __forceinline__ FragPipe(const float* pk_, int first, int lane_)
+      : pk(pk_), lane(lane_), cur(load_frag(pk_ + first * NSLAM_FRAG, lane_)) {}
+  __device__ __forceinline__ void gemm(f32x16& acc, const f32x16& x, int next) {
+    Frag n = cur;
+    if (next >= 0) n = load_frag(pk + next * NSLAM_FRAG, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    gemm_frag(acc, cur, x);
+    cur = n;
+  }
+};
+
 // feature-tile view of a natural [32] vector: v[F(r,h)]
 __device__ __forceinline__ f32x16 vec_tile(const float* __restrict__ v, int lane) {
   const int h = lane >> 5;

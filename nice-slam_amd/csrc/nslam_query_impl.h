@@ -327,6 +327,55 @@ __device__ __forceinline__ f32x16 xyz_forward(const float* __restrict__ pk, cons
 #undef PHF_
 }
 
+// xyz_forward of the decoder-parallel forward (VLDS: the vector section in LDS), its 15 (NC = 1) or 20
+// (NC = 2) GEMMs as a FragPipe: each weight fragment is loaded while the previous GEMM runs, so no GEMM
+// waits for its fragment's L2 round trip.  The same products in the same order as xyz_forward.
+template <int NC, bool TAPE>
+__device__ __forceinline__ f32x16 xyz_forward_pf(const float* __restrict__ pk, const f32x16 (&cin)[NC],
+                                                 const float x[3], int lane, uint32_t m[5],
+                                                 float* __restrict__ tape, const float* vs) {
+  const XyzPack L{NC};
+  FragPipe fp(pk, L.L0(), lane);
+  f32x16 a = vec_tile(vs + (L.Bias(0) - L.V()), lane);
+  f32x16 a3 = vec_tile(vs + (L.Bias(3) - L.V()), lane);
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    const f32x16 e = emb_tile<false, false>(vs + (L.FB() - L.V()), x, b, lane);
+    fp.gemm(a, e, L.L3() + b);
+    fp.gemm(a3, e, b < 2 ? L.L0() + b + 1 : L.FC(0, 0));
+  }
+  // fc_c.i (cin) with the next layer's first fragment after it
+  auto fc = [&](int i, int next) {
+    f32x16 z = vec_tile(vs + (L.BiasC(i) - L.V()), lane);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) fp.gemm(z, cin[c], c + 1 < NC ? L.FC(i, c + 1) : next);
+    return z;
+  };
+  m[0] = mask16(a);
+  f32x16 h = relu16(a) + fc(0, L.L1());
+  if (TAPE) tape_store(tape, 0, h, lane);
+  a = vec_tile(vs + (L.Bias(1) - L.V()), lane);
+  fp.gemm(a, h, L.FC(1, 0));
+  m[1] = mask16(a);
+  h = relu16(a) + fc(1, L.L2());
+  if (TAPE) tape_store(tape, 1, h, lane);
+  a = vec_tile(vs + (L.Bias(2) - L.V()), lane);
+  fp.gemm(a, h, L.FC(2, 0));
+  m[2] = mask16(a);
+  h = relu16(a) + fc(2, L.L3() + 3);
+  if (TAPE) tape_store(tape, 2, h, lane);
+  fp.gemm(a3, h, L.FC(3, 0));
+  m[3] = mask16(a3);
+  h = relu16(a3) + fc(3, L.L4());
+  if (TAPE) tape_store(tape, 3, h, lane);
+  a = vec_tile(vs + (L.Bias(4) - L.V()), lane);
+  fp.gemm(a, h, L.FC(4, 0));
+  m[4] = mask16(a);
+  h = relu16(a) + fc(4, -1);
+  if (TAPE) tape_store(tape, 4, h, lane);
+  return h;
+}
+
 // output_linear row j: sum_f Wo[j][f] h4[f] + bo[j]  (complete in both halves)
 __device__ __forceinline__ float out_row(const float* __restrict__ Wo, const float* __restrict__ bo, int j,
                                          const f32x16& h4, int lane) {
@@ -1092,6 +1141,9 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd(QueryKArgs a) {
 // and k_occ_combine then forms raw[p][3] = fine_occ + middle_occ (decoder.py:331-334, the
 // reference's operand order) — exactly 100 outside the bound (0 + 100; Renderer.py:57).
 // One decoder of the decoder-parallel forward for this wave's tile.
+#ifndef NSLAM_FWD_PF
+#define NSLAM_FWD_PF 1  // the GEMM chain with each weight fragment loaded one GEMM ahead (xyz_forward_pf)
+#endif
 __device__ __forceinline__ void fwd_part_middle(const QueryKArgs& a, const Pt& q, int64_t tile, int64_t idx, int lane,
                                                 float* __restrict__ occ_mid, const float* vec) {
   const int h = lane >> 5;
@@ -1104,7 +1156,8 @@ __device__ __forceinline__ void fwd_part_middle(const QueryKArgs& a, const Pt& q
   const float* pk = a.c.packed[NSLAM_DEC_MIDDLE];
   const XyzPack L{1};
   const f32x16 cms[1] = {cm};
-  const f32x16 h4 = xyz_forward<1, false, true, false, true>(pk, cms, q.x, lane, m, nullptr, nullptr, vec);
+  const f32x16 h4 = NSLAM_FWD_PF ? xyz_forward_pf<1, false>(pk, cms, q.x, lane, m, nullptr, vec)
+                                 : xyz_forward<1, false, true, false, true>(pk, cms, q.x, lane, m, nullptr, nullptr, vec);
   save_masks(a, NSLAM_DEC_MIDDLE, tile, m, lane);
   float o = out_row(vec + (L.Wo() - L.V()), vec + (L.Bo() - L.V()), 0, h4, lane);
   if (!q.inside) o = 100.f;
@@ -1126,7 +1179,8 @@ __device__ __forceinline__ void fwd_part_fine(const QueryKArgs& a, const Pt& q, 
   PHASE(0, 3);
   const float* pk = a.c.packed[NSLAM_DEC_FINE];
   const XyzPack L{2};
-  const f32x16 h4 = xyz_forward<2, false, true, false, true>(pk, cf, q.x, lane, m, nullptr, nullptr, vec);
+  const f32x16 h4 = NSLAM_FWD_PF ? xyz_forward_pf<2, false>(pk, cf, q.x, lane, m, nullptr, vec)
+                                 : xyz_forward<2, false, true, false, true>(pk, cf, q.x, lane, m, nullptr, nullptr, vec);
   save_masks(a, NSLAM_DEC_FINE, tile, m, lane);
   float o = out_row(vec + (L.Wo() - L.V()), vec + (L.Bo() - L.V()), 0, h4, lane);
   if (!q.inside) o = 0.f;
@@ -1153,7 +1207,8 @@ __device__ __forceinline__ void fwd_part_color(const QueryKArgs& a, const Pt& q,
   const float* pk = a.c.packed[NSLAM_DEC_COLOR];
   const XyzPack L{1};
   float* tp = TAPE ? a.c.act_tape + tile * kTapeFloats : nullptr;
-  const f32x16 h4 = xyz_forward<1, false, true, TAPE, true>(pk, cc, q.x, lane, m, nullptr, tp, vec);
+  const f32x16 h4 = NSLAM_FWD_PF ? xyz_forward_pf<1, TAPE>(pk, cc, q.x, lane, m, tp, vec)
+                                 : xyz_forward<1, false, true, TAPE, true>(pk, cc, q.x, lane, m, nullptr, tp, vec);
   save_masks(a, NSLAM_DEC_COLOR, tile, m, lane);
   float o[3];
 #pragma unroll

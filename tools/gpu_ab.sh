@@ -1,17 +1,20 @@
-# A/B of two libnslam builds (same ABI) on one box: knob-probe timing, then a one-iteration kernel
-# timeline of each.  usage: bash tools/gpu_ab.sh TAG LIB_A LIB_B   (paths relative to the repo)
+# A/B of libnslam builds (same ABI) on one box: the room0 colour-stage bench of each, then a
+# one-iteration kernel timeline of each.  usage: bash tools/gpu_ab.sh TAG LIB...   (paths relative
+# to the repo; build variants with make -C nice-slam_amd/csrc variant V=name X="-D...")
 set -o pipefail
-OUT=gpurun_out/${1:?tag}
+OUT=gpurun_out/${1:?tag}; shift
 mkdir -p $OUT
 export TMPDIR=/tmp
-for L in ${2:?lib a} ${3:?lib b}; do
+[ $# -ge 1 ] || { echo "no libraries"; exit 2; }
+summ() { python -c "
+import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[2], round(d['value']/1e6,2), 'M/s', round(d['ms_per_step'],4), 'ms', d.get('kernels_ms'))" "$1" "$2"; }
+for L in "$@"; do
   n=$(basename $L .so)
-  NSLAM_LIB=$PWD/$L timeout -k 10 200 python -u tools/probes/knobs.py default > $OUT/knobs_$n.log 2>&1 || { tail -20 $OUT/knobs_$n.log; exit 1; }
-  echo "$n: $(tail -1 $OUT/knobs_$n.log)"
+  NSLAM_LIB=$PWD/$L timeout -k 10 300 python bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-stress --no-bulk --no-frames > $OUT/bench_$n.json 2> $OUT/bench_$n.err || { tail -20 $OUT/bench_$n.err; exit 1; }
+  summ $OUT/bench_$n.json $n
 done
-for L in $2 $3; do
+for L in "$@"; do
   n=$(basename $L .so)
-  export NSLAM_LIB=$PWD/$L
-  timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace_$n -o run -- python bench.py --steps 8 --warmup 3 --no-cpu-baseline --no-stress --no-frames --no-bulk > $OUT/trace_$n.log 2>&1 || { tail -20 $OUT/trace_$n.log; exit 1; }
+  NSLAM_LIB=$PWD/$L timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace_$n -o run -- python bench.py --steps 8 --warmup 3 --no-cpu-baseline --no-stress --no-frames --no-bulk > $OUT/trace_$n.log 2>&1 || { tail -20 $OUT/trace_$n.log; exit 1; }
   python tools/timeline.py $OUT/trace_$n/run_kernel_trace.csv 7 > $OUT/timeline_$n.txt && echo "== $n" && cat $OUT/timeline_$n.txt
 done

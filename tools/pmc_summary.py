@@ -8,12 +8,14 @@ import os
 import sys
 from collections import defaultdict
 
+SIMDS = 1024  # MI355X: 256 CUs x 4 SIMDs
+
 
 def main():
     acc = defaultdict(lambda: defaultdict(list))
     dur = defaultdict(list)
     for d in sys.argv[1:]:
-        for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             seen = set()
             for r in csv.DictReader(open(f)):
                 name = r["Kernel_Name"]
@@ -29,8 +31,26 @@ def main():
     for k in sorted(acc):
         d = sum(dur[k]) / max(len(dur[k]), 1)
         print(f"== {k}  (avg {d:.1f} us over {len(dur[k])} dispatch-passes)")
-        for c, v in sorted(acc[k].items()):
-            print(f"   {c:28s} {sum(v) / len(v):16.1f}")
+        m = {c: sum(v) / len(v) for c, v in acc[k].items()}
+        for c, v in sorted(m.items()):
+            print(f"   {c:28s} {v:16.1f}")
+        # derived (MI355X_MICROARCH.md: GRBM_GUI_ACTIVE sums the 8 XCDs' cycles; SQ_WAVE_CYCLES and
+        # SQ_ACTIVE_INST_* count quad-cycles, SQ_VALU_MFMA_BUSY_CYCLES cycles; 1024 SIMDs)
+        if "GRBM_GUI_ACTIVE" in m:
+            clk = m["GRBM_GUI_ACTIVE"] / 8
+            simd_cyc = clk * SIMDS
+            print(f"   {'(clock GHz)':28s} {clk / (d * 1e3):16.3f}")
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
+                print(f"   {'(MFMA busy / SIMD-cycles)':28s} {m['SQ_VALU_MFMA_BUSY_CYCLES'] / simd_cyc:16.3f}")
+            if "SQ_WAVE_CYCLES" in m:
+                print(f"   {'(resident waves / SIMD)':28s} {4 * m['SQ_WAVE_CYCLES'] / simd_cyc:16.3f}")
+            if "SQ_ACTIVE_INST_VALU" in m:
+                print(f"   {'(VALU issue / SIMD-cycles)':28s} {4 * m['SQ_ACTIVE_INST_VALU'] / simd_cyc:16.3f}")
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in m and m.get("SQ_INSTS_MFMA"):
+            print(f"   {'(MFMA busy cycles / instr)':28s} {m['SQ_VALU_MFMA_BUSY_CYCLES'] / m['SQ_INSTS_MFMA']:16.1f}")
+        for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY"):
+            if c in m and m.get("SQ_WAVE_CYCLES"):
+                print(f"   {'(' + c + ' / WAVE_CYCLES)':28s} {m[c] / m['SQ_WAVE_CYCLES']:16.3f}")
 
 
 if __name__ == "__main__":
