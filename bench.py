@@ -504,11 +504,7 @@ def stress_iteration(dev, steps=10):
     if g is not None:
         g.finish()
     samples = int(scene.kept) * (STRESS["n_strat"] + STRESS["n_surf"])
-    P.ops.TIMER = P.ops.KernelTimer()
-    for _ in range(3):
-        scene.step()
-    timers = P.ops.TIMER.summary()
-    P.ops.TIMER = None
+    timers = span_timers(scene, 3)
     pts = samples / steps
     fwd = timers["query_fwd"]["avg_ms"] * 1e-3
     rows = {k: int(v.numel()) for k, v in scene.rows.items()}
@@ -690,6 +686,27 @@ def kernel_roofline(name, avg_ms, pts, traffic_path=None):
             "rocprof_kernels": list(SPAN_KERNELS.get(name, ())),
             "traffic_note": "HBM bytes per launch: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, "
                             + os.path.relpath(tp, REPO)}
+
+
+def span_timers(scene, steps, sharded=False):
+    """HIP-event spans of every C-ABI launch over `steps` extra eager iterations, with the backward
+    branches serialised (engine.concurrent = False): each span is then one kernel (or one kernel +
+    its slab reduction) alone on the chip, the duration its roofline is priced on.  The timed
+    iterations (the headline value) run the branches concurrently."""
+    P = pkg()
+    eng = getattr(scene, "engine", None)
+    conc = eng.concurrent if eng is not None else None
+    if eng is not None:
+        eng.concurrent = False
+    P.ops.TIMER = P.ops.KernelTimer()
+    try:
+        for _ in range(steps):
+            scene.step(sharded=sharded)
+        return P.ops.TIMER.summary()
+    finally:
+        P.ops.TIMER = None
+        if eng is not None:
+            eng.concurrent = conc
 
 
 def graph_time(scene, fn, reps):
@@ -901,11 +918,7 @@ def main():
     # extra eager steps of the same kernels (events cannot bracket single kernels inside a replay)
     if graph is not None:
         graph.finish()
-    P.ops.TIMER = P.ops.KernelTimer()
-    for _ in range(max(5, args.steps // 4)):
-        scene.step(sharded=sharded)
-    timers = P.ops.TIMER.summary()
-    P.ops.TIMER = None
+    timers = span_timers(scene, max(5, args.steps // 4), sharded=sharded)
     tot = torch.tensor([samples, dt], dtype=torch.float64, device=dev)
     if world > 1:
         s = tot[:1].clone()

@@ -359,19 +359,50 @@ __device__ __forceinline__ void handover() {
 // wave; cons(t, buf) consumes tile t.  Every role runs the same number of hand-overs (t1 - t0 + 1), so
 // the workgroup's barriers match; each role's loop-carried values are its own (one role per wave: the
 // register budget is the largest role's, not the union of all of them).
+#ifdef NSLAM_PHASES
+// phases build: per wave, the cycles spent producing, consuming and waiting at the hand-overs
+#define CW_MARK(acc)                                           \
+  do {                                                         \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    acc += now_ - last_;                                       \
+    last_ = now_;                                              \
+  } while (0)
+#else
+#define CW_MARK(acc) \
+  do {               \
+  } while (0)
+#endif
 template <class Prod, class Cons>
 __device__ __forceinline__ void role_loop(float* lds, int64_t t0, int64_t t1, const Prod& prod, const Cons& cons) {
+#ifdef NSLAM_PHASES
+  unsigned long long last_ = __builtin_amdgcn_s_memtime(), tp = 0, tc = 0, th = 0;
+#endif
   prod(t0, lds);
+  CW_MARK(tp);
   handover();
+  CW_MARK(th);
 #pragma nounroll
   for (int64_t t = t0; t < t1; ++t) {
     const float* buf = lds + ((t - t0) & 1) * kBuf;
     float* nbuf = lds + ((t + 1 - t0) & 1) * kBuf;
     if (t + 1 < t1) prod(t + 1, nbuf);  // (its loads fly while this tile is computed)
+    CW_MARK(tp);
     __builtin_amdgcn_sched_barrier(0);
     cons(t, buf);
+    CW_MARK(tc);
     handover();  // the next buffer is complete / this one is free
+    CW_MARK(th);
   }
+#ifdef NSLAM_PHASES
+  const int64_t w_ = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0 && w_ < kPhaseWaves) {
+    unsigned long long* o = g_phase + ((size_t)4 * kPhaseWaves + w_) * 16;
+    o[0] = tp;
+    o[1] = tc;
+    o[2] = th;
+    o[3] = (unsigned long long)(t1 - t0);
+  }
+#endif
 }
 
 // The laundered lane: LDS addresses are functions of the lane only, i.e. loop-invariant; letting LICM

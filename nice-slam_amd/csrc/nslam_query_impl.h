@@ -117,7 +117,8 @@ __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)"
 // at marks 0..15 of its tile into g_phase[decoder][wave][16].
 #ifdef NSLAM_PHASES
 constexpr int kPhaseWaves = 1 << 15;
-__device__ unsigned long long g_phase[4 * kPhaseWaves * 16];  // one-TU phases build only
+// slots: 0 forward, 1..3 decoder backward, 4 k_color_wgrad (per wave: cycles in prod / cons / hand-over)
+__device__ unsigned long long g_phase[5 * kPhaseWaves * 16];  // one-TU phases build only
 #define PHASE(dec, k)                                                                                     \
   do {                                                                                                    \
     const int64_t w_ = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);                     \
@@ -327,22 +328,61 @@ __device__ __forceinline__ f32x16 xyz_forward(const float* __restrict__ pk, cons
 #undef PHF_
 }
 
+#ifndef NSLAM_FWD_PF
+// the decoder-parallel forward's GEMM chain: 1 each weight fragment loaded one GEMM ahead
+// (xyz_forward_pf), 2 + the next embedding block computed in the MFMAs' shadow, 0 xyz_forward
+#define NSLAM_FWD_PF 1
+#endif
+#ifndef NSLAM_FWD_ROLL
+#define NSLAM_FWD_ROLL 0  // FragRoll (one fragment of registers) instead of FragPipe (two)
+#endif
 // xyz_forward of the decoder-parallel forward (VLDS: the vector section in LDS), its 15 (NC = 1) or 20
 // (NC = 2) GEMMs as a FragPipe: each weight fragment is loaded while the previous GEMM runs, so no GEMM
 // waits for its fragment's L2 round trip.  The same products in the same order as xyz_forward.
-template <int NC, bool TAPE>
+template <int NC, bool TAPE, bool ILV = (NSLAM_FWD_PF == 2)>
 __device__ __forceinline__ f32x16 xyz_forward_pf(const float* __restrict__ pk, const f32x16 (&cin)[NC],
                                                  const float x[3], int lane, uint32_t m[5],
                                                  float* __restrict__ tape, const float* vs) {
   const XyzPack L{NC};
+#if NSLAM_FWD_ROLL || NSLAM_FWD_PF == 2
+  FragRoll fp(pk, L.L0(), lane);
+#else
   FragPipe fp(pk, L.L0(), lane);
+#endif
   f32x16 a = vec_tile(vs + (L.Bias(0) - L.V()), lane);
   f32x16 a3 = vec_tile(vs + (L.Bias(3) - L.V()), lane);
+  if constexpr (ILV) {
+    // the embedding block b+1 (sin(x B): ~370 VALU instructions per lane) computed in the shadow of
+    // block b's two GEMMs (32 MFMAs of 64 cycles): one scheduling region per block, each MFMA followed
+    // by a group of VALU instructions, each fragment quarter's load right after its last reader
+    f32x16 e = emb_tile<false, false>(vs + (L.FB() - L.V()), x, 0, lane);
 #pragma unroll
-  for (int b = 0; b < 3; ++b) {
-    const f32x16 e = emb_tile<false, false>(vs + (L.FB() - L.V()), x, b, lane);
-    fp.gemm(a, e, L.L3() + b);
-    fp.gemm(a3, e, b < 2 ? L.L0() + b + 1 : L.FC(0, 0));
+    for (int b = 0; b < 3; ++b) {
+      __builtin_amdgcn_sched_barrier(0);
+      f32x16 en = e;
+      if (b < 2) en = emb_tile<false, false>(vs + (L.FB() - L.V()), x, b + 1, lane);
+      fp.template gemm<false>(a, e, L.L3() + b);
+      fp.template gemm<false>(a3, e, b < 2 ? L.L0() + b + 1 : L.FC(0, 0));
+      __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);  // B of block b+1 (LDS)
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 12, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // the next fragment's quarter g & 3
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      e = en;
+    }
+  } else {
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      const f32x16 e = emb_tile<false, false>(vs + (L.FB() - L.V()), x, b, lane);
+      fp.gemm(a, e, L.L3() + b);
+      fp.gemm(a3, e, b < 2 ? L.L0() + b + 1 : L.FC(0, 0));
+    }
   }
   // fc_c.i (cin) with the next layer's first fragment after it
   auto fc = [&](int i, int next) {
@@ -1141,9 +1181,6 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd(QueryKArgs a) {
 // and k_occ_combine then forms raw[p][3] = fine_occ + middle_occ (decoder.py:331-334, the
 // reference's operand order) — exactly 100 outside the bound (0 + 100; Renderer.py:57).
 // One decoder of the decoder-parallel forward for this wave's tile.
-#ifndef NSLAM_FWD_PF
-#define NSLAM_FWD_PF 1  // the GEMM chain with each weight fragment loaded one GEMM ahead (xyz_forward_pf)
-#endif
 __device__ __forceinline__ void fwd_part_middle(const QueryKArgs& a, const Pt& q, int64_t tile, int64_t idx, int lane,
                                                 float* __restrict__ occ_mid, const float* vec) {
   const int h = lane >> 5;

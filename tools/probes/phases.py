@@ -33,9 +33,9 @@ def main():
     L = P._lib.lib()
     L.nslam_debug_phases.argtypes = [ctypes.c_void_p, ctypes.c_int64]
     W = 1 << 15
-    buf = np.zeros(4 * W * 16, dtype=np.uint64)
+    buf = np.zeros(5 * W * 16, dtype=np.uint64)
     assert L.nslam_debug_phases(buf.ctypes.data, buf.size) == 0
-    buf = buf.reshape(4, W, 16).astype(np.int64)
+    buf = buf.reshape(5, W, 16).astype(np.int64)
     tiles = (scene.cfg["pixels"] * 48 + 31) // 32
     fwd_names = {0: "start", 1: "point", 2: "corners", 3: "gather", 5: "emb+L0+L3e", 6: "L1+L2", 7: "L3", 8: "L4",
                  9: "out+store"}
@@ -56,6 +56,20 @@ def main():
             dt = tp[:, b_] - tp[:, a_]
             print(f"   {fwd_names[a_]:>12s} -> {fwd_names[b_]:<12s} median {np.median(dt):8.0f}  "
                   f"({100 * np.median(dt) / max(np.median(tot), 1):5.1f}%)")
+    # k_color_wgrad: per wave (8 per workgroup, one chunk of tiles each) the cycles producing the next
+    # tile, consuming this one and waiting at the hand-over barriers
+    cw = buf[4]
+    nwg = int((cw[:, 3] > 0).sum()) // 8
+    if nwg:
+        cw = cw[:nwg * 8].reshape(nwg, 8, 16)
+        roles = {0: "S_b dW3/dW0", 1: "S_b dW3/dW0", 2: "S_b dW3/dW0", 3: "feature+h2/dW2", 4: "fc_c+dB",
+                 5: "fc_c+dB", 6: "fc_c.2,dW4+dB", 7: "chain producer"}
+        print(f"== k_color_wgrad: {nwg} workgroups, tiles per chunk median {np.median(cw[:, 0, 3]):.0f}")
+        for wv in range(8):
+            tp, tc, th = (np.median(cw[:, wv, k]) for k in range(3))
+            tot = tp + tc + th
+            print(f"   wave {wv} {roles[wv]:>16s}: prod {tp:8.0f}  cons {tc:8.0f}  wait {th:8.0f}  "
+                  f"(wait {100 * th / max(tot, 1):5.1f}%)")
     for d, nm in ((1, "middle"), (2, "fine"), (3, "color")):
         t = buf[d, :tiles]
         marks = [k for k in range(16) if (t[:, k] != 0).all()]
