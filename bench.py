@@ -95,8 +95,11 @@ SPAN_KERNELS = {
     "query_bwd.middle+fine": ("k_dec_bwd_multi<false>",),
     "query_bwd.middle+fine+color": ("k_dec_bwd_multi<false>",),
 }
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r03_traffic.json")
-STRESS_TRAFFIC_FILE = os.path.join(REPO, "profiles", "r03_traffic_stress.json")
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r04_traffic.json")
+STRESS_TRAFFIC_FILE = os.path.join(REPO, "profiles", "r04_traffic_stress.json")
+# SQ / GRBM counters of the same kernels (tools/gpu_counters.sh → tools/pmc_summary.py)
+PMC_FILE = os.path.join(REPO, "profiles", "r04_room0_pmc.txt")
+STRESS_PMC_FILE = os.path.join(REPO, "profiles", "r04_stress_pmc.txt")
 
 
 def pmc_traffic(span, path=None):
@@ -124,6 +127,32 @@ def pmc_write_bytes(span, path=None):
     pats = SPAN_KERNELS.get(span, (span,))
     hits = [v["write_size_kib"] * 1024.0 for k, v in kern.items() if any(k.startswith(p) for p in pats)]
     return sum(hits) if hits else None
+
+
+def pmc_counters(span, path=None):
+    """The derived SQ counters (MFMA busy / SIMD-cycles, resident waves per SIMD, VALU issue, wait
+    fractions, clock) and the average duration of the first rocprof kernel of `span` from a committed
+    pmc_summary.py output, or None."""
+    try:
+        with open(path or PMC_FILE) as f:
+            text = f.read()
+    except OSError:
+        return None
+    pats = SPAN_KERNELS.get(span, (span,))
+    for sec in text.split("== ")[1:]:
+        head, _, body = sec.partition("\n")
+        if not any(head.startswith(p) for p in pats):
+            continue
+        out = {"kernel": head.split("  (")[0], "file": os.path.relpath(path or PMC_FILE, REPO)}
+        if "(avg " in head:
+            out["avg_us"] = float(head.split("(avg ")[1].split(" us")[0])
+        for line in body.splitlines():
+            line = line.strip()
+            if line.startswith("("):
+                k, v = line.rsplit(" ", 1)
+                out[k.strip()[1:-1]] = float(v)
+        return out
+    return None
 
 
 def pkg():
@@ -511,7 +540,10 @@ def stress_iteration(dev, steps=10):
     out = {"value": samples / dt, "unit": "ray-samples/s", "ms_per_iteration": dt / steps * 1e3, "steps": steps,
            "launch_mode": mode, "ray_samples_per_iteration": pts,
            "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in timers.items()},
-           "query_fwd_roofline": kernel_roofline("query_fwd", timers["query_fwd"]["avg_ms"], pts, STRESS_TRAFFIC_FILE),
+           "query_fwd_roofline": kernel_roofline("query_fwd", timers["query_fwd"]["avg_ms"], pts, STRESS_TRAFFIC_FILE,
+                                                 STRESS_PMC_FILE),
+           "kernel_rooflines": {k: kernel_roofline(k, v["avg_ms"], pts, STRESS_TRAFFIC_FILE, STRESS_PMC_FILE)
+                                for k, v in timers.items() if k in KERNEL_WORK},
            "query_fwd_gather_gbs": pts * BYTES_FWD_PER_SAMPLE / fwd / 1e9,
            "query_fwd_gather_hbm_frac": pts * BYTES_FWD_PER_SAMPLE / fwd / 1e9 / HBM_PEAK_GBS,
            "frustum_rows": rows,
@@ -652,7 +684,7 @@ def reference_gpu_baseline(scene, budget_s=4.0):
                       "(torch ops of the reference path) on the GPU, eager"}
 
 
-def kernel_roofline(name, avg_ms, pts, traffic_path=None):
+def kernel_roofline(name, avg_ms, pts, traffic_path=None, pmc_path=None):
     """Roofline of one timed launch: algorithmic FLOPs and bytes (KERNEL_WORK × ray-samples per
     launch) over its HIP-event average; the bound is whichever roof (fp32 MFMA, HBM) the
     algorithmic work would hit first — or, for the frozen decoders' mask-only backward, the
@@ -685,7 +717,9 @@ def kernel_roofline(name, avg_ms, pts, traffic_path=None):
             # with the SUM of their average durations in the rocprof summary under profiles/
             "rocprof_kernels": list(SPAN_KERNELS.get(name, ())),
             "traffic_note": "HBM bytes per launch: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, "
-                            + os.path.relpath(tp, REPO)}
+                            + os.path.relpath(tp, REPO),
+            # the counters behind the bound: SQ_VALU_MFMA_BUSY_CYCLES etc. of the span's first kernel
+            "pmc": pmc_counters(name, pmc_path)}
 
 
 def span_timers(scene, steps, sharded=False):

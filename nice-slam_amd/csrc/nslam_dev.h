@@ -504,8 +504,10 @@ __device__ __forceinline__ float adam_one(float& p, float g, float& m, float& v,
 // One workgroup's share of a segment's update (k_adam's body; nthreads = the workgroup's size):
 // dense segments one element per thread (lb * nthreads + tid), row-masked segments row_len/4
 // threads per row (float4 each) — the same element update everywhere, so any launch that hands a
-// segment's workgroups this function updates it bit-identically.
-__device__ __forceinline__ void adam_segment_block(const nslam_adam_seg& sg, const AdamCoef& c, int64_t lb,
+// segment's workgroups this function updates it bit-identically.  coef() (the bias corrections: two
+// float64 pow) is evaluated after the element's loads are issued, so its latency overlaps theirs.
+template <class CoefFn>
+__device__ __forceinline__ void adam_segment_block(const nslam_adam_seg& sg, const CoefFn& coef, int64_t lb,
                                                    int zero_grad, int tid, int nthreads) {
   typedef float f4 __attribute__((ext_vector_type(4)));
   if (!sg.rows) {
@@ -513,6 +515,8 @@ __device__ __forceinline__ void adam_segment_block(const nslam_adam_seg& sg, con
     if (e < sg.n) {
       float p = sg.param[e], m = sg.exp_avg[e], v = sg.exp_avg_sq[e];
       const float g = sg.grad[e];
+      __builtin_amdgcn_sched_barrier(0);  // the loads first, then the coefficients (their latency hides)
+      const AdamCoef c = coef();
       adam_one(p, g, m, v, c);
       sg.param[e] = p;
       sg.exp_avg[e] = m;
@@ -537,6 +541,8 @@ __device__ __forceinline__ void adam_segment_block(const nslam_adam_seg& sg, con
       const f4 g = *reinterpret_cast<const f4*>(sg.grad + gbase);
       f4 m = *reinterpret_cast<const f4*>(sg.exp_avg + sbase);
       f4 v = *reinterpret_cast<const f4*>(sg.exp_avg_sq + sbase);
+      __builtin_amdgcn_sched_barrier(0);
+      const AdamCoef c = coef();
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         float pk = p[k], mk = m[k], vk = v[k];

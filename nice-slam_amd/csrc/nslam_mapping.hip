@@ -183,8 +183,10 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam(AdamArgs a) {
   int s = 0;
   while (s + 1 < a.nseg && b >= a.blk0[s + 1]) ++s;
   const nslam_adam_seg& sg = a.seg[s];
-  const AdamCoef c = adam_coef(a.b1, a.b2, a.eps, sg.lr, *sg.step);
-  adam_segment_block(sg, c, b - a.blk0[s], a.zero_grad, (int)threadIdx.x, kAdamThreads);
+  const float step = *sg.step;
+  adam_segment_block(
+      sg, [&] { return adam_coef(a.b1, a.b2, a.eps, sg.lr, step); }, b - a.blk0[s], a.zero_grad, (int)threadIdx.x,
+      kAdamThreads);
   if (a.ticket) {
     // Every workgroup read its segment's step count at its start (the value was consumed long
     // before this point), so once all of them have drawn a ticket no read is outstanding and the

@@ -186,7 +186,7 @@ extern "C" int nslam_pack_layout(int kind, int nc, int32_t* out, int n) {
 
 #ifdef NSLAM_PHASES
 extern "C" int nslam_debug_phases(unsigned long long* out, int64_t n) {
-  if (n > (int64_t)4 * kPhaseWaves * 16) n = (int64_t)4 * kPhaseWaves * 16;
+  if (n > (int64_t)5 * kPhaseWaves * 16) n = (int64_t)5 * kPhaseWaves * 16;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -106,9 +106,6 @@ class MappingEngine:
         # every mask-only decoder backward as ONE launch (ABI v10); False: one nslam_query_bwd_decoder
         # launch per decoder (the library then runs a colour tape backward's two kernels in sequence)
         self.merge = True
-        # one rank: Adam per backward branch on the branch's stream (True) or one Adam call for every
-        # parameter after the join (False)
-        self.branch_adam = os.environ.get("NSLAM_BRANCH_ADAM", "1") == "1"
         self._lean_ev = None
         for k, v in c.items():
             if not v.is_contiguous(memory_format=torch.channels_last_3d):
@@ -444,7 +441,7 @@ class MappingEngine:
             # on that branch's stream as soon as it finishes — the exchange does the optimiser step
             def on_branch(names, part=None):
                 exchange.branch(names, part, keys, dnames)
-        elif exchange is None and allreduce is None and mirror and self.branch_adam:
+        elif exchange is None and allreduce is None and mirror:
             # one rank: each backward branch updates what it completes on its own stream — the lean
             # launch the middle / fine grid rows, the weight-gradient branch (once the lean launch is
             # done too) the colour grid and the colour decoder — so no Adam waits for the whole backward

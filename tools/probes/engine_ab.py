@@ -15,7 +15,6 @@ import bench  # noqa: E402
 
 SETTINGS = {
     "default": {},
-    "join_adam": {"branch_adam": False},
     "lean_first": {"wgrad_first": False},
     "serial": {"concurrent": False},
 }

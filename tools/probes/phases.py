@@ -39,10 +39,14 @@ def main():
     tiles = (scene.cfg["pixels"] * 48 + 31) // 32
     fwd_names = {0: "start", 1: "point", 2: "corners", 3: "gather", 5: "emb+L0+L3e", 6: "L1+L2", 7: "L3", 8: "L4",
                  9: "out+store"}
-    nw = ((tiles + 3) // 4) * 3 * 4
+    print("nonzero marks per slot:", [int((buf[k] != 0).sum()) for k in range(5)])
+    # room0 colour stage: the 2-part forward (middle then colour | fine), parts alternating along
+    # blockIdx / 8 (XCD-aware mapping, k_query_fwd_parts); 4 waves per workgroup
+    groups = (tiles + 3) // 4
+    nw = (groups + 7) // 8 * 8 * 2 * 4
     t = buf[0, :nw]
-    part = (np.arange(nw) // 4) % 3
-    for pi, nm in ((0, "middle"), (1, "fine"), (2, "color")):
+    part = ((np.arange(nw) // 4) // 8) % 2
+    for pi, nm in ((0, "middle then colour"), (1, "fine")):
         tp = t[(part == pi) & (t[:, 0] != 0)]
         marks = [k for k in range(16) if (tp[:, k] != 0).all()]
         tot = tp[:, marks[-1]] - tp[:, marks[0]]
