@@ -20,7 +20,7 @@
 // in registers over the whole chunk and written once into the chunk's slab; k_slab_reduce sums the
 // slabs in a fixed order (deterministic).
 //
-// Roles (waves w and w + 4 share a SIMD):
+// Roles ("waves" 0-7; which hardware wave takes which role: the permutation in k_color_wgrad):
 //   wave b = 0..2  dW_3[:, 32b..] = Σ da3 ⊗ S_b, dW_0[:, 32b..] = Σ da0 ⊗ S_b (+ db_0, b = 0)
 //   wave 3         dW_3[:, 93:125] = Σ da3 ⊗ h2, dW_2 = Σ da2 ⊗ h1 (+ db_3, db_2)
 //   wave 4, 5      fc_c.k, fc_c.(k+3) = Σ dh ⊗ c (k = wave - 4), and dB[:, 32k..]
@@ -59,6 +59,9 @@ static_assert(kLds * 4 <= 100 * 1024, "LDS: leave room for the lean backward's w
 
 #ifndef NSLAM_CW_GATHER_NB
 #define NSLAM_CW_GATHER_NB 1  // corners in flight of the feature gather (2: 129 VGPRs, one over the 4-wave budget)
+#endif
+#ifndef NSLAM_CW_PERM
+#define NSLAM_CW_PERM 1  // roles permuted over the SIMDs (k_color_wgrad)
 #endif
 #ifndef NSLAM_CW_LB
 #define NSLAM_CW_LB 4  // min waves per SIMD: <= 128 VGPRs, so the lean backward's waves fit beside it
@@ -419,7 +422,12 @@ __global__ __launch_bounds__(64 * kCwWaves, NSLAM_CW_LB) void k_color_wgrad(CwAr
   // ONE __shared__ array (a second one can make hipcc drain the LDS-DMA early)
   __shared__ __attribute__((aligned(16))) float lds[kLds];
   const QueryKArgs& a = w.a;
-  const int lane0 = threadIdx.x & 63, wave = wave_id();
+  // role of this wave (the "wave" numbers of the header comment); hardware waves w and w + 4 share a
+  // SIMD, and the permutation pairs each producer with a light S_b role and the three fc_c roles apart:
+  // SIMD 0 chain + S_0, SIMD 1 feature + S_1, SIMD 2 fc_c.2 + S_2, SIMD 3 fc_c.0 + fc_c.1
+  // (tools/probes/phases.py: the two producers on one SIMD made it the busiest by ~35 %)
+  const int hw = wave_id();
+  const int lane0 = threadIdx.x & 63, wave = NSLAM_CW_PERM ? (int)((0x52104637u >> (4 * hw)) & 15u) : hw;
   const int chunk = (int)blockIdx.x;
   const int64_t ntiles = (a.n + 31) / 32;
   const int64_t t0 = chunk * w.chunk_tiles;

@@ -984,7 +984,8 @@ __device__ __forceinline__ void scatter_grid_grad_uniform(float* __restrict__ gr
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const bool keep = (kb >> j) & 1;
-        if (!keep && wsum[j] != 0.f) grid_add(grad + (size_t)rows[j] * NSLAM_C_DIM + ch, acc[j]);
+        // one exec-masked flush (both conditions evaluated: no nested branch)
+        if ((!keep) & (wsum[j] != 0.f)) grid_add(grad + (size_t)rows[j] * NSLAM_C_DIM + ch, acc[j]);
         acc[j] = keep ? acc[j] : 0.f;
         wsum[j] = keep ? wsum[j] : 0.f;
         rows[j] = nr[j];
