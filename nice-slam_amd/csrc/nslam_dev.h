@@ -501,69 +501,106 @@ __device__ __forceinline__ float adam_one(float& p, float g, float& m, float& v,
   return p;
 }
 
-// One workgroup's share of a segment's update (k_adam's body; nthreads = the workgroup's size):
-// dense segments one element per thread (lb * nthreads + tid), row-masked segments row_len/4
-// threads per row (float4 each) — the same element update everywhere, so any launch that hands a
-// segment's workgroups this function updates it bit-identically.  coef() (the bias corrections: two
-// float64 pow) is evaluated after the element's loads are issued, so its latency overlaps theirs.
-template <class CoefFn>
+// One workgroup's share of a segment's update (k_adam's body; nthreads = the workgroup's size): R
+// items per thread, dense segments one element per item (element (lb R + k) nthreads + tid),
+// row-masked segments row_len/4 threads per row (one float4 per item) — the same element update
+// everywhere, so any launch that hands a segment's workgroups this function updates it
+// bit-identically.  Every item's loads are issued before any arithmetic (R × 4 loads in flight per
+// thread), and coef() (the bias corrections: two float64 pow) is evaluated while they fly.
+template <int R, class CoefFn>
 __device__ __forceinline__ void adam_segment_block(const nslam_adam_seg& sg, const CoefFn& coef, int64_t lb,
                                                    int zero_grad, int tid, int nthreads) {
   typedef float f4 __attribute__((ext_vector_type(4)));
   if (!sg.rows) {
-    const int64_t e = lb * nthreads + tid;
-    if (e < sg.n) {
-      float p = sg.param[e], m = sg.exp_avg[e], v = sg.exp_avg_sq[e];
-      const float g = sg.grad[e];
-      __builtin_amdgcn_sched_barrier(0);  // the loads first, then the coefficients (their latency hides)
-      const AdamCoef c = coef();
-      adam_one(p, g, m, v, c);
-      sg.param[e] = p;
-      sg.exp_avg[e] = m;
-      sg.exp_avg_sq[e] = v;
-      if (zero_grad) sg.grad[e] = 0.f;
+    int64_t e[R];
+    float p[R], m[R], v[R], g[R];
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      e[k] = (lb * R + k) * nthreads + tid;
+      if (e[k] < sg.n) {
+        p[k] = sg.param[e[k]];
+        m[k] = sg.exp_avg[e[k]];
+        v[k] = sg.exp_avg_sq[e[k]];
+        g[k] = sg.grad[e[k]];
+        any = true;
+      }
+    }
+    if (!any) return;
+    __builtin_amdgcn_sched_barrier(0);  // the loads first, then the coefficients (their latency hides)
+    const AdamCoef c = coef();
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      if (e[k] >= sg.n) continue;
+      adam_one(p[k], g[k], m[k], v[k], c);
+      sg.param[e[k]] = p[k];
+      sg.exp_avg[e[k]] = m[k];
+      sg.exp_avg_sq[e[k]] = v[k];
+      if (zero_grad) sg.grad[e[k]] = 0.f;
       if (sg.mirror) {  // the packed MFMA copy of this parameter (up to two slots)
-        const int i0 = sg.mirror_idx[2 * e], i1 = sg.mirror_idx[2 * e + 1];
-        if (i0 >= 0) sg.mirror[i0] = p;
-        if (i1 >= 0) sg.mirror[i1] = p;
+        const int i0 = sg.mirror_idx[2 * e[k]], i1 = sg.mirror_idx[2 * e[k] + 1];
+        if (i0 >= 0) sg.mirror[i0] = p[k];
+        if (i1 >= 0) sg.mirror[i1] = p[k];
       }
     }
   } else {
     const int q = sg.row_len / 4;  // float4 per row
     const int64_t rows_per_block = nthreads / q;
-    const int64_t ri = lb * rows_per_block + tid / q;
     const int part = tid % q;
-    if (tid < rows_per_block * q && ri < sg.n) {
-      const int64_t base = (int64_t)sg.rows[ri] * sg.row_len + part * 4;
-      const int64_t sbase = ri * sg.row_len + part * 4;
-      f4 p = *reinterpret_cast<const f4*>(sg.param + base);
-      const int64_t gbase = sg.grad_rows ? sbase : base;
-      const f4 g = *reinterpret_cast<const f4*>(sg.grad + gbase);
-      f4 m = *reinterpret_cast<const f4*>(sg.exp_avg + sbase);
-      f4 v = *reinterpret_cast<const f4*>(sg.exp_avg_sq + sbase);
-      __builtin_amdgcn_sched_barrier(0);
-      const AdamCoef c = coef();
+    const bool lane_ok = tid < rows_per_block * q;
+    int64_t ri[R], base[R], sbase[R], gbase[R];
+    bool ok[R];
+    bool any = false;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float pk = p[k], mk = m[k], vk = v[k];
-        adam_one(pk, g[k], mk, vk, c);
-        p[k] = pk;
-        m[k] = mk;
-        v[k] = vk;
+    for (int k = 0; k < R; ++k) {
+      ri[k] = (lb * R + k) * rows_per_block + tid / q;
+      ok[k] = lane_ok && ri[k] < sg.n;
+      any |= ok[k];
+    }
+    if (!any) return;
+    int32_t row[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) row[k] = ok[k] ? sg.rows[ri[k]] : 0;
+    f4 p[R], g[R], m[R], v[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      if (!ok[k]) continue;
+      base[k] = (int64_t)row[k] * sg.row_len + part * 4;
+      sbase[k] = ri[k] * sg.row_len + part * 4;
+      gbase[k] = sg.grad_rows ? sbase[k] : base[k];
+      p[k] = *reinterpret_cast<const f4*>(sg.param + base[k]);
+      g[k] = *reinterpret_cast<const f4*>(sg.grad + gbase[k]);
+      m[k] = *reinterpret_cast<const f4*>(sg.exp_avg + sbase[k]);
+      v[k] = *reinterpret_cast<const f4*>(sg.exp_avg_sq + sbase[k]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const AdamCoef c = coef();
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      if (!ok[k]) continue;
+#pragma unroll
+      for (int l = 0; l < 4; ++l) {
+        float pk = p[k][l], mk = m[k][l], vk = v[k][l];
+        adam_one(pk, g[k][l], mk, vk, c);
+        p[k][l] = pk;
+        m[k][l] = mk;
+        v[k][l] = vk;
       }
-      *reinterpret_cast<f4*>(sg.param + base) = p;
-      *reinterpret_cast<f4*>(sg.exp_avg + sbase) = m;
-      *reinterpret_cast<f4*>(sg.exp_avg_sq + sbase) = v;
-      if (zero_grad) *reinterpret_cast<f4*>(sg.grad + gbase) = f4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<f4*>(sg.param + base[k]) = p[k];
+      *reinterpret_cast<f4*>(sg.exp_avg + sbase[k]) = m[k];
+      *reinterpret_cast<f4*>(sg.exp_avg_sq + sbase[k]) = v[k];
+      if (zero_grad) *reinterpret_cast<f4*>(sg.grad + gbase[k]) = f4{0.f, 0.f, 0.f, 0.f};
     }
   }
 }
 
-// workgroups of `nthreads` threads a segment's update takes (adam_segment_block)
+// workgroups of `nthreads` threads (R items each) a segment's update takes (adam_segment_block)
+template <int R>
 __host__ __device__ inline int64_t adam_segment_blocks(const nslam_adam_seg& sg, int nthreads) {
   if (sg.rows) {
-    const int64_t rpb = nthreads / (sg.row_len / 4);
+    const int64_t rpb = (int64_t)(nthreads / (sg.row_len / 4)) * R;
     return (sg.n + rpb - 1) / rpb;
   }
-  return (sg.n + nthreads - 1) / nthreads;
+  const int64_t per = (int64_t)nthreads * R;
+  return (sg.n + per - 1) / per;
 }

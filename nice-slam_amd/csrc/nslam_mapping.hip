@@ -175,7 +175,7 @@ struct AdamArgs {
 };
 
 constexpr int kAdamThreads = 256;
-constexpr int kDensePerBlock = kAdamThreads;  // one float per thread (dense segments are small)
+constexpr int kAdamItems = 4;  // float4 rows (or floats) per thread: 4 x 4 loads in flight
 
 // the element update and its coefficients: adam_coef / adam_one (nslam_dev.h)
 __global__ __launch_bounds__(kAdamThreads) void k_adam(AdamArgs a) {
@@ -184,7 +184,7 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam(AdamArgs a) {
   while (s + 1 < a.nseg && b >= a.blk0[s + 1]) ++s;
   const nslam_adam_seg& sg = a.seg[s];
   const float step = *sg.step;
-  adam_segment_block(
+  adam_segment_block<kAdamItems>(
       sg, [&] { return adam_coef(a.b1, a.b2, a.eps, sg.lr, step); }, b - a.blk0[s], a.zero_grad, (int)threadIdx.x,
       kAdamThreads);
   if (a.ticket) {
@@ -337,11 +337,8 @@ extern "C" int nslam_adam_step(const nslam_adam_seg* segs, int32_t n_segs, float
       if (g.row_len <= 0 || g.row_len % 4 || g.row_len / 4 > kAdamThreads) return NSLAM_EINVAL;
       const uintptr_t al = (uintptr_t)g.param | (uintptr_t)g.grad | (uintptr_t)g.exp_avg | (uintptr_t)g.exp_avg_sq;
       if (al & 15) return NSLAM_EINVAL;
-      const int64_t rpb = kAdamThreads / (g.row_len / 4);
-      blocks += (g.n + rpb - 1) / rpb;
-    } else {
-      blocks += (g.n + kDensePerBlock - 1) / kDensePerBlock;
     }
+    blocks += adam_segment_blocks<kAdamItems>(g, kAdamThreads);
   }
   a.blk0[n_segs] = blocks;
   a.nseg = n_segs;

@@ -13,8 +13,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, REPO)
 import bench  # noqa: E402
 
-SETTINGS = {
+SETTINGS = {  # engine attributes, or "bench.X" for bench.py module knobs
     "default": {},
+    "no_prefetch": {"bench.PREFETCH": False},
     "lean_first": {"wgrad_first": False},
     "serial": {"concurrent": False},
 }
@@ -26,14 +27,17 @@ def main():
     dev = torch.device("cuda:0")
     scene = bench.Room0Scene(dev, 0, path="fused")
     eng = scene.engine
-    base = {k: getattr(eng, k) for s in SETTINGS.values() for k in s}
+    def owner(k):
+        return (bench, k[6:]) if k.startswith("bench.") else (eng, k)
+
+    base = {k: getattr(*owner(k)) for s in SETTINGS.values() for k in s}
     res = {k: [] for k in SETTINGS}
     for r in range(rounds):
         for name, knobs in SETTINGS.items():
             for k, v in base.items():
-                setattr(eng, k, v)
+                setattr(*owner(k), v)
             for k, v in knobs.items():
-                setattr(eng, k, v)
+                setattr(*owner(k), v)
             ms, mode = bench.graph_time(scene, scene.step, reps)
             res[name].append(ms)
             print(f"round {r} {name:12s} {ms:.4f} ms ({mode})", flush=True)
