@@ -166,39 +166,12 @@ struct FragPipe {
   Frag cur;
   __device__ __forceinline__ FragPipe(const float* pk_, int first, int lane_)
       : pk(pk_), lane(lane_), cur(load_frag(pk_ + first * NSLAM_FRAG, lane_)) {}
-  template <bool FENCE = true>
   __device__ __forceinline__ void gemm(f32x16& acc, const f32x16& x, int next) {
     Frag n = cur;
     if (next >= 0) n = load_frag(pk + next * NSLAM_FRAG, lane);
-    if (FENCE) __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_sched_barrier(0);
     gemm_frag(acc, cur, x);
     cur = n;
-  }
-};
-
-// FragPipe with one fragment of registers: the next GEMM's fragment replaces the current one a
-// quarter at a time, each quarter as soon as the MFMAs that read it have issued (every quarter still
-// has 12 MFMAs = 768 cycles to arrive before its first use).
-struct FragRoll {
-  const float* pk;
-  int lane;
-  Frag cur;
-  __device__ __forceinline__ FragRoll(const float* pk_, int first, int lane_)
-      : pk(pk_), lane(lane_), cur(load_frag(pk_ + first * NSLAM_FRAG, lane_)) {}
-  // FENCE: order the loads with sched_barriers; else the caller's sched_group_barriers place them
-  template <bool FENCE = true>
-  __device__ __forceinline__ void gemm(f32x16& acc, const f32x16& x, int next) {
-    const gptr_t<f32x4> f = as_global(reinterpret_cast<const f32x4*>(pk + (next < 0 ? 0 : next) * NSLAM_FRAG)) + lane * 4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int s = 4 * i; s < 4 * i + 4; ++s) acc = mfma32(cur.q[i][s & 3], x[s], acc);
-      if (next >= 0) {
-        if (FENCE) __builtin_amdgcn_sched_barrier(0);
-        cur.q[i] = f[i];
-        if (FENCE) __builtin_amdgcn_sched_barrier(0);
-      }
-    }
   }
 };
 

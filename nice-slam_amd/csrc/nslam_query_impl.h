@@ -328,61 +328,22 @@ __device__ __forceinline__ f32x16 xyz_forward(const float* __restrict__ pk, cons
 #undef PHF_
 }
 
-#ifndef NSLAM_FWD_PF
-// the decoder-parallel forward's GEMM chain: 1 each weight fragment loaded one GEMM ahead
-// (xyz_forward_pf), 2 + the next embedding block computed in the MFMAs' shadow, 0 xyz_forward
-#define NSLAM_FWD_PF 1
-#endif
-#ifndef NSLAM_FWD_ROLL
-#define NSLAM_FWD_ROLL 0  // FragRoll (one fragment of registers) instead of FragPipe (two)
-#endif
 // xyz_forward of the decoder-parallel forward (VLDS: the vector section in LDS), its 15 (NC = 1) or 20
 // (NC = 2) GEMMs as a FragPipe: each weight fragment is loaded while the previous GEMM runs, so no GEMM
 // waits for its fragment's L2 round trip.  The same products in the same order as xyz_forward.
-template <int NC, bool TAPE, bool ILV = (NSLAM_FWD_PF == 2)>
+template <int NC, bool TAPE>
 __device__ __forceinline__ f32x16 xyz_forward_pf(const float* __restrict__ pk, const f32x16 (&cin)[NC],
                                                  const float x[3], int lane, uint32_t m[5],
                                                  float* __restrict__ tape, const float* vs) {
   const XyzPack L{NC};
-#if NSLAM_FWD_ROLL || NSLAM_FWD_PF == 2
-  FragRoll fp(pk, L.L0(), lane);
-#else
   FragPipe fp(pk, L.L0(), lane);
-#endif
   f32x16 a = vec_tile(vs + (L.Bias(0) - L.V()), lane);
   f32x16 a3 = vec_tile(vs + (L.Bias(3) - L.V()), lane);
-  if constexpr (ILV) {
-    // the embedding block b+1 (sin(x B): ~370 VALU instructions per lane) computed in the shadow of
-    // block b's two GEMMs (32 MFMAs of 64 cycles): one scheduling region per block, each MFMA followed
-    // by a group of VALU instructions, each fragment quarter's load right after its last reader
-    f32x16 e = emb_tile<false, false>(vs + (L.FB() - L.V()), x, 0, lane);
 #pragma unroll
-    for (int b = 0; b < 3; ++b) {
-      __builtin_amdgcn_sched_barrier(0);
-      f32x16 en = e;
-      if (b < 2) en = emb_tile<false, false>(vs + (L.FB() - L.V()), x, b + 1, lane);
-      fp.template gemm<false>(a, e, L.L3() + b);
-      fp.template gemm<false>(a3, e, b < 2 ? L.L0() + b + 1 : L.FC(0, 0));
-      __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);  // B of block b+1 (LDS)
-#pragma unroll
-      for (int g = 0; g < 8; ++g) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 12, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // the next fragment's quarter g & 3
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      e = en;
-    }
-  } else {
-#pragma unroll
-    for (int b = 0; b < 3; ++b) {
-      const f32x16 e = emb_tile<false, false>(vs + (L.FB() - L.V()), x, b, lane);
-      fp.gemm(a, e, L.L3() + b);
-      fp.gemm(a3, e, b < 2 ? L.L0() + b + 1 : L.FC(0, 0));
-    }
+  for (int b = 0; b < 3; ++b) {
+    const f32x16 e = emb_tile<false, false>(vs + (L.FB() - L.V()), x, b, lane);
+    fp.gemm(a, e, L.L3() + b);
+    fp.gemm(a3, e, b < 2 ? L.L0() + b + 1 : L.FC(0, 0));
   }
   // fc_c.i (cin) with the next layer's first fragment after it
   auto fc = [&](int i, int next) {
@@ -1194,8 +1155,7 @@ __device__ __forceinline__ void fwd_part_middle(const QueryKArgs& a, const Pt& q
   const float* pk = a.c.packed[NSLAM_DEC_MIDDLE];
   const XyzPack L{1};
   const f32x16 cms[1] = {cm};
-  const f32x16 h4 = NSLAM_FWD_PF ? xyz_forward_pf<1, false>(pk, cms, q.x, lane, m, nullptr, vec)
-                                 : xyz_forward<1, false, true, false, true>(pk, cms, q.x, lane, m, nullptr, nullptr, vec);
+  const f32x16 h4 = xyz_forward_pf<1, false>(pk, cms, q.x, lane, m, nullptr, vec);
   save_masks(a, NSLAM_DEC_MIDDLE, tile, m, lane);
   float o = out_row(vec + (L.Wo() - L.V()), vec + (L.Bo() - L.V()), 0, h4, lane);
   if (!q.inside) o = 100.f;
@@ -1217,8 +1177,7 @@ __device__ __forceinline__ void fwd_part_fine(const QueryKArgs& a, const Pt& q, 
   PHASE(0, 3);
   const float* pk = a.c.packed[NSLAM_DEC_FINE];
   const XyzPack L{2};
-  const f32x16 h4 = NSLAM_FWD_PF ? xyz_forward_pf<2, false>(pk, cf, q.x, lane, m, nullptr, vec)
-                                 : xyz_forward<2, false, true, false, true>(pk, cf, q.x, lane, m, nullptr, nullptr, vec);
+  const f32x16 h4 = xyz_forward_pf<2, false>(pk, cf, q.x, lane, m, nullptr, vec);
   save_masks(a, NSLAM_DEC_FINE, tile, m, lane);
   float o = out_row(vec + (L.Wo() - L.V()), vec + (L.Bo() - L.V()), 0, h4, lane);
   if (!q.inside) o = 0.f;
@@ -1245,8 +1204,7 @@ __device__ __forceinline__ void fwd_part_color(const QueryKArgs& a, const Pt& q,
   const float* pk = a.c.packed[NSLAM_DEC_COLOR];
   const XyzPack L{1};
   float* tp = TAPE ? a.c.act_tape + tile * kTapeFloats : nullptr;
-  const f32x16 h4 = NSLAM_FWD_PF ? xyz_forward_pf<1, TAPE>(pk, cc, q.x, lane, m, tp, vec)
-                                 : xyz_forward<1, false, true, TAPE, true>(pk, cc, q.x, lane, m, nullptr, tp, vec);
+  const f32x16 h4 = xyz_forward_pf<1, TAPE>(pk, cc, q.x, lane, m, tp, vec);
   save_masks(a, NSLAM_DEC_COLOR, tile, m, lane);
   float o[3];
 #pragma unroll

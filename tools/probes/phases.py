@@ -66,14 +66,15 @@ def main():
     nwg = int((cw[:, 3] > 0).sum()) // 8
     if nwg:
         cw = cw[:nwg * 8].reshape(nwg, 8, 16)
-        roles = {0: "S_b dW3/dW0", 1: "S_b dW3/dW0", 2: "S_b dW3/dW0", 3: "feature+h2/dW2", 4: "fc_c+dB",
-                 5: "fc_c+dB", 6: "fc_c.2,dW4+dB", 7: "chain producer"}
+        roles = {0: "S_b dW3/dW0", 1: "S_b dW3/dW0", 2: "S_b dW3/dW0", 3: "feature+h2/dW2",
+                 4: "fc_c+dB", 5: "fc_c+dB", 6: "fc_c.2,dW4+dB", 7: "chain producer"}
+        perm = [(0x52104637 >> (4 * w)) & 15 for w in range(8)]  # k_color_wgrad's role of hardware wave w
         print(f"== k_color_wgrad: {nwg} workgroups, tiles per chunk median {np.median(cw[:, 0, 3]):.0f}")
         for wv in range(8):
             tp, tc, th = (np.median(cw[:, wv, k]) for k in range(3))
             tot = tp + tc + th
-            print(f"   wave {wv} {roles[wv]:>16s}: prod {tp:8.0f}  cons {tc:8.0f}  wait {th:8.0f}  "
-                  f"(wait {100 * th / max(tot, 1):5.1f}%)")
+            print(f"   hw wave {wv} (SIMD {wv % 4}) role {perm[wv]} {roles[perm[wv]]:>16s}: prod {tp:8.0f}  "
+                  f"cons {tc:8.0f}  wait {th:8.0f}  (wait {100 * th / max(tot, 1):5.1f}%)")
     for d, nm in ((1, "middle"), (2, "fine"), (3, "color")):
         t = buf[d, :tiles]
         marks = [k for k in range(16) if (t[:, k] != 0).all()]
