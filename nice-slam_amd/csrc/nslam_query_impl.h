@@ -331,7 +331,8 @@ __device__ __forceinline__ f32x16 xyz_forward(const float* __restrict__ pk, cons
 // xyz_forward of the decoder-parallel forward (VLDS: the vector section in LDS), its 15 (NC = 1) or 20
 // (NC = 2) GEMMs as a FragPipe: each weight fragment is loaded while the previous GEMM runs, so no GEMM
 // waits for its fragment's L2 round trip.  The same products in the same order as xyz_forward.
-template <int NC, bool TAPE>
+// (phases build: marks MK .. MK + 3 after the embedding GEMMs, layers 1-2, layer 3 and layer 4)
+template <int NC, bool TAPE, int MK = 5>
 __device__ __forceinline__ f32x16 xyz_forward_pf(const float* __restrict__ pk, const f32x16 (&cin)[NC],
                                                  const float x[3], int lane, uint32_t m[5],
                                                  float* __restrict__ tape, const float* vs) {
@@ -345,6 +346,7 @@ __device__ __forceinline__ f32x16 xyz_forward_pf(const float* __restrict__ pk, c
     fp.gemm(a, e, L.L3() + b);
     fp.gemm(a3, e, b < 2 ? L.L0() + b + 1 : L.FC(0, 0));
   }
+  PHASE(0, MK);
   // fc_c.i (cin) with the next layer's first fragment after it
   auto fc = [&](int i, int next) {
     f32x16 z = vec_tile(vs + (L.BiasC(i) - L.V()), lane);
@@ -365,15 +367,18 @@ __device__ __forceinline__ f32x16 xyz_forward_pf(const float* __restrict__ pk, c
   m[2] = mask16(a);
   h = relu16(a) + fc(2, L.L3() + 3);
   if (TAPE) tape_store(tape, 2, h, lane);
+  PHASE(0, MK + 1);
   fp.gemm(a3, h, L.FC(3, 0));
   m[3] = mask16(a3);
   h = relu16(a3) + fc(3, L.L4());
   if (TAPE) tape_store(tape, 3, h, lane);
+  PHASE(0, MK + 2);
   a = vec_tile(vs + (L.Bias(4) - L.V()), lane);
   fp.gemm(a, h, L.FC(4, 0));
   m[4] = mask16(a);
   h = relu16(a) + fc(4, -1);
   if (TAPE) tape_store(tape, 4, h, lane);
+  PHASE(0, MK + 3);
   return h;
 }
 
@@ -1198,13 +1203,13 @@ __device__ __forceinline__ void fwd_part_color(const QueryKArgs& a, const Pt& q,
   uint32_t m[5];
   Corners cr;
   grid_corners(cr, a.c.grid[NSLAM_DEC_COLOR], q);
-  PHASE(0, 2);
+  PHASE(0, 10);
   const f32x16 cc[1] = {gather_tile(a.c.grid[NSLAM_DEC_COLOR].data, cr, lane)};
-  PHASE(0, 3);
+  PHASE(0, 11);
   const float* pk = a.c.packed[NSLAM_DEC_COLOR];
   const XyzPack L{1};
   float* tp = TAPE ? a.c.act_tape + tile * kTapeFloats : nullptr;
-  const f32x16 h4 = xyz_forward_pf<1, TAPE>(pk, cc, q.x, lane, m, tp, vec);
+  const f32x16 h4 = xyz_forward_pf<1, TAPE, 12>(pk, cc, q.x, lane, m, tp, vec);
   save_masks(a, NSLAM_DEC_COLOR, tile, m, lane);
   float o[3];
 #pragma unroll

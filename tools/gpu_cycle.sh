@@ -1,7 +1,7 @@
 # One GPU measurement cycle.  usage (via gpurun): bash tools/gpu_cycle.sh TAG [steps...]
 # steps (default: tests bench prof): tests | tests-fast (fused+parity only) | bench | bench-quick
 # (no baselines / stress / side legs) | eager | gloo2 (2-rank gloo rehearsal of the sharded bench)
-# | prof (rocprofv3 kernel stats) | trace (timeline of one replayed iteration) | phases
+# | gloo2ar (the same with --exchange allreduce) | prof (rocprofv3 kernel stats) | trace (timeline of one replayed iteration) | phases
 # (s_memtime phase breakdown of the backward waves; needs `make -C nice-slam_amd/csrc phases`).
 # Every GPU step runs under its own timeout; the first failure ends the script.
 set -o pipefail
@@ -34,6 +34,9 @@ for s in $STEPS; do
     gloo2)
       timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 20 --warmup 5 --backend gloo > $OUT/bench_gloo2.json 2> $OUT/bench_gloo2.err || { tail -30 $OUT/bench_gloo2.err; stop gloo2 1; }
       summ $OUT/bench_gloo2.json gloo2 ;;
+    gloo2ar)  # the same rehearsal with the all-reduce exchange (replicated Adam)
+      timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --backend gloo --exchange allreduce > $OUT/bench_gloo2_allreduce.json 2> $OUT/bench_gloo2_allreduce.err || { tail -30 $OUT/bench_gloo2_allreduce.err; stop gloo2ar 1; }
+      summ $OUT/bench_gloo2_allreduce.json gloo2ar ;;
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-stress --no-bulk > $OUT/prof.log 2>&1 || { tail -20 $OUT/prof.log; stop prof 1; }
       python tools/prof_summary.py $OUT/prof > $OUT/kernels.md 2>&1 && head -30 $OUT/kernels.md ;;

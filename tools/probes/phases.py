@@ -38,17 +38,19 @@ def main():
     buf = buf.reshape(5, W, 16).astype(np.int64)
     tiles = (scene.cfg["pixels"] * 48 + 31) // 32
     fwd_names = {0: "start", 1: "point", 2: "corners", 3: "gather", 5: "emb+L0+L3e", 6: "L1+L2", 7: "L3", 8: "L4",
-                 9: "out+store"}
+                 9: "out+store", 10: "c.corners", 11: "c.gather", 12: "c.emb+L0+L3e", 13: "c.L1+L2", 14: "c.L3",
+                 15: "c.L4"}
     print("nonzero marks per slot:", [int((buf[k] != 0).sum()) for k in range(5)])
     # room0 colour stage: the 2-part forward (middle then colour | fine), parts alternating along
-    # blockIdx / 8 (XCD-aware mapping, k_query_fwd_parts); 4 waves per workgroup
+    # blockIdx (k_query_fwd_parts); 4 waves per workgroup
     groups = (tiles + 3) // 4
-    nw = (groups + 7) // 8 * 8 * 2 * 4
+    nw = groups * 2 * 4
     t = buf[0, :nw]
-    part = ((np.arange(nw) // 4) // 8) % 2
+    part = (np.arange(nw) // 4) % 2
     for pi, nm in ((0, "middle then colour"), (1, "fine")):
         tp = t[(part == pi) & (t[:, 0] != 0)]
         marks = [k for k in range(16) if (tp[:, k] != 0).all()]
+        marks.sort(key=lambda k: np.median(tp[:, k] - tp[:, 0]))  # in time order (part 0: middle, then colour)
         tot = tp[:, marks[-1]] - tp[:, marks[0]]
         print(f"== forward part {nm}: {len(tp)} waves, marks {marks}; wave total median {np.median(tot):.0f} "
               f"p10 {np.percentile(tot, 10):.0f} p90 {np.percentile(tot, 90):.0f}")
