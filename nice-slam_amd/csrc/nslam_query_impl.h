@@ -67,6 +67,93 @@ __device__ __forceinline__ void grid_corners(Corners& cr, const nslam_grid& g, c
   make_corners(cr, nc3, g.dims);
 }
 
+// The trilinear cell of a point in one grid, corners formed on demand (make_corners' rows and weights,
+// the same arithmetic): 10 values per lane instead of a Corners struct's 8 rows + 8 weights.
+struct LazyCell {
+  int row0, nx, nxy;
+  float f0[3], f1[3];
+  bool hi_ok[3];
+  __device__ __forceinline__ LazyCell(const nslam_grid& g, const Pt& q) {
+    const int n[3] = {g.dims[2], g.dims[1], g.dims[0]};  // x→W, y→H, z→D
+    int i0[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      float gm;
+      const float u = unnorm_clip(norm_coord(q.p[a], g.lo[a], g.hi[a]), n[a], gm);
+      const float fl = floorf(u);
+      i0[a] = (int)fl;
+      f1[a] = u - fl;
+      f0[a] = (float)(i0[a] + 1) - u;
+      hi_ok[a] = (i0[a] + 1) <= n[a] - 1;
+    }
+    nx = n[0];
+    nxy = n[1] * n[0];
+    row0 = (i0[2] * n[1] + i0[1]) * n[0] + i0[0];
+  }
+  // corner k's row (0 when out of range) and weight (exactly 0 when out of range)
+  __device__ __forceinline__ int row(int k, float& w) const {
+    const int dx = k & 1, dy = (k >> 1) & 1, dz = k >> 2;
+    const bool ok = (!dx || hi_ok[0]) && (!dy || hi_ok[1]) && (!dz || hi_ok[2]);
+    const float wr = ((dx ? f1[0] : f0[0]) * (dy ? f1[1] : f0[1])) * (dz ? f1[2] : f0[2]);
+    w = ok ? wr : 0.f;
+    return (row0 + dz * nxy + dy * nx + dx) & -(int)ok;  // (a select, not a branch)
+  }
+};
+
+// Two trilinear gathers (the fine decoder's fine and middle features, decoder.py:184-187) software-
+// pipelined corner by corner: corner k + 1's rows of both grids are loaded while corner k is summed, so
+// 16 row loads per lane are in flight and no corner waits for a full round trip after the previous one.
+// Each feature sums its corners in gather_tile's order (the same values).
+__device__ __forceinline__ void gather_pair(const nslam_grid& gA, const nslam_grid& gB, const Pt& q, int lane,
+                                            f32x16& accA, f32x16& accB) {
+  const int h = lane >> 5;
+  const LazyCell A(gA, q), B(gB, q);
+  accA = zero16();
+  accB = zero16();
+  auto load = [&](const LazyCell& L, const float* data, int k, f32x4 (&v)[4], float& w) {
+    const gptr_t<f32x4> rp =
+        as_global(reinterpret_cast<const f32x4*>(data + (size_t)(uint32_t)L.row(k, w) * NSLAM_C_DIM + 4 * h));
+    v[0] = rp[0];
+    v[1] = rp[2];
+    v[2] = rp[4];
+    v[3] = rp[6];
+  };
+  f32x4 va[4], vb[4];
+  float wa, wb;
+  load(A, gA.data, 0, va, wa);
+  load(B, gB.data, 0, vb, wb);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    f32x4 na[4], nb[4];
+    float nwa = 0.f, nwb = 0.f;
+    if (k < 7) {
+      load(A, gA.data, k + 1, na, nwa);
+      load(B, gB.data, k + 1, nb, nwb);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // the next corner's loads are issued before this one is summed
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      accA[j] += va[0][j] * wa;
+      accA[4 + j] += va[1][j] * wa;
+      accA[8 + j] += va[2][j] * wa;
+      accA[12 + j] += va[3][j] * wa;
+      accB[j] += vb[0][j] * wb;
+      accB[4 + j] += vb[1][j] * wb;
+      accB[8 + j] += vb[2][j] * wb;
+      accB[12 + j] += vb[3][j] * wb;
+    }
+    if (k < 7) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        va[i] = na[i];
+        vb[i] = nb[i];
+      }
+      wa = nwa;
+      wb = nwb;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Fourier embedding (decoder.py:26-30): block b, reg r of lane (h,p) is dim k = 32b + F(r,h)
 // ------------------------------------------------------------------------------------------
@@ -1148,15 +1235,12 @@ __global__ __launch_bounds__(256, 2) void k_query_fwd(QueryKArgs a) {
 // and k_occ_combine then forms raw[p][3] = fine_occ + middle_occ (decoder.py:331-334, the
 // reference's operand order) — exactly 100 outside the bound (0 + 100; Renderer.py:57).
 // One decoder of the decoder-parallel forward for this wave's tile.
-__device__ __forceinline__ void fwd_part_middle(const QueryKArgs& a, const Pt& q, int64_t tile, int64_t idx, int lane,
-                                                float* __restrict__ occ_mid, const float* vec) {
+// the middle decoder's chain and output for this wave's tile from its gathered feature cm
+__device__ __forceinline__ void fwd_middle_chain(const QueryKArgs& a, const Pt& q, int64_t tile, int64_t idx,
+                                                 int lane, float* __restrict__ occ_mid, const float* vec,
+                                                 const f32x16& cm) {
   const int h = lane >> 5;
   uint32_t m[5];
-  Corners cr;
-  grid_corners(cr, a.c.grid[NSLAM_DEC_MIDDLE], q);
-  PHASE(0, 2);
-  const f32x16 cm = gather_tile(a.c.grid[NSLAM_DEC_MIDDLE].data, cr, lane);
-  PHASE(0, 3);
   const float* pk = a.c.packed[NSLAM_DEC_MIDDLE];
   const XyzPack L{1};
   const f32x16 cms[1] = {cm};
@@ -1166,6 +1250,15 @@ __device__ __forceinline__ void fwd_part_middle(const QueryKArgs& a, const Pt& q
   if (!q.inside) o = 100.f;
   if (h == 0 && q.valid) occ_mid[idx] = o;
 }
+__device__ __forceinline__ void fwd_part_middle(const QueryKArgs& a, const Pt& q, int64_t tile, int64_t idx, int lane,
+                                                float* __restrict__ occ_mid, const float* vec) {
+  Corners cr;
+  grid_corners(cr, a.c.grid[NSLAM_DEC_MIDDLE], q);
+  PHASE(0, 2);
+  const f32x16 cm = gather_tile(a.c.grid[NSLAM_DEC_MIDDLE].data, cr, lane);
+  PHASE(0, 3);
+  fwd_middle_chain(a, q, tile, idx, lane, occ_mid, vec, cm);
+}
 
 template <int STAGE>
 __device__ __forceinline__ void fwd_part_fine(const QueryKArgs& a, const Pt& q, int64_t tile, int64_t idx, int lane,
@@ -1173,12 +1266,9 @@ __device__ __forceinline__ void fwd_part_fine(const QueryKArgs& a, const Pt& q, 
   // the fine decoder also reads the middle feature (decoder.py:184-187)
   const int h = lane >> 5;
   uint32_t m[5];
-  Corners cm, cr;
-  grid_corners(cm, a.c.grid[NSLAM_DEC_MIDDLE], q);
-  grid_corners(cr, a.c.grid[NSLAM_DEC_FINE], q);
   PHASE(0, 2);
-  const f32x16 cf[2] = {gather_tile(a.c.grid[NSLAM_DEC_FINE].data, cr, lane),
-                        gather_tile(a.c.grid[NSLAM_DEC_MIDDLE].data, cm, lane)};
+  f32x16 cf[2];
+  gather_pair(a.c.grid[NSLAM_DEC_FINE], a.c.grid[NSLAM_DEC_MIDDLE], q, lane, cf[0], cf[1]);
   PHASE(0, 3);
   const float* pk = a.c.packed[NSLAM_DEC_FINE];
   const XyzPack L{2};
@@ -1196,20 +1286,17 @@ __device__ __forceinline__ void fwd_part_fine(const QueryKArgs& a, const Pt& q, 
   }
 }
 
+// the colour decoder's chain (+ activation tape) and outputs for this wave's tile from its feature cc
 template <bool TAPE>
-__device__ __forceinline__ void fwd_part_color(const QueryKArgs& a, const Pt& q, int64_t tile, int64_t idx, int lane,
-                                               const float* vec) {
+__device__ __forceinline__ void fwd_color_chain(const QueryKArgs& a, const Pt& q, int64_t tile, int64_t idx,
+                                                int lane, const float* vec, const f32x16& cc) {
   const int h = lane >> 5;
   uint32_t m[5];
-  Corners cr;
-  grid_corners(cr, a.c.grid[NSLAM_DEC_COLOR], q);
-  PHASE(0, 10);
-  const f32x16 cc[1] = {gather_tile(a.c.grid[NSLAM_DEC_COLOR].data, cr, lane)};
-  PHASE(0, 11);
   const float* pk = a.c.packed[NSLAM_DEC_COLOR];
   const XyzPack L{1};
   float* tp = TAPE ? a.c.act_tape + tile * kTapeFloats : nullptr;
-  const f32x16 h4 = xyz_forward_pf<1, TAPE, 12>(pk, cc, q.x, lane, m, tp, vec);
+  const f32x16 ccs[1] = {cc};
+  const f32x16 h4 = xyz_forward_pf<1, TAPE, 12>(pk, ccs, q.x, lane, m, tp, vec);
   save_masks(a, NSLAM_DEC_COLOR, tile, m, lane);
   float o[3];
 #pragma unroll
@@ -1218,6 +1305,16 @@ __device__ __forceinline__ void fwd_part_color(const QueryKArgs& a, const Pt& q,
 #pragma unroll
     for (int j = 0; j < 3; ++j) a.raw[idx * 4 + j] = o[j];
   }
+}
+template <bool TAPE>
+__device__ __forceinline__ void fwd_part_color(const QueryKArgs& a, const Pt& q, int64_t tile, int64_t idx, int lane,
+                                               const float* vec) {
+  Corners cr;
+  grid_corners(cr, a.c.grid[NSLAM_DEC_COLOR], q);
+  PHASE(0, 10);
+  const f32x16 cc = gather_tile(a.c.grid[NSLAM_DEC_COLOR].data, cr, lane);
+  PHASE(0, 11);
+  fwd_color_chain<TAPE>(a, q, tile, idx, lane, vec, cc);
 }
 
 // Decoder-parallel forward (fine and colour stages): each workgroup evaluates ONE part for its 4
