@@ -965,14 +965,11 @@ __device__ __forceinline__ void stage_walk_table(float* __restrict__ tab, const 
   }
 }
 
-// Step codes of the walk (NSLAM_WALK_CODES, default): every lane evaluates, in parallel before the
+// Step codes of the walk: every lane evaluates, in parallel before the
 // walk, what the step from point p-1's cell to point p's does — bit 8: the cell changes; bit 4 hh + j:
 // voxel (hh, j) of the previous cell is kept (a neighbouring-cell step).  The walk itself then
 // reads one code per point (v_readlane) instead of deriving the steps' axis deltas and parities on the
 // scalar unit point after point (~3k SALU instructions per tile, shared by the CU's waves).
-#ifndef NSLAM_WALK_CODES
-#define NSLAM_WALK_CODES 1
-#endif
 __device__ __forceinline__ int walk_code(int cellk, int lane) {
   const int p = lane & 31;
   const int prev = __shfl(cellk, (lane & 32) | ((p + 31) & 31), 64);  // point p - 1 (same half)
@@ -997,6 +994,7 @@ __device__ __forceinline__ int walk_code(int cellk, int lane) {
   return code;
 }
 
+template <bool STAGED = false>  // STAGED: the caller wrote the walk table already
 __device__ __forceinline__ void scatter_grid_grad_uniform(float* __restrict__ grad, const ScatterCorners& sc,
                                                           int cellk, const f32x16& dc, float* __restrict__ img,
                                                           float* __restrict__ tab, int lane) {
@@ -1010,11 +1008,8 @@ __device__ __forceinline__ void scatter_grid_grad_uniform(float* __restrict__ gr
   // table, and the cotangent column of channel ch from one LDS transpose of dc.
   const int h = lane >> 5, ch = lane & 31;
   tstore(img, dc, lane);
-  stage_walk_table(tab, sc, cellk, lane);
+  if (!STAGED) stage_walk_table(tab, sc, cellk, lane);
   lds_sync();
-  float vcol[32];
-#pragma unroll
-  for (int t = 0; t < 32; ++t) vcol[t] = img[t * TPITCH + ch];
   const f32x4* wt = reinterpret_cast<const f32x4*>(tab) + h;        // (t, h) at wt[2 t]
   const i32x4* rt = reinterpret_cast<const i32x4*>(tab + 256) + h;  // (t, h) at rt[2 t]
   float acc[4], wsum[4];
@@ -1025,11 +1020,11 @@ __device__ __forceinline__ void scatter_grid_grad_uniform(float* __restrict__ gr
     wsum[j] = 0.f;
     rows[j] = 0;
   }
-#if NSLAM_WALK_CODES
   const int codes = walk_code(cellk, lane);
 #pragma unroll
   for (int t = 0; t < 32; ++t) {
     const int code = __builtin_amdgcn_readlane(codes, t);
+    const float vc = img[t * TPITCH + ch];
     const f32x4 w = wt[2 * t];
     const i32x4 nr = rt[2 * t];
     if (code & 0x100) {  // wave-uniform: the walk steps to another cell
@@ -1046,50 +1041,10 @@ __device__ __forceinline__ void scatter_grid_grad_uniform(float* __restrict__ gr
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      acc[j] += w[j] * vcol[t];
+      acc[j] += w[j] * vc;
       wsum[j] += w[j];
     }
   }
-#else
-  int cur = -1;
-#pragma unroll
-  for (int t = 0; t < 32; ++t) {
-    const int cell = __builtin_amdgcn_readlane(cellk, t);
-    const f32x4 w = wt[2 * t];
-    const i32x4 nr = rt[2 * t];
-    if (cell != cur) {  // wave-uniform
-      // a voxel of the old cell at offset d (0/1) along an axis stays in the new cell iff the step
-      // a along that axis is 0, or +1 with d == 1, or -1 with d == 0; d = register parity ^ cell parity
-      int ax = 2, ay = 2, az = 2, px = 0, py = 0, pz = 0;
-      if (cur >= 0) {
-        ax = (cell & 1023) - (cur & 1023);
-        ay = ((cell >> 10) & 1023) - ((cur >> 10) & 1023);
-        az = (cell >> 20) - (cur >> 20);
-        px = cur & 1;
-        py = (cur >> 10) & 1;
-        pz = (cur >> 20) & 1;
-      }
-      const bool kx = ax == 0 || (ax == 1 && (h ^ px) == 1) || (ax == -1 && (h ^ px) == 0);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int dy = (j & 1) ^ py, dz = (j >> 1) ^ pz;
-        const bool ky = ay == 0 || (ay == 1 && dy == 1) || (ay == -1 && dy == 0);
-        const bool kz = az == 0 || (az == 1 && dz == 1) || (az == -1 && dz == 0);
-        const bool keep = kx && ky && kz;
-        if (!keep && wsum[j] != 0.f) grid_add(grad + (size_t)rows[j] * NSLAM_C_DIM + ch, acc[j]);
-        acc[j] = keep ? acc[j] : 0.f;
-        wsum[j] = keep ? wsum[j] : 0.f;
-        rows[j] = nr[j];
-      }
-      cur = cell;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      acc[j] += w[j] * vcol[t];
-      wsum[j] += w[j];
-    }
-  }
-#endif
 #pragma unroll
   for (int j = 0; j < 4; ++j)
     if (wsum[j] != 0.f) grid_add(grad + (size_t)rows[j] * NSLAM_C_DIM + ch, acc[j]);
@@ -1441,6 +1396,9 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
   if (SAVED) {  // masks from the forward: no recompute (the mask-only chain)
     uint32_t m[5];
     load_masks(a, DEC, tile, m, lane);
+    // the walk table goes to LDS before the chain (its corner rows and weights need no registers
+    // through it); the slot loads were issued before the masks, so this waits for nothing extra
+    if (WG == 0 && gr.grad) stage_walk_table(S.sA + TILE_FLOATS, scn, cr.cell, lane);
     if (DEC == NSLAM_DEC_COARSE) {
       noxyz_backward_saved(pk, m, g[3], lane, dc);
     } else if (DEC == NSLAM_DEC_FINE) {
@@ -1472,7 +1430,7 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
     if (WG) {
       scatter_grid_grad_halves(gr.grad, gr.slot, cr, dc, q.valid, S, lane);
     } else {  // walk table: the lean kernels' slot after the transpose image
-      scatter_grid_grad_uniform(gr.grad, scn, cr.cell, dc, S.sA, S.sA + TILE_FLOATS, lane);
+      scatter_grid_grad_uniform<SAVED>(gr.grad, scn, cr.cell, dc, S.sA, S.sA + TILE_FLOATS, lane);
     }
   }
   PHASE(DEC, 13);
@@ -1554,8 +1512,18 @@ struct MultiDecArgs {
 };
 // (a colour decoder with weight gradients runs here as its lean chain too: grid gradient, d/dpts;
 // its parameter gradients come from k_color_wgrad, nslam_color_wgrad.hip)
+// Register bound of the mapping (no d/dpts) variant: 4 waves/SIMD -> 106 VGPRs (the walk table staged
+// before the chain frees its corner registers).  A/B on one box, 3 alternating rounds (r4t): 0.2287 ms
+// per iteration at the old 2-wave bound (115 VGPRs), 0.2208 ms at 4, 0.2260 ms at 5 (96 VGPRs: one
+// resident round for room0's 4500 waves, but the standalone launch only 1 % shorter than at 4).
+#ifndef NSLAM_MULTI_LB
+#define NSLAM_MULTI_LB 4
+#endif
+#ifndef NSLAM_MULTI_PG_LB
+#define NSLAM_MULTI_PG_LB 2  // the d/dpts (tracking) variant: 218 VGPRs; 3 or 4 waves/SIMD spill
+#endif
 template <bool PG>
-__global__ __launch_bounds__(64 * kWavesBwd, 2) void k_dec_bwd_multi(QueryKArgs a, MultiDecArgs m) {
+__global__ __launch_bounds__(64 * kWavesBwd, PG ? NSLAM_MULTI_PG_LB : NSLAM_MULTI_LB) void k_dec_bwd_multi(QueryKArgs a, MultiDecArgs m) {
   constexpr int kScr = TILE_FLOATS + kWalkFloats;
   __shared__ __attribute__((aligned(16))) float lds[kWavesBwd * kScr];
   const int lane = threadIdx.x & 63, wave = wave_id();
