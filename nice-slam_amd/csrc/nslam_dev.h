@@ -142,6 +142,32 @@ __device__ __forceinline__ void gemm_acc(f32x16& acc, const float* __restrict__ 
   acc = mfma32(a3[3], x[15], acc);
 }
 
+// acc += (W^T X) TRANSPOSED: the backward fragment W[F(s,h)][k] as the B operand and the C-layout tile X
+// (lane (p, h), register s = X[p][F(s, h)]) as the A operand, so D[i = point][j = k] = Σ_o X[p][o] W[o][k]
+// lands as lane (k, h') register r = point F(r, h') — the MFMA with its operands swapped
+__device__ __forceinline__ void gemm_acc_t(f32x16& acc, const float* __restrict__ frag, const f32x16& x, int lane) {
+  const gptr_t<f32x4> f = as_global(reinterpret_cast<const f32x4*>(frag)) + lane * 4;
+  const f32x4 a0 = f[0], a1 = f[1], a2 = f[2], a3 = f[3];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) acc = mfma32(x[k], a0[k], acc);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) acc = mfma32(x[4 + k], a1[k], acc);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) acc = mfma32(x[8 + k], a2[k], acc);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) acc = mfma32(x[12 + k], a3[k], acc);
+}
+
+// acc += Wblock * X in the C layout (TR false) or its transpose (TR true: gemm_acc_t)
+template <bool TR>
+__device__ __forceinline__ void gemm_acc_tr(f32x16& acc, const float* __restrict__ frag, const f32x16& x, int lane) {
+  if (TR)
+    gemm_acc_t(acc, frag, x, lane);
+  else
+    gemm_acc(acc, frag, x, lane);
+}
+
+
 // A weight fragment (16 floats per lane) held in registers, so a GEMM's fragment can be in flight
 // while the previous GEMM runs
 struct Frag {

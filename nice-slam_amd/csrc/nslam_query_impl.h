@@ -787,10 +787,14 @@ __device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, con
 // dh_{i-1} = L_iT mask_i(dh_i) (layer 3 through its hidden block); EMBG adds d/dx through the
 // Fourier features from mask_3(dh_3) and mask_0(dh_0).
 // ------------------------------------------------------------------------------------------
-template <int NC, int NOUT, int GOFS, bool EMBG>
+// TR: dc is formed transposed (lane (c, h) register r = channel c of point F(r, h); gemm_acc_t), the
+// layout the lean scatter walk consumes without an LDS transpose (only without EMBG: coord_grad
+// reads the C layout)
+template <int NC, int NOUT, int GOFS, bool EMBG, bool TR = false>
 __device__ __forceinline__ void xyz_backward_saved(const float* __restrict__ pk, const uint32_t m[5],
                                                    const float x[3], const float (&gall)[4], int lane, f32x16& dc,
                                                    float gx[3]) {
+  static_assert(!(TR && EMBG), "d/dpts needs dc in the C layout");
   const XyzPack L{NC};
   const int h = lane >> 5;
   f32x16 dh = zero16();
@@ -801,23 +805,23 @@ __device__ __forceinline__ void xyz_backward_saved(const float* __restrict__ pk,
     for (int r = 0; r < 16; ++r) dh[r] += w[r] * gall[GOFS + j];
   }
   dc = zero16();
-  gemm_acc(dc, pk + L.FCT(4) * NSLAM_FRAG, dh, lane);
+  gemm_acc_tr<TR>(dc, pk + L.FCT(4) * NSLAM_FRAG, dh, lane);
   f32x16 da = apply_mask(dh, m[4]);
   dh = zero16();
   gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
-  gemm_acc(dc, pk + L.FCT(3) * NSLAM_FRAG, dh, lane);
+  gemm_acc_tr<TR>(dc, pk + L.FCT(3) * NSLAM_FRAG, dh, lane);
   const f32x16 da3 = apply_mask(dh, m[3]);
   dh = zero16();
   gemm_acc(dh, pk + (L.L3T() + 3) * NSLAM_FRAG, da3, lane);
-  gemm_acc(dc, pk + L.FCT(2) * NSLAM_FRAG, dh, lane);
+  gemm_acc_tr<TR>(dc, pk + L.FCT(2) * NSLAM_FRAG, dh, lane);
   da = apply_mask(dh, m[2]);
   dh = zero16();
   gemm_acc(dh, pk + L.L2T() * NSLAM_FRAG, da, lane);
-  gemm_acc(dc, pk + L.FCT(1) * NSLAM_FRAG, dh, lane);
+  gemm_acc_tr<TR>(dc, pk + L.FCT(1) * NSLAM_FRAG, dh, lane);
   da = apply_mask(dh, m[1]);
   dh = zero16();
   gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
-  gemm_acc(dc, pk + L.FCT(0) * NSLAM_FRAG, dh, lane);
+  gemm_acc_tr<TR>(dc, pk + L.FCT(0) * NSLAM_FRAG, dh, lane);
   gx[0] = gx[1] = gx[2] = 0.f;
   if (EMBG) {
     da = apply_mask(dh, m[0]);
@@ -848,6 +852,7 @@ __device__ __forceinline__ void xyz_backward_saved(const float* __restrict__ pk,
   }
 }
 
+template <bool TR = false>
 __device__ __forceinline__ void noxyz_backward_saved(const float* __restrict__ pk, const uint32_t m[5], float g,
                                                      int lane, f32x16& dc) {
   const NoXyzPack L;
@@ -862,7 +867,7 @@ __device__ __forceinline__ void noxyz_backward_saved(const float* __restrict__ p
   dh = zero16();
   gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
   da = apply_mask(dh, m[3]);
-  gemm_acc(dc, pk + L.L3T() * NSLAM_FRAG, da, lane);
+  gemm_acc_tr<TR>(dc, pk + L.L3T() * NSLAM_FRAG, da, lane);
   dh = zero16();
   gemm_acc(dh, pk + (L.L3T() + 1) * NSLAM_FRAG, da, lane);
   da = apply_mask(dh, m[2]);
@@ -872,7 +877,7 @@ __device__ __forceinline__ void noxyz_backward_saved(const float* __restrict__ p
   dh = zero16();
   gemm_acc(dh, pk + L.L1T() * NSLAM_FRAG, da, lane);
   da = apply_mask(dh, m[0]);
-  gemm_acc(dc, pk + L.L0T() * NSLAM_FRAG, da, lane);
+  gemm_acc_tr<TR>(dc, pk + L.L0T() * NSLAM_FRAG, da, lane);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -994,7 +999,10 @@ __device__ __forceinline__ int walk_code(int cellk, int lane) {
   return code;
 }
 
-template <bool STAGED = false>  // STAGED: the caller wrote the walk table already
+// STAGED: the caller wrote the walk table already.  TR: dc arrives transposed (xyz_backward_saved<..., TR>):
+// lane (ch, h) holds channel ch of points F(r, h), and one v_permlane32_swap per register hands every
+// lane both halves' points — the walk's cotangent columns straight from registers, no LDS image.
+template <bool STAGED = false, bool TR = false>
 __device__ __forceinline__ void scatter_grid_grad_uniform(float* __restrict__ grad, const ScatterCorners& sc,
                                                           int cellk, const f32x16& dc, float* __restrict__ img,
                                                           float* __restrict__ tab, int lane) {
@@ -1007,7 +1015,20 @@ __device__ __forceinline__ void scatter_grid_grad_uniform(float* __restrict__ gr
   // v_readlane (it steers the uniform branch), weights and rows by broadcast LDS reads of the walk
   // table, and the cotangent column of channel ch from one LDS transpose of dc.
   const int h = lane >> 5, ch = lane & 31;
-  tstore(img, dc, lane);
+  float vlo[16], vhi[16];  // TR: channel ch of point F(r, 0) / F(r, 1)
+  if (TR) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      // (through a scalar: clang's __builtin_bit_cast of a vector-element lvalue reads element 0)
+      const float d = dc[r];
+      const unsigned u = __builtin_bit_cast(unsigned, d);
+      const auto sw = __builtin_amdgcn_permlane32_swap(u, u, false, false);  // {lower half's, upper half's}
+      vlo[r] = __builtin_bit_cast(float, (unsigned)sw[0]);
+      vhi[r] = __builtin_bit_cast(float, (unsigned)sw[1]);
+    }
+  } else {
+    tstore(img, dc, lane);
+  }
   if (!STAGED) stage_walk_table(tab, sc, cellk, lane);
   lds_sync();
   const f32x4* wt = reinterpret_cast<const f32x4*>(tab) + h;        // (t, h) at wt[2 t]
@@ -1024,7 +1045,9 @@ __device__ __forceinline__ void scatter_grid_grad_uniform(float* __restrict__ gr
 #pragma unroll
   for (int t = 0; t < 32; ++t) {
     const int code = __builtin_amdgcn_readlane(codes, t);
-    const float vc = img[t * TPITCH + ch];
+    // point t = F(r, hh): r = (t & 3) + 4 (t >> 3), hh = (t >> 2) & 1
+    const float vc = TR ? (((t >> 2) & 1) ? vhi[(t & 3) + 4 * (t >> 3)] : vlo[(t & 3) + 4 * (t >> 3)])
+                        : img[t * TPITCH + ch];
     const f32x4 w = wt[2 * t];
     const i32x4 nr = rt[2 * t];
     if (code & 0x100) {  // wave-uniform: the walk steps to another cell
@@ -1349,6 +1372,13 @@ constexpr int kScratchFloats = 2 * TILE_FLOATS + 32 * 4 + 32 * 3 + 32 * 8 * 2 + 
 constexpr int kWavesBwd = 4;
 constexpr int kMaxSlabs = 4096;  // WG == 2 above this many tiles
 
+// lean mapping tile (saved masks, no weight or point gradients): dc transposed, walk without LDS image
+constexpr bool lean_tr(int WG, bool PG, bool SAVED) { return SAVED && WG == 0 && !PG; }
+// per-wave LDS floats of a backward kernel variant
+constexpr int bwd_scratch_floats(int WG, bool PG, bool SAVED) {
+  return WG ? kScratchFloats : lean_tr(WG, PG, SAVED) ? kWalkFloats : TILE_FLOATS + kWalkFloats;
+}
+
 template <int DEC, int WG, bool PG, bool FIRST, bool SAVED>
 __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, const Slab& A, const Scratch& S,
                                              int lane, double* __restrict__ gpts, int64_t gbase = 0) {
@@ -1393,20 +1423,23 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
   f32x16 dc;
   float gx[3] = {0.f, 0.f, 0.f};
   static_assert(!(SAVED && WG), "weight gradients from saved masks run as k_color_wgrad");
+  // the lean mapping chain forms dc transposed for the register-only scatter walk (lean_tr)
+  constexpr bool TR = lean_tr(WG, PG, SAVED);
+  float* const tab = TR ? S.sA : S.sA + TILE_FLOATS;  // the walk table (after the transpose image if any)
   if (SAVED) {  // masks from the forward: no recompute (the mask-only chain)
     uint32_t m[5];
     load_masks(a, DEC, tile, m, lane);
     // the walk table goes to LDS before the chain (its corner rows and weights need no registers
     // through it); the slot loads were issued before the masks, so this waits for nothing extra
-    if (WG == 0 && gr.grad) stage_walk_table(S.sA + TILE_FLOATS, scn, cr.cell, lane);
+    if (WG == 0 && gr.grad) stage_walk_table(tab, scn, cr.cell, lane);
     if (DEC == NSLAM_DEC_COARSE) {
-      noxyz_backward_saved(pk, m, g[3], lane, dc);
+      noxyz_backward_saved<TR>(pk, m, g[3], lane, dc);
     } else if (DEC == NSLAM_DEC_FINE) {
-      xyz_backward_saved<2, 1, 3, PG>(pk, m, q.x, g, lane, dc, gx);
+      xyz_backward_saved<2, 1, 3, PG, TR>(pk, m, q.x, g, lane, dc, gx);
     } else if (DEC == NSLAM_DEC_COLOR) {
-      xyz_backward_saved<1, 3, 0, PG>(pk, m, q.x, g, lane, dc, gx);
+      xyz_backward_saved<1, 3, 0, PG, TR>(pk, m, q.x, g, lane, dc, gx);
     } else {
-      xyz_backward_saved<1, 1, 3, PG>(pk, m, q.x, g, lane, dc, gx);
+      xyz_backward_saved<1, 1, 3, PG, TR>(pk, m, q.x, g, lane, dc, gx);
     }
   } else if (DEC == NSLAM_DEC_COARSE) {
     const f32x16 c = gather_tile(gr.data, cr, lane);
@@ -1430,7 +1463,7 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
     if (WG) {
       scatter_grid_grad_halves(gr.grad, gr.slot, cr, dc, q.valid, S, lane);
     } else {  // walk table: the lean kernels' slot after the transpose image
-      scatter_grid_grad_uniform<SAVED>(gr.grad, scn, cr.cell, dc, S.sA, S.sA + TILE_FLOATS, lane);
+      scatter_grid_grad_uniform<SAVED, TR>(gr.grad, scn, cr.cell, dc, S.sA, tab, lane);
     }
   }
   PHASE(DEC, 13);
@@ -1455,7 +1488,7 @@ __global__ __launch_bounds__(64 * kWavesBwd, (WG || PG || !SAVED) ? 2 : NSLAM_LE
   // per-wave scratch: the scatter needs sA + corner rows/weights; weight gradients add sX and
   // the per-point tables (sizing LDS per variant keeps the lean kernels at 5+ waves/SIMD)
   // (the lean kernels' scatter walk needs only the sA transpose image and its walk table)
-  constexpr int kScr = WG ? kScratchFloats : TILE_FLOATS + kWalkFloats;
+  constexpr int kScr = bwd_scratch_floats(WG, PG, SAVED);
   __shared__ __attribute__((aligned(16))) float lds[kWavesBwd * kScr];
   const int lane = threadIdx.x & 63, wave = wave_id();
   float* sc = lds + wave * kScr;
@@ -1524,7 +1557,7 @@ struct MultiDecArgs {
 #endif
 template <bool PG>
 __global__ __launch_bounds__(64 * kWavesBwd, PG ? NSLAM_MULTI_PG_LB : NSLAM_MULTI_LB) void k_dec_bwd_multi(QueryKArgs a, MultiDecArgs m) {
-  constexpr int kScr = TILE_FLOATS + kWalkFloats;
+  constexpr int kScr = bwd_scratch_floats(0, PG, true);
   __shared__ __attribute__((aligned(16))) float lds[kWavesBwd * kScr];
   const int lane = threadIdx.x & 63, wave = wave_id();
   Scratch S;
