@@ -269,6 +269,18 @@ def test_scene0000_bundle_adjustment_window5(monkeypatch):
     monkeypatch.setattr(mp, "keyframe_selection_overlap", lambda *a, **k: [0, 1, 2])
     fp = FixedPixels(seed=93)
     monkeypatch.setattr(P.common, "select_uv", fp)
+    # the cameras' gradients at the colour iteration, as each Adam sees them (product first, then the
+    # oracle replica below): the one Adam step they get is sign-like, so the pose deltas alone would
+    # not catch a wrong gradient scale
+    cam_grads = []
+
+    class CapturingAdam(torch.optim.Adam):
+        def step(self, *a, **k):
+            if len(self.param_groups) > 5 and self.param_groups[5]["lr"] > 0:
+                cam_grads.append([q.grad.detach().float().cpu().clone() for q in self.param_groups[5]["params"]])
+            return super().step(*a, **k)
+
+    monkeypatch.setattr(torch.optim, "Adam", CapturingAdam)
     kf = [{"gt_c2w": m, "idx": 10 * i, "depth": d, "color": c, "est_c2w": m.clone()}
           for i, (d, c, m) in enumerate(frames[:4])]
     cur_d, cur_c, cur_m = frames[4]
@@ -324,5 +336,11 @@ def test_scene0000_bundle_adjustment_window5(monkeypatch):
     assert torch.equal(kf[0]["est_c2w"], poses0[0])
     for k in go:
         report[k] = rel_l2(slam.shared_c[k].detach().cpu() - grids[k], go[k].detach() - grids[k])
+    assert len(cam_grads) == 2 and len(cam_grads[0]) == len(cam_grads[1]) == 4
+    for f, (gp, go_) in enumerate(zip(*cam_grads)):
+        assert float(go_.abs().max()) > 0
+        report[f"cam{f + 1}_grad"] = rel_l2(gp, go_)
     print(json.dumps(report, indent=1))
-    assert all(v < 5e-2 for v in report.values()), report
+    # measured on MI355X: poses <= 2.7e-5, grid deltas <= 7.8e-5, camera gradients <= 3.3e-6
+    assert all(v < 1e-4 for k, v in report.items() if k.endswith("_grad")), report
+    assert all(v < 1e-3 for v in report.values()), report

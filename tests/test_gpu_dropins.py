@@ -156,7 +156,8 @@ def test_mapper_optimize_map_schedule(tiny, monkeypatch):
     for k in grids:
         delta = slam.shared_c[k].detach().cpu() - sc.grids[k]
         rdelta = grids[k].detach() - sc.grids[k]
-        assert rel_l2(delta.numpy(), rdelta.numpy()) < 5e-2, k
+        # measured on MI355X: middle 1.7e-5, fine 3.9e-4, colour 5.1e-5
+        assert rel_l2(delta.numpy(), rdelta.numpy()) < 5e-3, k
 
 
 def _nudged(c2w, ang, t):
@@ -230,5 +231,5 @@ def test_mapper_bundle_adjustment(tiny, monkeypatch):
         d_got = got[:3].detach().cpu() - start[:3]
         d_ref = ref_pose - start[:3]
         assert float(d_ref.abs().max()) > 1e-5  # the colour-stage step moved the camera
-        assert rel_l2(d_got.numpy(), d_ref.numpy()) < 5e-2
+        assert rel_l2(d_got.numpy(), d_ref.numpy()) < 1e-3  # measured on MI355X: <= 8.2e-5
     assert torch.equal(kf[0]["est_c2w"], est[0])  # the oldest frame is not optimised

@@ -11,7 +11,7 @@
 Tolerances: forward quantities as tests/test_gpu_parity.py; multi-iteration loops (Adam
 normalises every gradient, so fp32-level differences in tiny gradient entries become lr-sized
 steps) as tests/test_gpu_dropins.py: losses rtol 2e-3 (mapper) / 2e-4 (tracker), parameter
-updates rel-L2 5e-2 / 1e-2.
+updates rel-L2 1e-3 (mapper, BA window: measured <= 8e-5 on MI355X) / 1e-2 (tracker).
 """
 import importlib
 import json
@@ -215,7 +215,8 @@ def test_mapper_loop_matches_reference(tiny, loop, monkeypatch):
         report[f"pose{k}"] = rel_l2(got - start, ref - start)
     report["cur"] = rel_l2(out.detach().cpu() - torch.from_numpy(cur), loop["map.cur_c2w_out"] - cur)
     print(json.dumps(report, indent=1))
-    assert all(v < 5e-2 for v in report.values()), report
+    # (measured on MI355X: grids <= 1.9e-5, colour decoder 5.8e-7, poses <= 4.5e-6)
+    assert all(v < 1e-3 for v in report.values()), report
 
 
 def test_frustum_mask_device_matches_reference(loop):
