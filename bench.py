@@ -928,11 +928,19 @@ def main():
             # blocks of GRAPH_BLOCK iterations per graph whatever --steps is (a replay starts only
             # after the previous one drained, ~20 us, paid once per block)
             graph, mode = capture_step_graphs(lambda: scene.step(sharded=sharded), sync=scene.flip_parity)
-            graph.run(graph.block)
-            torch.cuda.synchronize()
         except Exception as e:  # pragma: no cover - fall back to eager launches
             print(f"graph capture failed, eager mode: {e!r}", file=sys.stderr)
-            graph = None
+            graph, mode = None, "eager"
+        if world > 1:
+            # every rank replays graphs or every rank launches eagerly: a rank whose capture failed
+            # would otherwise issue fewer collectives than the others and the job would hang
+            ok = torch.tensor([0 if graph is None else 1], dtype=torch.int32, device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if int(ok.item()) == 0:
+                graph, mode = None, "eager"
+        if graph is not None:
+            graph.run(graph.block)
+            torch.cuda.synchronize()
     scene.kept.zero_()
     if world > 1:
         dist.barrier()
