@@ -44,7 +44,7 @@ extern "C" int nslam_query_fwd_ws(const nslam_query_cfg* cfg, const double* pts,
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   float* occ = reinterpret_cast<float*>(ws);
   // Colour stage: 3 parts (middle | fine | colour) while 3 waves per tile fit the chip's wave slots
-  // in one round (4 per SIMD at the forward's ~124 VGPRs; e.g. tracking, 300 tiles), else 2 parts
+  // in one round (3 per SIMD at the forward's 168 VGPRs; e.g. tracking, 300 tiles), else 2 parts
   // (middle then colour | fine: fewer, balanced waves — room0 mapping: 3000 instead of 4500 for
   // 4096 slots, 187 -> 198 M ray-samples/s).  NSLAM_FWD_PARTS=2|3 forces one (experiments).
   static const int forced_parts = [] {
@@ -56,7 +56,7 @@ extern "C" int nslam_query_fwd_ws(const nslam_query_cfg* cfg, const double* pts,
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
       cus = 256;
-    return (int64_t)cus * 4 * 4;
+    return (int64_t)cus * 4 * 3;
   }();
   const int64_t tiles = (n_pts + 31) / 32;
   const int color_parts = forced_parts == 2 || forced_parts == 3 ? forced_parts : (3 * tiles <= wave_slots ? 3 : 2);
