@@ -32,9 +32,14 @@ PREFETCH = True
 # iterations per captured hipGraph, whatever --steps is (a replay starts only after the previous one has
 # drained, ~20 us on MI355X: paid once per block), so runs of any length measure the same thing
 GRAPH_BLOCK = 10
-# gradient exchange of a ray-sharded run (N > 1): "sharded" (reduce-scatter, Adam on the rank's
-# shard, all-gather: distributed.ShardedAdamExchange) or "allreduce" (SparseGradExchange, replicated Adam)
-EXCHANGE = "sharded"
+# gradient exchange of a ray-sharded run (N > 1): "allreduce" (SparseGradExchange: one all-reduce of the
+# frustum rows + colour-decoder gradient after the backward, replicated Adam — one collective per
+# iteration, on one stream) or "sharded" (reduce-scatter, Adam on the rank's shard, all-gather per
+# backward branch: distributed.ShardedAdamExchange — four collectives on two communicators)
+EXCHANGE = "allreduce"
+# --force-exchange: a one-rank job issues the exchange's collectives anyway (RCCL identities), so the
+# N > 1 code path — collectives captured in the hipGraph — runs on a one-GPU box
+FORCE_EXCHANGE = False
 
 ROOM0 = {
     "bound": [[-2.9, 8.9], [-3.2, 5.5], [-3.5, 3.3]], "bound_divisible": 0.32,
@@ -319,10 +324,12 @@ class Room0Scene:
             # reduce-scatter, Adam on this rank's shard, all-gather, per backward branch
             # (distributed.ShardedAdamExchange); --exchange allreduce: one all-reduce, replicated Adam
             world = int(os.environ.get("WORLD_SIZE", "1"))
-            if world > 1 and EXCHANGE == "sharded":
-                self.exchange = P.distributed.ShardedAdamExchange(self.engine, self.opt)
+            if (world > 1 or FORCE_EXCHANGE) and EXCHANGE == "sharded":
+                self.exchange = P.distributed.ShardedAdamExchange(self.engine, self.opt,
+                                                                  force_collectives=FORCE_EXCHANGE)
             else:
-                self.exchange = P.distributed.SparseGradExchange(self.engine, self.rows)
+                self.exchange = P.distributed.SparseGradExchange(self.engine, self.rows,
+                                                                 force_collectives=FORCE_EXCHANGE)
         else:
             params = [{"params": list(self.nice.color_decoder.parameters()), "lr": cfg["lr"]["decoders"]},
                       {"params": [self.grids["grid_middle"]], "lr": cfg["lr"]["middle"]},
@@ -888,16 +895,20 @@ def main():
                     help="override mapping pixels per iteration (scaling studies; the metric uses room0's 1000)")
     ap.add_argument("--path", choices=("fused", "autograd"), default="fused",
                     help="fused engine (default) or the autograd drop-in path")
-    ap.add_argument("--exchange", choices=("sharded", "allreduce"), default="sharded",
-                    help="N>1 gradient exchange: sharded Adam (default) or all-reduce + replicated Adam")
+    ap.add_argument("--exchange", choices=("sharded", "allreduce"), default="allreduce",
+                    help="N>1 gradient exchange: all-reduce + replicated Adam (default) or sharded Adam")
+    ap.add_argument("--force-exchange", action="store_true",
+                    help="one rank: run the exchange's collectives anyway over a one-rank RCCL group "
+                         "(identities), captured in the hipGraph like an N>1 job's")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="draw + sample each iteration's rays inside it (no overlap with the previous backward)")
     ap.add_argument("--leg", choices=("frames", "stress", "stress_iter", "bulk", "frame_io", "apartment"), default=None,
                     help="run one auxiliary measurement and print its JSON (bench.py spawns these itself)")
     args = ap.parse_args()
-    global PREFETCH, EXCHANGE
+    global PREFETCH, EXCHANGE, FORCE_EXCHANGE
     PREFETCH = not args.no_prefetch
     EXCHANGE = args.exchange
+    FORCE_EXCHANGE = args.force_exchange
     if args.leg:
         return leg_main(args.leg)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -905,8 +916,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.backend == "gloo":  # rehearsal of the sharded path with several ranks on one GPU
         local = local % max(torch.cuda.device_count(), 1)
-    if world > 1:
+    if args.force_exchange and world != 1:
+        raise SystemExit("--force-exchange is the one-rank rehearsal of the exchange")
+    if world > 1 or args.force_exchange:
         torch.cuda.set_device(local)
+        if world == 1:  # not under torch.distributed.run: a one-rank rendezvous of our own
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -917,7 +935,7 @@ def main():
     if args.pixels:
         cfg["pixels"] = args.pixels
     scene = Room0Scene(dev, rank, cfg=cfg, path=args.path)
-    sharded = world > 1
+    sharded = world > 1 or args.force_exchange
     for _ in range(args.warmup):
         scene.step(sharded=sharded)
     torch.cuda.synchronize()
@@ -1002,6 +1020,12 @@ def main():
             keys, dn = scene.engine.grads_for("color", ("color",))
             out["exchange_bytes_per_step"] = scene.exchange.payload_bytes(keys, dn)
             out["exchange"] = EXCHANGE
+            out["exchange_backend"] = dist.get_backend() if dist.is_initialized() else None
+            out["exchange_forced_world1"] = bool(args.force_exchange)
+            # the collectives' own HIP-event spans (eager iterations, branches serialised), per iteration
+            coll = {k: v for k, v in timers.items() if k.startswith("collective.")}
+            out["collective_ms_per_step"] = {k: round(v["total_ms"] / max(5, args.steps // 4), 4)
+                                             for k, v in coll.items()}
             out["dense_grad_bytes_per_step"] = sum(v.numel() for v in scene.grids.values()) * 4
         # the auxiliary measurements run as child processes: a failure there (one run on a fresh
         # box ended in a host heap abort inside a later leg) cannot take the headline line with it
@@ -1020,7 +1044,7 @@ def main():
             out["reference_gpu_path"] = ref
             out["vs_reference_gpu_path"] = out["value"] / ref["value"]
         print(json.dumps(out))
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -233,6 +233,7 @@ __device__ __forceinline__ void produce_chain(const QueryKArgs& a, int64_t t, fl
 #pragma unroll
     for (int r = 0; r < 16; ++r) dh[r] += w[r] * gv[j];
   }
+  if (a.c.g_h4 && idx < a.n) add_gh4(dh, a.c.g_h4 + idx * 32, lane);  // ABI v17: d/dh4 of a direct caller
   tstore(dimg(buf, 4), dh, lane);
   constexpr int kNext[3] = {3, 2, 1};  // the chain's next GEMMs: L3's h2 block, L2, L1 (transposed)
 #pragma unroll
@@ -416,6 +417,7 @@ __global__ __launch_bounds__(64 * kCwWaves, NSLAM_CW_LB) void k_color_wgrad(CwAr
   const int64_t ntiles = (a.n + 31) / 32;
   const int64_t t0 = chunk * w.chunk_tiles;
   const int64_t t1 = t0 + w.chunk_tiles < ntiles ? t0 + w.chunk_tiles : ntiles;
+  TL(2, 0, chunk);
   const nslam_dec_grad& dg = a.c.dgrad[NSLAM_DEC_COLOR];
   const float* pk = a.c.packed[NSLAM_DEC_COLOR];
   const XyzPack L{1};
@@ -529,6 +531,7 @@ __global__ __launch_bounds__(64 * kCwWaves, NSLAM_CW_LB) void k_color_wgrad(CwAr
       if (j0 < 4) as_global_w(sl)[dg.bo + j0] = j0 < 3 ? bo : 0.f;
     }
   }
+  TL(2, 1, 0);
 }
 
 int launch_color_wgrad(const QueryKArgs& a, float* ws, hipStream_t s) {

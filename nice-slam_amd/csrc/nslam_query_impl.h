@@ -212,9 +212,28 @@ __device__ unsigned long long g_phase[5 * kPhaseWaves * 16];  // one-TU phases b
     if ((threadIdx.x & 63) == 0 && w_ < kPhaseWaves)                                                      \
       g_phase[((size_t)(dec) * kPhaseWaves + w_) * 16 + (k)] = __builtin_amdgcn_s_memtime();              \
   } while (0)
+// Timeline (same build): per wave of kernel slot k (0 forward, 1 mask-only backward, 2 k_color_wgrad)
+// {start, end} of s_memrealtime (100 MHz, one clock for all XCDs), HW_ID | XCC_ID << 32, tile
+__device__ unsigned long long g_tl[3 * kPhaseWaves * 4];
+__device__ __forceinline__ void tl_mark(int slot, int end, long long tile) {
+  const int64_t w_ = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if ((threadIdx.x & 63) != 0 || w_ >= kPhaseWaves) return;
+  unsigned long long* o = g_tl + ((size_t)slot * kPhaseWaves + w_) * 4;
+  o[end] = __builtin_amdgcn_s_memrealtime();
+  if (!end) {
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+    const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
+    o[2] = (unsigned long long)hw | ((unsigned long long)(xcc & 15) << 32);
+    o[3] = (unsigned long long)tile;
+  }
+}
+#define TL(slot, end, tile) tl_mark(slot, end, tile)
 #else
 #define PHASE(dec, k) \
   do {                \
+  } while (0)
+#define TL(slot, end, tile) \
+  do {                      \
   } while (0)
 #endif
 
@@ -479,6 +498,19 @@ __device__ __forceinline__ float out_row(const float* __restrict__ Wo, const flo
   return (s + xor32(s)) + bo[j];
 }
 
+// dh += the caller's cotangent of h4 (ABI v17 nslam_query_cfg.g_h4; row = this lane's point, [32] floats,
+// NULL: none): feature F(r, h) of register r = 4i + j is float 8i + 4h + j of the row
+__device__ __forceinline__ void add_gh4(f32x16& dh, const float* __restrict__ row, int lane) {
+  if (!row) return;
+  const gptr_t<f32x4> p = as_global(reinterpret_cast<const f32x4*>(row + 4 * (lane >> 5)));
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x4 v = p[2 * i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dh[4 * i + j] += v[j];
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // MLP with Fourier embedding: backward (forward recomputed first).
 //   gall[GOFS + j], j < NOUT : cotangents of the decoder outputs (per point, both halves)
@@ -502,7 +534,8 @@ __device__ __forceinline__ void fc_bwd(const float* __restrict__ pk, const XyzPa
 template <int NC, int NOUT, int GOFS, int WG, bool EMBG>
 __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const f32x16 (&cin)[NC],
                                              const float x[3], const float (&gall)[4], const nslam_dec_grad& dg,
-                                             const Slab& A, const Scratch& S, int lane, f32x16& dc, float gx[3]) {
+                                             const Slab& A, const Scratch& S, int lane, f32x16& dc, float gx[3],
+                                             const float* gh4 = nullptr) {
   const XyzPack L{NC};
   [[maybe_unused]] constexpr int DEC_ = NOUT == 3 ? 3 : (NC == 2 ? 2 : 1);
   const int h = lane >> 5;
@@ -519,6 +552,7 @@ __device__ __forceinline__ void xyz_backward(const float* __restrict__ pk, const
 #pragma unroll
     for (int r = 0; r < 16; ++r) dh[r] += w[r] * gall[GOFS + j];
   }
+  add_gh4(dh, gh4, lane);
   if (WG) {
     tstore(S.sX, h4, lane);
     lds_sync();
@@ -793,7 +827,7 @@ __device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, con
 template <int NC, int NOUT, int GOFS, bool EMBG, bool TR = false>
 __device__ __forceinline__ void xyz_backward_saved(const float* __restrict__ pk, const uint32_t m[5],
                                                    const float x[3], const float (&gall)[4], int lane, f32x16& dc,
-                                                   float gx[3]) {
+                                                   float gx[3], const float* gh4 = nullptr) {
   static_assert(!(TR && EMBG), "d/dpts needs dc in the C layout");
   const XyzPack L{NC};
   const int h = lane >> 5;
@@ -804,6 +838,7 @@ __device__ __forceinline__ void xyz_backward_saved(const float* __restrict__ pk,
 #pragma unroll
     for (int r = 0; r < 16; ++r) dh[r] += w[r] * gall[GOFS + j];
   }
+  add_gh4(dh, gh4, lane);
   dc = zero16();
   gemm_acc_tr<TR>(dc, pk + L.FCT(4) * NSLAM_FRAG, dh, lane);
   f32x16 da = apply_mask(dh, m[4]);
@@ -1315,6 +1350,7 @@ template <int STAGE, int NPARTS, bool TAPE>
 __global__ __launch_bounds__(256, NSLAM_FWD_LB) void k_query_fwd_parts(QueryKArgs a, float* __restrict__ occ_mid) {
   const int part = (int)(blockIdx.x % NPARTS);
   const int lane = threadIdx.x & 63;
+  TL(0, 0, part);
   // The part's decoder vector sections (biases, output rows, Fourier B: ~3 KiB each) are read by
   // every layer of every wave: an LDS copy per workgroup turns ~90 global loads per wave into
   // ds_reads.  Part 0 of the 2-part colour forward evaluates middle then colour: two copies.
@@ -1352,6 +1388,7 @@ __global__ __launch_bounds__(256, NSLAM_FWD_LB) void k_query_fwd_parts(QueryKArg
     fwd_part_color<TAPE>(a, q, tile, idx, lane, vsec[0]);
   }
   PHASE(0, 9);
+  TL(0, 1, 0);
 }
 
 static __global__ __launch_bounds__(256) void k_occ_combine(float* __restrict__ raw, const float* __restrict__ occ_mid,
@@ -1411,6 +1448,8 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
   const nslam_grid& gr = a.c.grid[DEC];
   const nslam_dec_grad& dg = a.c.dgrad[DEC];
   const float* pk = a.c.packed[DEC];
+  // the colour decoder's h4 cotangent of a direct MLP(color=True) caller (ABI v17), none for tail lanes
+  const float* gh4 = (DEC == NSLAM_DEC_COLOR && a.c.g_h4 && q.valid) ? a.c.g_h4 + idx * 32 : nullptr;
   // The weight fragments are loop-invariant across the tile loop; hoisting their ~100 loads out of
   // the loop would pin hundreds of registers.  Launder the base pointer per tile so they stay put.
   asm volatile("" : "+s"(pk));
@@ -1437,7 +1476,7 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
     } else if (DEC == NSLAM_DEC_FINE) {
       xyz_backward_saved<2, 1, 3, PG, TR>(pk, m, q.x, g, lane, dc, gx);
     } else if (DEC == NSLAM_DEC_COLOR) {
-      xyz_backward_saved<1, 3, 0, PG, TR>(pk, m, q.x, g, lane, dc, gx);
+      xyz_backward_saved<1, 3, 0, PG, TR>(pk, m, q.x, g, lane, dc, gx, gh4);
     } else {
       xyz_backward_saved<1, 1, 3, PG, TR>(pk, m, q.x, g, lane, dc, gx);
     }
@@ -1454,7 +1493,7 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
     const f32x16 c[1] = {gather_tile(gr.data, cr, lane)};
     PHASE(DEC, 3);
     if (DEC == NSLAM_DEC_COLOR)  // the colour decoder's 4th output is overwritten by the combiner
-      xyz_backward<1, 3, 0, WG, PG || WG>(pk, c, q.x, g, dg, A, S, lane, dc, gx);
+      xyz_backward<1, 3, 0, WG, PG || WG>(pk, c, q.x, g, dg, A, S, lane, dc, gx, gh4);
     else
       xyz_backward<1, 1, 3, WG, PG || WG>(pk, c, q.x, g, dg, A, S, lane, dc, gx);
   }
@@ -1571,6 +1610,7 @@ __global__ __launch_bounds__(64 * kWavesBwd, PG ? NSLAM_MULTI_PG_LB : NSLAM_MULT
   const int64_t w = (int64_t)(blockIdx.x / (unsigned)m.ndec) * kWavesBwd + wave;
   const int64_t ntiles = (a.n + 31) / 32;
   if (w >= ntiles) return;
+  TL(1, 0, part);
   const Slab A = make_slab(nullptr, 0);
   switch (dec) {
     case NSLAM_DEC_COARSE: dec_bwd_tile<NSLAM_DEC_COARSE, 0, PG, true, true>(a, w, A, S, lane, gp); break;
@@ -1578,6 +1618,7 @@ __global__ __launch_bounds__(64 * kWavesBwd, PG ? NSLAM_MULTI_PG_LB : NSLAM_MULT
     case NSLAM_DEC_FINE: dec_bwd_tile<NSLAM_DEC_FINE, 0, PG, true, true>(a, w, A, S, lane, gp); break;
     default: dec_bwd_tile<NSLAM_DEC_COLOR, 0, PG, true, true>(a, w, A, S, lane, gp); break;
   }
+  TL(1, 1, 0);
 }
 
 // base[j] += sum_b slab[b][j].  A workgroup owns 64 parameters; lane (r, c) of a wave reads the

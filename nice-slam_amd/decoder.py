@@ -92,11 +92,10 @@ class MLP(nn.Module):
         """decoder.py:177-203 for this decoder alone (NICE.forward evaluates a whole stage in one
         fused launch instead): occupancy [P] (middle, fine) or [P, 4] (colour).
 
-        Limitation (colour decoder): the gradient of the 4th output column (which NICE.forward
-        overwrites with the occupancy, decoder.py:341, so no NICE-SLAM loss reaches it) flows to
-        output_linear's row 3 but not into the hidden layers, grid or points: a loss that depends
-        on it with a nonzero gradient raises NotImplementedError in the backward
-        (tests/test_gpu_decoders.py)."""
+        Colour decoder: all four output columns are differentiable, as in the reference module —
+        the 4th (which NICE.forward overwrites with the occupancy, decoder.py:341) reaches
+        output_linear's row 3 through torch and the hidden layers, grid and points through the
+        kernels' h4 cotangent (ABI v17 nslam_query_cfg.g_h4; tests/test_gpu_decoders.py)."""
         return ops.query_decoder(self, p, c_grid)
 
 

@@ -13,6 +13,15 @@ import torch
 import torch.distributed as dist
 
 
+def _collectives(group, force: bool) -> bool:
+    """Whether an exchange issues its collectives: world > 1, or `force` with an initialised process
+    group of any size (world 1 over RCCL: the collectives run as they would in a job, an identity
+    on the data — the path the single-GPU box can exercise, bit-identical to no exchange)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return force or dist.get_world_size(group) > 1
+
+
 def shard_range(n: int, rank: int, world: int):
     """Contiguous split of n rays over `world` ranks (first n % world ranks get one more)."""
     base, rem = divmod(n, world)
@@ -78,11 +87,13 @@ class SparseGradExchange:
 
     rows: {grid key: int32 row indices} (the FusedAdam group "rows"); pack/unpack default to the
     HIP entry points (ops.rows_pack / ops.rows_unpack) and are injectable for CPU tests.
+    force_collectives: issue the all-reduce at world size 1 too (RCCL on one GPU).
     """
 
-    def __init__(self, engine, rows, group=None, pack=None, unpack=None):
+    def __init__(self, engine, rows, group=None, pack=None, unpack=None, force_collectives=False):
         from . import ops
         self.engine, self.group = engine, group
+        self.force = force_collectives
         self.pack = pack or ops.rows_pack
         self.unpack = unpack or ops.rows_unpack
         offs, off = {}, 0
@@ -91,6 +102,17 @@ class SparseGradExchange:
             off += v.numel() // 32
         self.rows = {k: (r.to(torch.int64) + offs[k]).to(torch.int32) for k, r in rows.items()}
         self._plan = {}
+        self._gen = getattr(engine, "layout_gen", 0)
+
+    def validate(self, engine, keys, dnames):
+        """engine.MappingEngine.iteration calls this before it enqueues anything: the cached plans hold
+        views of the engine's gradient buffers, which set_rows reallocates."""
+        if engine is not self.engine:
+            raise ValueError("SparseGradExchange: built for another engine")
+        gen = getattr(engine, "layout_gen", 0)
+        if gen != self._gen:
+            self._plan.clear()  # (views of the old buffers)
+            self._gen = gen
 
     def plan(self, keys, dnames):
         """(flat row list, [(decoder grad, offset)], payload buffer) for the grids in `keys` and
@@ -132,8 +154,10 @@ class SparseGradExchange:
             self.pack(gbuf, rows, None, buf)
         for g, off in tails:
             self.pack(None, None, g.reshape(-1), buf[off:off + g.numel()])
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1:
-            dist.all_reduce(buf, group=self.group)
+        if _collectives(self.group, self.force):
+            from .ops import _span
+            with _span("collective.all_reduce"):
+                dist.all_reduce(buf, group=self.group)
         if rows.numel():
             self.unpack(buf, rows, gbuf, None)
         for g, off in tails:
@@ -167,18 +191,28 @@ class ShardedAdamExchange:
     second process group (two communicators: collectives from two streams never share one).
 
     The engine's compact gradients are padded to whole shards (engine.set_rows(pad_rows=world)); the
-    exchange zeroes every gradient entry it consumed, so the next iteration needs no memset.
+    exchange zeroes every gradient entry it consumed, so the next iteration needs no memset.  The two
+    branches' collectives run on two communicators from two streams, so the engine orders them
+    (query_bwd(ordered_branches=True): the weight-gradient branch's exchange starts after the lean
+    branch's) and every rank issues them in the same order.  Supported: the colour decoder as the only
+    trainable decoder, with the engine's merged mask-only launch (its parameters then come from the
+    weight-gradient branch); validate() raises before an iteration enqueues anything otherwise.
+    force_collectives: issue the collectives at world size 1 too (RCCL on one GPU: identities).
     pack / unpack / adam_slices default to the HIP entry points and are injectable for CPU tests."""
 
     leaves_clean = True
 
-    def __init__(self, engine, optimizer, group=None, group_dec=None, pack=None, unpack=None, adam_slices=None):
+    def __init__(self, engine, optimizer, group=None, group_dec=None, pack=None, unpack=None, adam_slices=None,
+                 force_collectives=False):
         from . import ops
         self.engine, self.opt, self.group = engine, optimizer, group
         init = dist.is_available() and dist.is_initialized()
         self.world = dist.get_world_size(group) if init else 1
         self.rank = dist.get_rank(group) if init else 0
-        if group_dec is None and self.world > 1:
+        self.coll = _collectives(group, force_collectives)
+        if not engine.merge:
+            raise ValueError("ShardedAdamExchange needs the engine's merged mask-only backward (engine.merge)")
+        if group_dec is None and self.coll:
             group_dec = dist.new_group(dist.get_process_group_ranks(group) if group is not None else None)
         self.group_dec = group_dec
         self.pack = pack or ops.rows_pack
@@ -187,6 +221,21 @@ class ShardedAdamExchange:
         if engine.pad_rows != self.world:
             engine.set_rows(engine.rows, pad_rows=self.world)
         self._plans = {}
+        self._gen = engine.layout_gen
+
+    def validate(self, engine, keys, dnames):
+        """Raise, before an iteration enqueues any kernel or collective, on what branch() cannot run."""
+        if engine is not self.engine:
+            raise ValueError("ShardedAdamExchange: built for another engine")
+        if engine.layout_gen != self._gen or engine.pad_rows != self.world:
+            raise RuntimeError("ShardedAdamExchange: the engine's gradient rows changed (MappingEngine.set_rows) "
+                               "after the exchange was built; its shards and the optimiser's Adam state belong "
+                               "to the old rows — build a new optimiser and exchange")
+        if not engine.merge:
+            raise ValueError("ShardedAdamExchange needs the engine's merged mask-only backward (engine.merge)")
+        if any(n != "color" for n in dnames):
+            raise ValueError(f"ShardedAdamExchange: trainable decoders {list(dnames)}: only the colour decoder "
+                             "(its weight gradients in nslam_color_wgrad) is supported; use SparseGradExchange")
 
     # -- layout ---------------------------------------------------------------------------------
     def _span(self, pieces):
@@ -220,32 +269,35 @@ class ShardedAdamExchange:
     # -- collectives (gloo has no in-place reduce-scatter of device tensors: all-reduce, same shard) --
     def _reduce_scatter(self, span, chunk, group):
         own = span[self.rank * chunk:(self.rank + 1) * chunk]
-        if self.world == 1:
+        if not self.coll:
             return own
-        if dist.get_backend(group) == "gloo":
-            dist.all_reduce(span, group=group)
-        else:
-            dist.reduce_scatter_tensor(own, span, group=group)
+        from .ops import _span
+        with _span("collective.reduce_scatter"):
+            if dist.get_backend(group) == "gloo":
+                dist.all_reduce(span, group=group)
+            else:
+                dist.reduce_scatter_tensor(own, span, group=group)
         return own
 
     def _all_gather(self, vals, chunk, group):
-        if self.world == 1:
+        if not self.coll:
             return
         own = vals[self.rank * chunk:(self.rank + 1) * chunk]
-        if dist.get_backend(group) == "gloo":
-            parts = list(vals.split(chunk))
-            dist.all_gather(parts, own.clone(), group=group)
-        else:
-            dist.all_gather_into_tensor(vals, own, group=group)
+        from .ops import _span
+        with _span("collective.all_gather"):
+            if dist.get_backend(group) == "gloo":
+                parts = list(vals.split(chunk))
+                dist.all_gather(parts, own.clone(), group=group)
+            else:
+                dist.all_gather_into_tensor(vals, own, group=group)
 
     # -- one branch -----------------------------------------------------------------------------
     def branch(self, names, part, keys, dnames):
         """One backward branch's exchange + sharded Adam (engine.MappingEngine.query_bwd's on_branch):
         part "grids" (the lean launch: its grids, over `group`) or "all" (the weight-gradient branch:
         the colour grid and decoder, one span, over `group_dec`)."""
-        if part not in ("grids", "all"):
-            raise ValueError("ShardedAdamExchange: every weight-gradient decoder must have the tape path "
-                             "(its grids in the lean launch, its parameters in nslam_color_wgrad)")
+        if part not in ("grids", "all"):  # (validate() rules this out before the iteration starts)
+            raise ValueError(f"ShardedAdamExchange: unsupported backward branch {part!r}")
         gk = tuple(k for k in ("grid_" + n for n in names) if k in keys)
         dk = tuple(n for n in names if n in dnames) if part == "all" else ()
         if not gk and not dk:

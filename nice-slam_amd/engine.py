@@ -111,9 +111,11 @@ class MappingEngine:
             if not v.is_contiguous(memory_format=torch.channels_last_3d):
                 raise ValueError(f"{k} must be channels-last (ops.channels_last)")
         self.grid_grads = grid_grads
+        self.layout_gen = 0  # bumped by set_rows: consumers holding views of the buffers re-check it
+        self.pad_rows = 1
         self.set_rows(rows)
 
-    def set_rows(self, rows, pad_rows=1):
+    def set_rows(self, rows, pad_rows=None):
         """Grid-gradient layout.  rows=None: dense gradients (one flat buffer for every grid, so
         zeroing is a single memset).  rows={grid key: int32 voxel rows} (the frustum selection of
         Mapper.py:314-333, the FusedAdam group "rows"): those grids accumulate a COMPACT gradient
@@ -123,9 +125,13 @@ class MappingEngine:
         ray-sharded exchange sums them as they are.
         pad_rows: every compact grid's rows and every decoder's gradient are padded (with entries
         nothing writes) to a multiple of pad_rows rows / elements, so a stage's gradient span splits
-        into equal whole-row shards (distributed.ShardedAdamExchange: pad_rows = world size)."""
+        into equal whole-row shards (distributed.ShardedAdamExchange: pad_rows = world size); None keeps
+        the current padding.  Every call reallocates the gradient buffers and bumps self.layout_gen: an
+        optimiser's compact Adam state and an exchange built for the old rows are invalid afterwards
+        (the exchanges raise; rebuild both for the new rows)."""
         c = self.c
-        pad = max(1, int(pad_rows))
+        pad = max(1, int(self.pad_rows if pad_rows is None else pad_rows))
+        self.layout_gen += 1
         rup = lambda n: -(-n // pad) * pad  # noqa: E731
         drup = lambda n: -(-n // (32 * pad)) * 32 * pad  # noqa: E731  (decoders: whole rows per shard too)
         self.rows = dict(rows) if rows else {}
@@ -201,7 +207,7 @@ class MappingEngine:
         return raw
 
     def query_bwd(self, stage, ro, rd, z, g_raw, grid_grads, dec_grads, concurrent=None, pts_grad=False,
-                  on_branch=None, pts_parts=False):
+                  on_branch=None, pts_parts=False, ordered_branches=False):
         """Backward into the engine's gradient buffers, as independent launches ("branches") that write
         disjoint buffers:
           lean     every decoder's grid gradient (and d/dpts) from the forward's ReLU masks, ONE launch
@@ -218,7 +224,10 @@ class MappingEngine:
         the grids of the lean launch's decoders but the colour one; "all": the colour grid and the
         colour decoder, on the weight-gradient branch after it AND the lean launch (k_color_wgrad reads
         the colour grid: it is not rewritten before that kernel is done); "unit": a per-decoder launch's
-        grid and parameters — the per-branch Adam of the mapping iteration."""
+        grid and parameters — the per-branch Adam of the mapping iteration.
+        ordered_branches: the weight-gradient branch's on_branch starts only after the lean branch's
+        on_branch work (not just the lean launch) — for collectives issued there on two communicators,
+        which every rank must then run in the same order (distributed.ShardedAdamExchange)."""
         n = z.numel()
         self._clean = False
         concurrent = self.concurrent if concurrent is None else concurrent
@@ -281,16 +290,21 @@ class MappingEngine:
                             rc = lib().nslam_query_bwd_decoders(ctypes.byref(lc), mask, None, n, ptr(g_raw), gps,
                                                                 st.cuda_stream)
                         check(rc, "nslam_query_bwd_decoders")
-                        if has_wgrad:
-                            if self._lean_ev is None:  # one persistent event (never destroyed mid-capture)
-                                self._lean_ev = torch.cuda.Event()
+                        if has_wgrad and self._lean_ev is None:  # one persistent event (never destroyed mid-capture)
+                            self._lean_ev = torch.cuda.Event()
+                        if has_wgrad and not ordered_branches:
                             self._lean_ev.record(st)
                         if on_branch is not None:
                             # the grids of this launch — but the colour grid, which k_color_wgrad reads (its
-                            # colour feature) and which is updated on that branch once both are done
+                            # colour feature) and which is updated on that branch once both are done.  A
+                            # trainable decoder here without a weight-gradient branch (no points) still
+                            # takes its Adam step (torch's Adam steps a parameter whose gradient is zero)
                             own = [d for d in names if not (d == "color" and has_wgrad)]
+                            dec_here = not has_wgrad and any(d in wgt for d in own)
                             if own:
-                                on_branch(own, part="grids")
+                                on_branch(own, part="all" if dec_here else "grids")
+                        if has_wgrad and ordered_branches:
+                            self._lean_ev.record(st)
                     else:
                         name = names[0]
                         d = ops._DEC_ID[name]
@@ -368,6 +382,9 @@ class MappingEngine:
         """
         H, W = hw
         fx, fy, cx, cy = intrinsics
+        keys, dnames = self.grads_for(stage, trainable_decoders)
+        if exchange is not None and hasattr(exchange, "validate"):
+            exchange.validate(self, keys, dnames)  # raises before anything of the iteration is enqueued
         draw = None
         if pix is None:
             key = (seed, world, rank)
@@ -417,7 +434,6 @@ class MappingEngine:
             ro, rd, gd, gc, keep, z = cur
         else:
             ro, rd, gd, gc, keep, z = rays()
-        keys, dnames = self.grads_for(stage, trainable_decoders)
         mirror = hasattr(optimizer, "set_mirror")
         raw = self.query_fwd(stage, ro, rd, z, defer_occ=True, tape="color" in dnames)
         _, _, _, ray_loss, g_raw = ops.render_loss(raw, z, gd, gc, keep, mode="mapper", use_color=stage == "color",
@@ -455,7 +471,7 @@ class MappingEngine:
                 if sub:
                     optimizer.step(grads=sub, zero_grad=clean)
 
-        self.query_bwd(stage, ro, rd, z, g_raw, keys, dnames, on_branch=on_branch)
+        self.query_bwd(stage, ro, rd, z, g_raw, keys, dnames, on_branch=on_branch, ordered_branches=sharded)
         if sharded:
             pass
         elif exchange is not None:  # frustum-compacted all-reduce (distributed.SparseGradExchange)

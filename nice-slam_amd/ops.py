@@ -316,7 +316,9 @@ class _OneDecoder(torch.autograd.Function):
     occupancy comes from the forward's deferred-combine mode (raw[...,3] = fine only), the colour
     decoder's rgb from raw[..., :3], and its 4th output row (which NICE.forward overwrites,
     decoder.py:341) from the forward's activation tape h4 (returned as a second output so torch
-    forms h4 @ Wo[3] + bo[3]).  Backward: that decoder's share only (nslam_query_bwd_decoder)."""
+    forms h4 @ Wo[3] + bo[3]).  Backward: that decoder's share only (nslam_query_bwd_decoder); the
+    cotangent torch forms for h4 (the 4th row's Wo[3] g) enters the kernels' Woᵀg as
+    nslam_query_cfg.g_h4 (ABI v17), so it reaches the hidden layers, the grid and the points."""
 
     @staticmethod
     def forward(ctx, meta, name, pts, g_own, g_middle, *params):
@@ -355,9 +357,6 @@ class _OneDecoder(torch.autograd.Function):
         meta, name = ctx.meta, ctx.name
         (pts,) = ctx.saved_tensors
         need = ctx.needs_input_grad
-        if g_h4 is not None and need[2:].count(True) and bool(g_h4.ne(0).any()):
-            raise NotImplementedError("gradient of the colour decoder's 4th output through its hidden layers "
-                                      "(NICE.forward overwrites that row, decoder.py:341)")
         n = pts.shape[0]
         d = _DEC_ID[name]
         g_raw = torch.zeros(n, 4, dtype=torch.float32, device=pts.device)
@@ -377,6 +376,9 @@ class _OneDecoder(torch.autograd.Function):
         cfg.saved_masks = ctx.saved_masks.data_ptr()
         if ctx.tape is not None:
             cfg.act_tape = ctx.tape.data_ptr()
+        if g_h4 is not None:  # d/dh4 of the 4th output row (decoder.py:198-203), [n, 32] float32
+            g_h4 = g_h4.detach().to(torch.float32).contiguous()
+            cfg.g_h4 = g_h4.data_ptr()
         if n and (g_grid is not None or dgrad is not None or g_pts is not None):
             wsb = lib().nslam_query_bwd_decoder_workspace_size(ctypes.byref(cfg), d, n)
             ws = torch.empty(wsb, dtype=torch.uint8, device=pts.device) if wsb else None

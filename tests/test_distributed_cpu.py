@@ -193,7 +193,7 @@ def _compact_exchange_worker(rank, world, port, out_path, inplace=False):
                           decs={"color": SimpleNamespace(grad=dgrad)})
     before_g, before_d = gbuf.clone(), eng.decs["color"].grad.clone()
     ex = D.SparseGradExchange.__new__(D.SparseGradExchange)
-    ex.engine, ex.group, ex.rows, ex._plan = eng, None, {}, {}
+    ex.engine, ex.group, ex.rows, ex._plan, ex.force = eng, None, {}, {}, False
     ex.pack, ex.unpack = _torch_rows_pack, _torch_rows_unpack
     if inplace:  # one contiguous span: all-reduced where it lies, no pack/unpack copies
         def _no_copy(*a):
@@ -335,3 +335,34 @@ def test_sharded_adam_exchange_equals_replicated_step(tmp_path):
         assert torch.allclose(r[0][k], c[k], rtol=0, atol=1e-7), k
     assert torch.allclose(r[0]["dec"], eng.decs["color"].param, rtol=0, atol=1e-7)
     assert torch.allclose(r[0]["packed"], eng.decs["color"].packed, rtol=0, atol=1e-7)
+
+
+def test_sharded_exchange_validates_before_enqueue(pkg):
+    """ShardedAdamExchange.validate (engine.MappingEngine.iteration calls it before it enqueues
+    anything) rejects what branch() cannot run: gradient rows changed after the exchange was built
+    (its cached spans and the optimiser's shard state belong to the old buffers), the per-decoder
+    backward (engine.merge False) and a trainable decoder other than the colour one."""
+    from types import SimpleNamespace
+    D = pkg.distributed
+
+    class Eng(SimpleNamespace):
+        def set_rows(self, rows, pad_rows=None):
+            self.rows = rows
+            self.pad_rows = self.pad_rows if pad_rows is None else pad_rows
+            self.layout_gen += 1
+
+    eng = Eng(merge=True, pad_rows=1, layout_gen=1, rows={})
+    ex = D.ShardedAdamExchange(eng, optimizer=None, pack=lambda *a: None, unpack=lambda *a: None,
+                               adam_slices=lambda *a: None)
+    ex.validate(eng, ("grid_color",), ("color",))
+    with pytest.raises(ValueError, match="only the colour decoder"):
+        ex.validate(eng, ("grid_fine",), ("fine",))
+    eng.merge = False
+    with pytest.raises(ValueError, match="merged"):
+        ex.validate(eng, ("grid_color",), ("color",))
+    eng.merge = True
+    eng.set_rows({})  # a new frustum selection: new buffers
+    with pytest.raises(RuntimeError, match="rows changed"):
+        ex.validate(eng, ("grid_color",), ("color",))
+    with pytest.raises(ValueError, match="merged"):
+        D.ShardedAdamExchange(Eng(merge=False, pad_rows=1, layout_gen=1, rows={}), optimizer=None)

@@ -67,16 +67,39 @@ def test_sub_decoder_direct_call(pkg, tiny, name):
 
 
 def test_color_decoder_fourth_output(pkg, tiny):
-    """The colour decoder's 4th output row (h4 @ Wo[3] + bo[3]) matches the module; a cotangent on
-    it that would reach the hidden layers fails loudly instead of being dropped."""
+    """The colour decoder's 4th output row (h4 @ Wo[3] + bo[3], decoder.py:198-203; NICE.forward
+    overwrites it, decoder.py:341, but a direct MLP(color=True) caller may differentiate it): its
+    value, and a cotangent on all four rows reaching the colour grid, every decoder parameter and the
+    points (ABI v17 nslam_query_cfg.g_h4), vs the oracle's module on the device."""
     bound = torch.from_numpy(tiny["bound"])
+    sd = sd_from(tiny)
     nice = pkg.NICE(c_dim=32, coarse_grid_len=2.0, middle_grid_len=0.64, fine_grid_len=0.32, color_grid_len=0.32,
                     hidden_size=32, coarse=True)
-    nice.load_state_dict(sd_from(tiny))
+    nice.load_state_dict(sd)
     nice.set_bound(bound)
     nice = nice.to(DEV)
-    grids = {k: v.to(DEV).contiguous(memory_format=torch.channels_last_3d) for k, v in grids_from(tiny).items()}
-    p = (bound[:, 0] + torch.rand(100, 3, dtype=torch.float64) * (bound[:, 1] - bound[:, 0])).to(DEV)
-    out = nice.color_decoder(p, grids)
-    with pytest.raises(NotImplementedError):
-        out[:, 3].sum().backward()
+    g = torch.Generator().manual_seed(11)
+    n = 1000
+    p = (bound[:, 0] + torch.rand(n, 3, generator=g, dtype=torch.float64) * (bound[:, 1] - bound[:, 0])).to(DEV)
+    grids = {k: v.to(DEV).contiguous(memory_format=torch.channels_last_3d).requires_grad_(True)
+             for k, v in grids_from(tiny).items()}
+    sdo = {k: v.to(DEV).clone().requires_grad_(k.startswith("color_decoder.")) for k, v in sd.items()}
+    go = {k: v.detach().clone().requires_grad_(True) for k, v in grids.items()}
+    for rows in ((3,), (0, 1, 2, 3)):  # the 4th row alone, then all four
+        for t in list(grids.values()) + list(go.values()) + list(nice.color_decoder.parameters()) + list(sdo.values()):
+            t.grad = None
+        pp = p.clone().requires_grad_(True)
+        po = p.clone().requires_grad_(True)
+        out = nice.color_decoder(pp, grids)
+        ref = oracle_decoder(sdo, "color", po, go, bound.to(DEV))
+        assert float((out.detach() - ref.detach()).abs().max()) < 2e-4
+        w = torch.zeros(ref.shape)
+        w[:, list(rows)] = torch.randn(n, len(rows), generator=g)
+        w = w.to(DEV)
+        (out * w).sum().backward()
+        (ref * w).sum().backward()
+        assert rel_l2(grids["grid_color"].grad, go["grid_color"].grad) <= TOL["color"], rows
+        got = torch.cat([q.grad.reshape(-1) for q in nice.color_decoder.parameters()])
+        exp = torch.cat([sdo["color_decoder." + k].grad.reshape(-1) for k, _ in nice.color_decoder.named_parameters()])
+        assert rel_l2(got, exp) <= 2e-4, rows
+        assert rel_l2(pp.grad, po.grad) <= 5e-3, rows

@@ -36,8 +36,10 @@ def _free_port():
     return p
 
 
-def _run(world, rank, group=None, mode="allreduce"):
-    """The mapping loop of one rank on cuda:0; returns CPU copies of the final map."""
+def _run(world, rank, group=None, mode="allreduce", force=False, graph=False):
+    """The mapping loop of one rank on cuda:0; returns CPU copies of the final map.
+    force: world 1 with the exchange's collectives issued anyway (a one-rank RCCL group);
+    graph: iteration 1 eager, then one iteration captured in a hipGraph and replayed ITERS - 1 times."""
     import importlib
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "tests"))
@@ -69,18 +71,32 @@ def _run(world, rank, group=None, mode="allreduce"):
     opt = P.ops.FusedAdam([{"params": [eng.decs["color"].param], "lr": 0.005}] +
                           [{"params": [c[k]], "lr": 0.005, "rows": rows[k]} for k in c])
     dec0 = eng.decs["color"].param.detach().cpu().clone()
-    if world == 1:
+    if world == 1 and not force:
         ex = None
     elif mode == "sharded":
-        ex = P.distributed.ShardedAdamExchange(eng, opt, group=group)
+        ex = P.distributed.ShardedAdamExchange(eng, opt, group=group, force_collectives=force)
     else:
-        ex = P.distributed.SparseGradExchange(eng, rows, group=group)
+        ex = P.distributed.SparseGradExchange(eng, rows, group=group, force_collectives=force)
     losses = []
-    for _ in range(ITERS):
+
+    def step():
         rl, _ = eng.iteration("color", frames, None, N_PER * (2 // world), (cam["H"], cam["W"]),
                               (cam["fx"], cam["fy"], cam["cx"], cam["cy"]), opt, seed=SEED, world=world, rank=rank,
                               exchange=ex)
-        losses.append(float(rl.sum()))
+        return rl
+
+    if graph:
+        losses.append(float(step().sum()))
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            rl = step()
+        for _ in range(ITERS - 1):
+            g.replay()
+            losses.append(float(rl.sum()))
+    else:
+        for _ in range(ITERS):
+            losses.append(float(step().sum()))
     torch.cuda.synchronize()
     out = {k: v.detach().cpu().clone() for k, v in c.items()}
     out["color_decoder"] = eng.decs["color"].param.detach().cpu().clone() - dec0
@@ -122,3 +138,40 @@ def test_two_rank_sharded_engine_matches_single_rank(tmp_path, mode):
         assert rel < 1e-3, (k, rel)
     rel = float((r0["color_decoder"] - full["color_decoder"]).norm() / full["color_decoder"].norm())
     assert float(full["color_decoder"].abs().max()) > 0 and rel < 1e-3, rel
+
+
+def _rccl1_worker(rank, port, path, mode):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        res = _run(1, 0, mode=mode, force=True, graph=True)
+        res["backend"] = torch.tensor([dist.get_backend() == "nccl"])
+        torch.save(res, os.path.join(path, "rccl1.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["allreduce", "sharded"])
+def test_world1_rccl_exchange_in_hipgraph_is_identity(tmp_path, mode):
+    """The N > 1 exchange path on one GPU: a one-rank RCCL group, the exchange's collectives issued
+    anyway (force_collectives: all-reduce, or reduce-scatter + sharded Adam + all-gather per backward
+    branch on two communicators) and captured with the iteration in a hipGraph.  At world 1 every
+    collective is an identity, so the map after 3 iterations equals the no-exchange run's — up to
+    float-atomic summation order in the grid-gradient scatter (rel 1e-5 of the map's change)."""
+    port = _free_port()
+    mp.spawn(_rccl1_worker, args=(port, str(tmp_path), mode), nprocs=1, join=True)
+    r = torch.load(tmp_path / "rccl1.pt", weights_only=True)
+    assert bool(r.pop("backend"))
+    ref = _run(1, 0, graph=True)
+    with np.load(os.path.join(GOLDEN, "tiny_scene.npz")) as z:
+        start = {k: torch.from_numpy(z[k]) for k in ("grid_middle", "grid_fine", "grid_color")}
+    np.testing.assert_allclose(r["losses"].numpy(), ref["losses"].numpy(), rtol=1e-6)
+    for k, s0 in start.items():
+        d, d_ref = r[k] - s0, ref[k] - s0
+        assert float(d_ref.abs().max()) > 0, k
+        assert float((d - d_ref).norm() / d_ref.norm()) <= 1e-5, k
+    rel = float((r["color_decoder"] - ref["color_decoder"]).norm() / ref["color_decoder"].norm())
+    assert rel <= 1e-5, rel
