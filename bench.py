@@ -516,8 +516,12 @@ def stress_iteration(dev, steps=10):
     Adam — replayed in a hipGraph.  Per-kernel HIP-event spans come from extra eager iterations;
     the forward's 3 trilinear lookups (3 KiB per sample) are priced against the HBM roof, its FLOPs
     against the fp32 MFMA roof."""
+    global PREFETCH
     scene = Room0Scene(dev, 0, cfg=dict(STRESS), path="fused", device_init=True)
     P = pkg()
+    if os.environ.get("NSLAM_BENCH_EAGER"):  # counter passes: every kernel alone on the chip
+        scene.engine.concurrent = False
+        PREFETCH = False
     for _ in range(2):
         scene.step()
     torch.cuda.synchronize()
@@ -609,11 +613,13 @@ def bulk_queries(scene, res=256, reps=2):
     return out
 
 
-def frame_io(dev, n=6):
+def frame_io(dev, n=6, n_prefetch=128, workers=8):
     """Frame source: Replica-format frames at room0 size (680×1200 JPEG colour,
     16-bit PNG depth, traj.txt) written to a temp folder, then read through datasets.Replica onto
     the device — decode + H2D per frame, float64 colour (the reference's, datasets.py:91) vs the
-    float32 colour the engine keeps resident."""
+    float32 colour the engine keeps resident; and through Replica.prefetch (the reference's
+    DataLoader worker, Tracker.py:64-65: `workers` decode processes, pinned buffers, H2D on a side
+    stream) over `n_prefetch` frames."""
     import tempfile
 
     import numpy as np
@@ -625,13 +631,14 @@ def frame_io(dev, n=6):
     with tempfile.TemporaryDirectory() as d:
         os.makedirs(os.path.join(d, "results"))
         yy, xx = np.mgrid[0:H, 0:W]
-        for i in range(n):  # smooth synthetic content (JPEG cost like a real frame, not noise)
+        nf = max(n, 16)  # files on disk; the read-ahead pass cycles through them
+        for i in range(nf):  # smooth synthetic content (JPEG cost like a real frame, not noise)
             img = np.stack([(xx * 255 // W + 20 * i) % 256, yy * 255 // H, (xx + yy) % 256], -1).astype(np.uint8)
             Image.fromarray(img).save(os.path.join(d, f"results/frame{i:06d}.jpg"), quality=95)
             Image.fromarray(rng.integers(5000, 30000, (H, W)).astype(np.uint16)).save(
                 os.path.join(d, f"results/depth{i:06d}.png"))
         with open(os.path.join(d, "traj.txt"), "w") as f:
-            for _ in range(n):
+            for _ in range(nf):
                 f.write(" ".join(str(v) for v in np.eye(4).ravel()) + "\n")
         cfg = {"dataset": "replica", "data": {"input_folder": d},
                "cam": {"H": H, "W": W, "fx": 600.0, "fy": 600.0, "cx": 599.5, "cy": 339.5,
@@ -648,7 +655,24 @@ def frame_io(dev, n=6):
             out["color_" + name] = {"ms_per_frame": dt * 1e3, "frames_per_s": 1.0 / dt,
                                     "device_bytes_per_frame": H * W * (3 * (8 if cd == torch.float64 else 4) + 4),
                                     "h2d_bytes_per_frame": H * W * (3 + 4)}
-    out["workload"] = f"{n} Replica-format frames {H}x{W} (JPEG q95 colour, 16-bit PNG depth), Pillow decode + H2D"
+            # read-ahead: worker processes decode, H2D on a side stream (a consumer would render meanwhile)
+            ds = P.get_dataset(cfg, None, 1.0, device=dev, color_dtype=cd)
+            torch.cuda.synchronize()
+            t_start = time.perf_counter()
+            k, t0 = -1, None
+            for _ in ds.prefetch([i % nf for i in range(n_prefetch)], workers=workers, ahead=2 * workers):
+                if t0 is None:  # steady state: from the first frame handed out (workers started)
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                k += 1
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            dt = (t1 - t0) / max(k, 1)
+            out["prefetch_" + name] = {"ms_per_frame": dt * 1e3, "frames_per_s": 1.0 / dt, "frames": k,
+                                       "workers": workers, "startup_ms": (t0 - t_start) * 1e3,
+                                       "frames_per_s_incl_startup": (k + 1) / (t1 - t_start)}
+    out["workload"] = (f"{n} Replica-format frames {H}x{W} (JPEG q95 colour, 16-bit PNG depth), Pillow decode + H2D, "
+                       f"one by one (dataset[i]) and {n_prefetch} through dataset.prefetch ({workers} workers)")
     return out
 
 
@@ -886,6 +910,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture")
+    ap.add_argument("--serial-branches", action="store_true",
+                    help="the backward's branches one after the other (counter passes: every kernel alone "
+                         "on the chip, so its GRBM window holds no other work)")
     ap.add_argument("--no-stress", action="store_true", help="skip the 512^3 grid-query HBM measurement")
     ap.add_argument("--no-frames", action="store_true", help="skip the room0 frames/s (tracking + mapping stages)")
     ap.add_argument("--no-bulk", action="store_true", help="skip the forward-only mesher / render_img queries")
@@ -935,6 +962,8 @@ def main():
     if args.pixels:
         cfg["pixels"] = args.pixels
     scene = Room0Scene(dev, rank, cfg=cfg, path=args.path)
+    if args.serial_branches and getattr(scene, "engine", None) is not None:
+        scene.engine.concurrent = False
     sharded = world > 1 or args.force_exchange
     for _ in range(args.warmup):
         scene.step(sharded=sharded)

@@ -11,11 +11,17 @@ crop_size interpolation and crop_edge are exact restatements.
 
 `color_dtype=torch.float32` keeps a frame at half the bytes on the device (the fused engine reads
 f32); the default float64 is the reference's (datasets.py:91).
+
+`BaseDataset.prefetch(indices)` is the reference's DataLoader worker (Tracker.py:64-65, Mapper.py:
+frame_reader): worker processes decode ahead into pinned host memory and each frame's H2D copy and
+device-side normalisation run on a side stream, so decode overlaps the consumer's GPU work; it
+yields exactly what `dataset[i]` returns (the same host half and device half).
 Out of scope: CoFusion (OpenEXR), TUM-RGBD, lens undistortion (cv2.undistort) — none is a BASELINE
 config; a config asking for `distortion` raises.
 """
 from __future__ import annotations
 
+import collections
 import glob
 import os
 
@@ -72,16 +78,25 @@ class BaseDataset(torch.utils.data.Dataset):
             lut = self._u8_lut = (torch.arange(256, dtype=torch.float64) / 255.0).to(device)
         return lut
 
+    def _load_host(self, index):
+        """The host half of __getitem__: decoded colour bytes (uint8 [H,W,3]) and depth in metres
+        before scaling (float32 [H,W]) — the part a prefetch worker process runs."""
+        u8 = torch.from_numpy(np.ascontiguousarray(_read_color(self.color_paths[index])))
+        depth = torch.from_numpy(_read_depth(self.depth_paths[index]).astype(np.float32) / np.float32(self.png_depth_scale))
+        return u8, depth
+
     def __getitem__(self, index):
+        return self._finish(index, *self._load_host(index))
+
+    def _finish(self, index, u8, depth, non_blocking=False):
         # Only the decoded bytes cross PCIe for colour (uint8: 1/8 of the reference's float64 copy).
         # /255 (float64, datasets.py:91) is a 256-entry table divided on the host and gathered on
         # the device — torch's device kernels turn a scalar division into a reciprocal multiply,
         # which is not the reference's correctly-rounded quotient.  Depth is divided on the host
         # (float32, :92) for the same reason.  Resize and crops then run on the device.
-        u8 = torch.from_numpy(np.ascontiguousarray(_read_color(self.color_paths[index]))).to(self.device)
+        u8 = u8.to(self.device, non_blocking=non_blocking)
         color = self._lut(u8.device)[u8.long()]
-        depth = torch.from_numpy(_read_depth(self.depth_paths[index]).astype(np.float32) / np.float32(self.png_depth_scale))
-        depth = depth.to(self.device)
+        depth = depth.to(self.device, non_blocking=non_blocking)
         H, W = depth.shape
         if color.shape[:2] != (H, W):  # cv2.resize(color, (W, H)) INTER_LINEAR (datasets.py:94)
             color = F.interpolate(color.permute(2, 0, 1)[None], (H, W), mode="bilinear",
@@ -98,6 +113,59 @@ class BaseDataset(torch.utils.data.Dataset):
         pose = self.poses[index]
         pose[:3, 3] *= self.scale  # in place, as datasets.py:112
         return index, color.to(self.color_dtype).contiguous(), depth.contiguous(), pose.to(self.device)
+
+    def prefetch(self, indices=None, workers=4, ahead=8):
+        """Frames `indices` (default: all, in order) as dataset[i] returns them, read ahead: `workers`
+        processes (torch DataLoader, fork; they run _load_host only, no GPU call) decode up to
+        `ahead` frames ahead into pinned host memory, and each frame's H2D copy + normalisation is
+        enqueued on a side stream as soon as it arrives, one frame before it is handed out — the
+        current stream waits for that frame's work only.  Same values as dataset[i] (same code)."""
+        idx = list(range(len(self))) if indices is None else [int(i) for i in indices]
+        if not idx:
+            return
+        dev = torch.device(self.device)
+        use_stream = dev.type == "cuda"
+        loader = torch.utils.data.DataLoader(
+            _HostFrames(self), batch_size=None, sampler=idx, num_workers=workers,
+            pin_memory=use_stream, prefetch_factor=max(1, -(-ahead // max(workers, 1))) if workers else None)
+        side = torch.cuda.Stream(dev) if use_stream else None
+        pending = collections.deque()
+
+        def ready():
+            item, ev = pending.popleft()
+            if ev is not None:
+                torch.cuda.current_stream(dev).wait_event(ev)
+                for t in item[1:]:
+                    t.record_stream(torch.cuda.current_stream(dev))
+            return item
+
+        for i, u8, depth in loader:
+            if side is not None:
+                side.wait_stream(torch.cuda.current_stream(dev))  # (the LUT, the poses' earlier users)
+                with torch.cuda.stream(side):
+                    item = self._finish(int(i), u8, depth, non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+            else:
+                item, ev = self._finish(int(i), u8, depth), None
+            pending.append((item, ev))
+            if len(pending) > 1:
+                yield ready()
+        while pending:
+            yield ready()
+
+
+class _HostFrames(torch.utils.data.Dataset):
+    """The host half of a BaseDataset (file decode, BaseDataset._load_host) for prefetch workers."""
+
+    def __init__(self, ds):
+        self.ds = ds
+
+    def __len__(self):
+        return len(self.ds)
+
+    def __getitem__(self, index):
+        return (index,) + self.ds._load_host(index)
 
 
 class Replica(BaseDataset):

@@ -164,3 +164,30 @@ def test_device_frames_equal_host_frames(tmp_path):
         _, c0, d0, p0 = host[k]
         _, c1, d1, p1 = dev[k]
         assert c1.is_cuda and torch.allclose(c1.cpu(), c0, rtol=0, atol=1e-12) and torch.equal(d1.cpu(), d0) and torch.equal(p1.cpu(), p0)
+
+
+def _prefetch_equals_getitem(tmp_path, device):
+    test_scannet_folder_resize_sort_and_crop(tmp_path)  # writes the folder
+    cfg = _cfg("scannet", str(tmp_path), 24, 32, 1000.0, crop_edge=2)
+    a = P.get_dataset(cfg, None, 0.5, device=device)
+    b = P.get_dataset(cfg, None, 0.5, device=device)
+    order = [2, 0, 1]
+    got = list(a.prefetch(order, workers=2, ahead=3))
+    assert [g[0] for g in got] == order
+    for g in got:
+        e = b[g[0]]
+        assert g[1].device == e[1].device
+        for x, y in zip(g[1:], e[1:]):
+            assert x.dtype == y.dtype and torch.equal(x.cpu(), y.cpu())
+
+
+def test_prefetch_yields_getitem(tmp_path):
+    """BaseDataset.prefetch (the reference's DataLoader worker, Tracker.py:64-65): decode in worker
+    processes, then the same device half as __getitem__ — the same tuples, in the requested order."""
+    _prefetch_equals_getitem(tmp_path, "cpu")
+
+
+@pytest.mark.gpu
+def test_prefetch_yields_getitem_on_device(tmp_path):
+    """The same on the GPU: pinned host buffers, H2D + normalisation on a side stream."""
+    _prefetch_equals_getitem(tmp_path, "cuda:0")

@@ -8,7 +8,9 @@ TAG=${1:?tag}
 OUT=gpurun_out/$TAG/counters
 mkdir -p $OUT
 export TMPDIR=/tmp
-ROOM0="python bench.py --steps 6 --warmup 3 --no-cpu-baseline --eager --no-stress --no-frames --no-bulk"
+# eager launches, branches serialised, no ray prefetch: each kernel runs alone, so its counter window
+# (GRBM_GUI_ACTIVE) holds no other kernel's work
+ROOM0="python bench.py --steps 6 --warmup 3 --no-cpu-baseline --eager --serial-branches --no-prefetch --no-stress --no-frames --no-bulk"
 STRESS="python bench.py --leg stress_iter"
 GRIDQ="python bench.py --leg stress"   # the standalone grid query (k_grid_fwd) at the stress shape
 pass() {  # name, command, counters...

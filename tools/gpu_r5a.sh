@@ -5,7 +5,7 @@ timeout -k 10 240 python -u tools/probes/wave_timeline.py > $D/tl_default.log 2>
 cat $D/tl_default.log
 timeout -k 10 240 python -u tools/probes/wave_timeline.py --no-prefetch --serial > $D/tl_serial.log 2>&1 || { tail -30 $D/tl_serial.log; exit 1; }
 cat $D/tl_serial.log
-timeout -k 10 400 python -u -m pytest -x -v --timeout 150 --timeout-method thread tests/test_gpu_decoders.py tests/test_gpu_sharded.py > $D/tests.log 2>&1 || { tail -40 $D/tests.log; exit 1; }
+timeout -k 10 400 python -u -m pytest -x -v --timeout 150 --timeout-method thread tests/test_gpu_decoders.py tests/test_gpu_sharded.py tests/test_datasets_cpu.py > $D/tests.log 2>&1 || { tail -40 $D/tests.log; exit 1; }
 tail -3 $D/tests.log
 timeout -k 10 200 python -u bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-stress --no-bulk --no-frames > $D/bench_default.json 2> $D/bench_default.err || { tail -20 $D/bench_default.err; exit 1; }
 tail -c 600 $D/bench_default.json
@@ -13,3 +13,5 @@ timeout -k 10 200 python -u bench.py --steps 50 --warmup 10 --no-cpu-baseline --
 tail -c 900 $D/bench_rccl1_allreduce.json
 timeout -k 10 200 python -u bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-stress --no-bulk --no-frames --force-exchange --exchange sharded > $D/bench_rccl1_sharded.json 2> $D/bench_rccl1_sharded.err || { tail -20 $D/bench_rccl1_sharded.err; exit 1; }
 tail -c 900 $D/bench_rccl1_sharded.json
+timeout -k 10 200 python -u bench.py --leg frame_io > $D/frame_io.json 2> $D/frame_io.err || { tail -20 $D/frame_io.err; exit 1; }
+cat $D/frame_io.json

@@ -9,6 +9,7 @@ import sys
 from collections import defaultdict
 
 SIMDS = 1024  # MI355X: 256 CUs x 4 SIMDs
+F_MAX_GHZ = 2.4  # MI355X peak engine clock
 
 
 def main():
@@ -35,11 +36,17 @@ def main():
         for c, v in sorted(m.items()):
             print(f"   {c:28s} {v:16.1f}")
         # derived (MI355X_MICROARCH.md: GRBM_GUI_ACTIVE sums the 8 XCDs' cycles; SQ_WAVE_CYCLES and
-        # SQ_ACTIVE_INST_* count quad-cycles, SQ_VALU_MFMA_BUSY_CYCLES cycles; 1024 SIMDs)
-        if "GRBM_GUI_ACTIVE" in m:
-            clk = m["GRBM_GUI_ACTIVE"] / 8
-            simd_cyc = clk * SIMDS
-            print(f"   {'(clock GHz)':28s} {clk / (d * 1e3):16.3f}")
+        # SQ_ACTIVE_INST_* count quad-cycles, SQ_VALU_MFMA_BUSY_CYCLES cycles; 1024 SIMDs).
+        # SIMD-cycles = the kernel's own rocprof duration x its clock: GRBM_GUI_ACTIVE / 8 over the
+        # duration when that is a clock the part can run (<= 2.4 GHz), else 2.4 GHz — a GRBM window
+        # that yields more also counted other work (launch overhead of a short kernel, or a kernel
+        # beside it), and normalising by it would understate every fraction.
+        if "GRBM_GUI_ACTIVE" in m and d > 0:
+            ghz_grbm = m["GRBM_GUI_ACTIVE"] / 8 / (d * 1e3)
+            ghz = min(ghz_grbm, F_MAX_GHZ)
+            simd_cyc = d * 1e3 * ghz * SIMDS
+            flag = "" if ghz_grbm <= F_MAX_GHZ else f"   (GRBM window {ghz_grbm:.2f} GHz: capped)"
+            print(f"   {'(clock GHz)':28s} {ghz:16.3f}{flag}")
             if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
                 print(f"   {'(MFMA busy / SIMD-cycles)':28s} {m['SQ_VALU_MFMA_BUSY_CYCLES'] / simd_cyc:16.3f}")
             if "SQ_WAVE_CYCLES" in m:
