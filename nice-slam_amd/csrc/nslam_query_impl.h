@@ -1345,9 +1345,17 @@ __device__ __forceinline__ void fwd_part_color(const QueryKArgs& a, const Pt& q,
 #ifndef NSLAM_FWD_LB
 #define NSLAM_FWD_LB 2  // min waves per SIMD (experiments: 3..5 trade VGPRs for occupancy)
 #endif
+// register cap of the forward (experiments: a SIMD's wave slots are shared with the ray prefetch's
+// sampler / gather waves of the next iteration, which run beside this launch)
+#ifdef NSLAM_FWD_NUMVGPR
+#define NSLAM_FWD_ATTR __attribute__((amdgpu_num_vgpr(NSLAM_FWD_NUMVGPR)))
+#else
+#define NSLAM_FWD_ATTR
+#endif
 constexpr int kVecFloats = 744;  // XyzPack vector section (740) rounded to float4s
 template <int STAGE, int NPARTS, bool TAPE>
-__global__ __launch_bounds__(256, NSLAM_FWD_LB) void k_query_fwd_parts(QueryKArgs a, float* __restrict__ occ_mid) {
+NSLAM_FWD_ATTR __global__ __launch_bounds__(256, NSLAM_FWD_LB) void k_query_fwd_parts(QueryKArgs a,
+                                                                                     float* __restrict__ occ_mid) {
   const int part = (int)(blockIdx.x % NPARTS);
   const int lane = threadIdx.x & 63;
   TL(0, 0, part);

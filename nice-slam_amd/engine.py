@@ -107,6 +107,11 @@ class MappingEngine:
         # launch per decoder (the library then runs a colour tape backward's two kernels in sequence)
         self.merge = True
         self._lean_ev = None
+        # where the ray prefetch of the next iteration forks off the main stream: "start" (beside the
+        # forward) or "after_fwd" (beside the loss and the backward: the forward's waves then have every
+        # wave slot of the chip; a prefetch sampler wave resident on a SIMD leaves room for only two of
+        # the forward's three)
+        self.prefetch_at = os.environ.get("NSLAM_PREFETCH_AT", "start")
         for k, v in c.items():
             if not v.is_contiguous(memory_format=torch.channels_last_3d):
                 raise ValueError(f"{k} must be channels-last (ops.channels_last)")
@@ -428,14 +433,21 @@ class MappingEngine:
             if self._pre_stream is None:
                 self._pre_stream = torch.cuda.Stream(self.device)
             side = self._pre_stream
-            side.wait_stream(main)  # the previous iteration's backward has released `nxt`
-            with torch.cuda.stream(side):
-                rays(out=nxt)  # the next iteration's batch, beside this iteration's render + backward
+
+            def launch_prefetch():
+                side.wait_stream(main)  # the previous iteration's backward has released `nxt`
+                with torch.cuda.stream(side):
+                    rays(out=nxt)  # the next iteration's batch, beside this iteration's render + backward
+
+            if self.prefetch_at == "start":
+                launch_prefetch()
             ro, rd, gd, gc, keep, z = cur
         else:
             ro, rd, gd, gc, keep, z = rays()
         mirror = hasattr(optimizer, "set_mirror")
         raw = self.query_fwd(stage, ro, rd, z, defer_occ=True, tape="color" in dnames)
+        if side is not None and self.prefetch_at != "start":
+            launch_prefetch()  # forks after the forward: beside the loss and the backward
         _, _, _, ray_loss, g_raw = ops.render_loss(raw, z, gd, gc, keep, mode="mapper", use_color=stage == "color",
                                                    w_color=self.w_color, occ_add=self.occ_add)
         if not self._clean:

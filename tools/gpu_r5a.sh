@@ -15,3 +15,11 @@ timeout -k 10 200 python -u bench.py --steps 50 --warmup 10 --no-cpu-baseline --
 tail -c 900 $D/bench_rccl1_sharded.json
 timeout -k 10 200 python -u bench.py --leg frame_io > $D/frame_io.json 2> $D/frame_io.err || { tail -20 $D/frame_io.err; exit 1; }
 cat $D/frame_io.json
+timeout -k 10 300 python -u tools/probes/touched_rows.py > $D/touched_rows.json 2> $D/touched_rows.err || { tail -20 $D/touched_rows.err; exit 1; }
+cat $D/touched_rows.json
+NSLAM_PREFETCH_AT=after_fwd timeout -k 10 240 python -u tools/probes/wave_timeline.py > $D/tl_after_fwd.log 2>&1 || { tail -30 $D/tl_after_fwd.log; exit 1; }
+cat $D/tl_after_fwd.log
+for r in 1 2; do for at in start after_fwd; do
+NSLAM_PREFETCH_AT=$at timeout -k 10 200 python -u bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-stress --no-bulk --no-frames > $D/ab_${at}_$r.json 2> $D/ab_$at.err || { tail -20 $D/ab_$at.err; exit 1; }
+python -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[2], round(d['value']/1e6,2), 'M/s', round(d['ms_per_step'],4), 'ms')" $D/ab_${at}_$r.json "$at round $r"
+done; done
