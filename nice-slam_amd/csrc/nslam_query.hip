@@ -189,9 +189,11 @@ extern "C" int nslam_debug_phases(unsigned long long* out, int64_t n) {
   if (n > (int64_t)5 * kPhaseWaves * 16) n = (int64_t)5 * kPhaseWaves * 16;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
-// per-wave timeline {start, end, HW_ID | XCC_ID << 32, tile} of slots 0 forward, 1 mask-only bwd, 2 wgrad
+#endif
+#if defined(NSLAM_PHASES) || defined(NSLAM_TIMELINE)
+// per-wave timeline {start, end, HW_ID | XCC_ID << 32, tag} of slots 0 forward, 1 mask-only bwd, 2 wgrad
 extern "C" int nslam_debug_timeline(unsigned long long* out, int64_t n) {
-  if (n > (int64_t)3 * kPhaseWaves * 4) n = (int64_t)3 * kPhaseWaves * 4;
+  if (n > (int64_t)3 * kTlWaves * 4) n = (int64_t)3 * kTlWaves * 4;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tl), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -212,28 +212,34 @@ __device__ unsigned long long g_phase[5 * kPhaseWaves * 16];  // one-TU phases b
     if ((threadIdx.x & 63) == 0 && w_ < kPhaseWaves)                                                      \
       g_phase[((size_t)(dec) * kPhaseWaves + w_) * 16 + (k)] = __builtin_amdgcn_s_memtime();              \
   } while (0)
-// Timeline (same build): per wave of kernel slot k (0 forward, 1 mask-only backward, 2 k_color_wgrad)
-// {start, end} of s_memrealtime (100 MHz, one clock for all XCDs), HW_ID | XCC_ID << 32, tile
-__device__ unsigned long long g_tl[3 * kPhaseWaves * 4];
-__device__ __forceinline__ void tl_mark(int slot, int end, long long tile) {
+#else
+#define PHASE(dec, k) \
+  do {                \
+  } while (0)
+#endif
+// Timeline (make phases, or make timeline: the marks below only, so the kernels keep their production
+// register allocation — the phase marks cost the forward 88 VGPRs and its third wave per SIMD): per
+// wave of kernel slot k (0 forward, 1 mask-only backward, 2 k_color_wgrad) {start, end} of
+// s_memrealtime (100 MHz, one clock for all XCDs), HW_ID | XCC_ID << 32, and a tag
+#if defined(NSLAM_PHASES) || defined(NSLAM_TIMELINE)
+constexpr int kTlWaves = 1 << 15;
+__device__ unsigned long long g_tl[3 * kTlWaves * 4];
+__device__ __forceinline__ void tl_mark(int slot, int end, long long tag) {
   const int64_t w_ = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if ((threadIdx.x & 63) != 0 || w_ >= kPhaseWaves) return;
-  unsigned long long* o = g_tl + ((size_t)slot * kPhaseWaves + w_) * 4;
+  if ((threadIdx.x & 63) != 0 || w_ >= kTlWaves) return;
+  unsigned long long* o = g_tl + ((size_t)slot * kTlWaves + w_) * 4;
   o[end] = __builtin_amdgcn_s_memrealtime();
   if (!end) {
     const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
     const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
     o[2] = (unsigned long long)hw | ((unsigned long long)(xcc & 15) << 32);
-    o[3] = (unsigned long long)tile;
+    o[3] = (unsigned long long)tag;
   }
 }
-#define TL(slot, end, tile) tl_mark(slot, end, tile)
+#define TL(slot, end, tag) tl_mark(slot, end, tag)
 #else
-#define PHASE(dec, k) \
-  do {                \
-  } while (0)
-#define TL(slot, end, tile) \
-  do {                      \
+#define TL(slot, end, tag) \
+  do {                     \
   } while (0)
 #endif
 

@@ -1,6 +1,6 @@
-"""Per-wave timeline of the mapping iteration's big kernels (phases build: make -C nice-slam_amd/csrc phases).
+"""Per-wave timeline of the mapping iteration's big kernels (timeline build: make -C nice-slam_amd/csrc timeline).
 
-NSLAM_LIB=nice-slam_amd/libnslam_phases.so python tools/probes/wave_timeline.py [--no-prefetch] [--serial]
+NSLAM_LIB=nice-slam_amd/libnslam_tl.so python tools/probes/wave_timeline.py [--no-prefetch] [--serial]
 Every wave of k_query_fwd_parts (slot 0), k_dec_bwd_multi (slot 1) and k_color_wgrad (slot 2) records
 s_memrealtime (100 MHz, one clock for every XCD) at its start and end, and its HW_ID / XCC_ID.  Prints,
 per kernel of the last iteration: the span, when waves start (dispatch), their lifetimes, the waves each
@@ -16,7 +16,7 @@ import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, REPO)
-os.environ.setdefault("NSLAM_LIB", os.path.join(REPO, "nice-slam_amd", "libnslam_phases.so"))
+os.environ.setdefault("NSLAM_LIB", os.path.join(REPO, "nice-slam_amd", "libnslam_tl.so"))
 import bench  # noqa: E402
 
 W = 1 << 15
