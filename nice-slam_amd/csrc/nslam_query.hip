@@ -1,6 +1,8 @@
 // nslam_query.hip — C-ABI entry points of the fused point query (include/nslam.h): forward
 // launches, backward dispatch (the per-decoder backward launchers are compiled in
 // nslam_query_dec.hip), workspace / tape / mask sizes and the pack layout.
+#include <string.h>
+
 #include "nslam_query_impl.h"
 
 using namespace nslamq;
@@ -27,7 +29,7 @@ extern "C" int nslam_query_fwd(const nslam_query_cfg* cfg, const double* pts, in
 
 extern "C" size_t nslam_query_fwd_workspace_size(const nslam_query_cfg* cfg, int64_t n_pts) {
   if (!cfg || n_pts <= 0 || cfg->stage < NSLAM_STAGE_FINE || cfg->stage > NSLAM_STAGE_COLOR) return 0;
-  return ((size_t)n_pts * sizeof(float) + 255) & ~(size_t)255;
+  return (((size_t)n_pts * sizeof(float) + 255) & ~(size_t)255) + 256;  // + the dynamic forward's counter
 }
 
 extern "C" int nslam_query_fwd_ws(const nslam_query_cfg* cfg, const double* pts, int64_t n_pts, float* raw, void* ws,
@@ -61,7 +63,34 @@ extern "C" int nslam_query_fwd_ws(const nslam_query_cfg* cfg, const double* pts,
   const int64_t tiles = (n_pts + 31) / 32;
   const int color_parts = forced_parts == 2 || forced_parts == 3 ? forced_parts : (3 * tiles <= wave_slots ? 3 : 2);
   const dim3 b256(256);
-  if (cfg->stage == NSLAM_STAGE_FINE)
+  // forward variant: NSLAM_FWD_MODE=units (one-wave workgroups per decoder-tile), dyn (a counter), parts
+  static const int mode = [] {
+    const char* e = getenv("NSLAM_FWD_MODE");
+    if (!e) return 1;
+    return !strcmp(e, "dyn") ? 2 : !strcmp(e, "parts") ? 0 : 1;
+  }();
+  if (mode == 1) {
+    const int np = cfg->stage == NSLAM_STAGE_COLOR ? 3 : 2;
+    const dim3 g((unsigned)(tiles * np)), b64(64);
+    if (cfg->stage == NSLAM_STAGE_FINE)
+      hipLaunchKernelGGL((k_query_fwd_units<NSLAM_STAGE_FINE, false>), g, b64, 0, s, a, occ);
+    else if (cfg->act_tape)
+      hipLaunchKernelGGL((k_query_fwd_units<NSLAM_STAGE_COLOR, true>), g, b64, 0, s, a, occ);
+    else
+      hipLaunchKernelGGL((k_query_fwd_units<NSLAM_STAGE_COLOR, false>), g, b64, 0, s, a, occ);
+  } else if (mode == 2) {
+    const int np = cfg->stage == NSLAM_STAGE_COLOR ? 3 : 2;
+    unsigned* ctr = reinterpret_cast<unsigned*>(static_cast<char*>(ws) + (need - 256));
+    if (hipMemsetAsync(ctr, 0, 8, s) != hipSuccess) return hip_status();
+    const int64_t waves = tiles * np < wave_slots ? tiles * np : wave_slots;
+    const dim3 g((unsigned)((waves + 3) / 4));
+    if (cfg->stage == NSLAM_STAGE_FINE)
+      hipLaunchKernelGGL((k_query_fwd_dyn<NSLAM_STAGE_FINE, false>), g, b256, 0, s, a, occ, ctr);
+    else if (cfg->act_tape)
+      hipLaunchKernelGGL((k_query_fwd_dyn<NSLAM_STAGE_COLOR, true>), g, b256, 0, s, a, occ, ctr);
+    else
+      hipLaunchKernelGGL((k_query_fwd_dyn<NSLAM_STAGE_COLOR, false>), g, b256, 0, s, a, occ, ctr);
+  } else if (cfg->stage == NSLAM_STAGE_FINE)
     hipLaunchKernelGGL((k_query_fwd_parts<NSLAM_STAGE_FINE, 2, false>), dim3((unsigned)(groups * 2)), b256, 0, s, a,
                        occ);
   else if (color_parts == 2 && cfg->act_tape)

@@ -1405,6 +1405,92 @@ NSLAM_FWD_ATTR __global__ __launch_bounds__(256, NSLAM_FWD_LB) void k_query_fwd_
   TL(0, 1, 0);
 }
 
+// Decoder-parallel forward with DYNAMIC work distribution: the same per-decoder units (one decoder of one
+// 32-point tile: fwd_part_fine / fwd_part_middle / fwd_part_color, the same arithmetic and outputs as
+// k_query_fwd_parts), but a launch of at most one wave per wave slot whose waves take units off a
+// device counter until none is left — the heaviest (fine: two gathers, 20 GEMMs) first.  A SIMD whose
+// waves drew light units takes more of them, so the launch ends when the chip's work does, not when the
+// unluckiest SIMD's statically assigned mix does.  ctr: 2 uint32 zeroed before the launch.
+template <int STAGE, bool TAPE>
+__global__ __launch_bounds__(256, 3) void k_query_fwd_dyn(QueryKArgs a, float* __restrict__ occ_mid,
+                                                                      unsigned* __restrict__ ctr) {
+  constexpr int NP = STAGE == NSLAM_STAGE_COLOR ? 3 : 2;
+  // every part's vector section (biases, output rows, Fourier B) once per workgroup
+  __shared__ __attribute__((aligned(16))) float vsec[NP][kVecFloats];
+  {
+    const float* s0 = a.c.packed[NSLAM_DEC_MIDDLE] + XyzPack{1}.V();
+    const float* s1 = a.c.packed[NSLAM_DEC_FINE] + XyzPack{2}.V();
+    const float* s2 = NP == 3 ? a.c.packed[NSLAM_DEC_COLOR] + XyzPack{1}.V() : nullptr;
+    for (int i = threadIdx.x; i < 740; i += 256) {
+      vsec[0][i] = s0[i];
+      vsec[1][i] = s1[i];
+      if (NP == 3) vsec[NP - 1][i] = s2[i];
+    }
+    __syncthreads();
+  }
+  const int lane0 = threadIdx.x & 63;
+  const int64_t ntiles = (a.n + 31) / 32;
+  const int64_t nunits = ntiles * NP;
+  TL(0, 0, 0);
+  for (;;) {
+    unsigned u = 0;
+    if (lane0 == 0) u = atomicAdd(ctr, 1u);
+    u = __builtin_amdgcn_readfirstlane(u);
+    if ((int64_t)u >= nunits) break;  // wave-uniform
+    // units [0, T): fine; [T, 2T): middle; [2T, 3T): colour
+    const int part = (int64_t)u < ntiles ? 1 : (int64_t)u < 2 * ntiles ? 0 : 2;
+    const int64_t tile = (int64_t)u - (part == 1 ? 0 : part == 0 ? ntiles : 2 * ntiles);
+    // every lane-dependent address (weight fragments, vector tiles) is loop-invariant: laundered per unit,
+    // so none of their loads is hoisted out of the loop to pin registers for all of it
+    int lane = lane0;
+    asm volatile("" : "+v"(lane));
+    const int64_t idx = tile * 32 + (lane & 31);
+    const Pt q = load_point(a, idx);
+    if (part == 1) {
+      fwd_part_fine<STAGE>(a, q, tile, idx, lane, vsec[1]);
+    } else if (part == 0) {
+      fwd_part_middle(a, q, tile, idx, lane, occ_mid, vsec[0]);
+    } else if (NP == 3) {
+      fwd_part_color<TAPE>(a, q, tile, idx, lane, vsec[NP - 1]);
+    }
+  }
+  TL(0, 1, 0);
+}
+
+// Decoder-parallel forward, one wave per workgroup: unit u = blockIdx is one decoder of one 32-point
+// tile — [0, T) fine (two gathers, 20 GEMMs: the heaviest, dispatched first), [T, 2T) middle, [2T, 3T)
+// colour — with the same per-decoder code and outputs as k_query_fwd_parts.  With one-wave workgroups
+// the dispatcher refills every wave slot the moment its wave exits, so the launch balances itself over
+// the SIMDs (k_query_fwd_parts' 4-wave workgroups of middle-then-colour waves left the SIMDs that drew
+// two of them running ~25 us after the others: tools/probes/wave_timeline.py, profiles/r05_*).
+template <int STAGE, bool TAPE>
+__global__ __launch_bounds__(64, 3) void k_query_fwd_units(QueryKArgs a, float* __restrict__ occ_mid) {
+  const int64_t ntiles = (a.n + 31) / 32;
+  const int64_t u = blockIdx.x;
+  const int part = u < ntiles ? 1 : u < 2 * ntiles ? 0 : 2;
+  const int64_t tile = u - (part == 1 ? 0 : part == 0 ? ntiles : 2 * ntiles);
+  TL(0, 0, part);
+  // this unit's decoder vector section (biases, output rows, Fourier B), read by every layer
+  __shared__ __attribute__((aligned(16))) float vsec[kVecFloats];
+  {
+    const int d = part == 0 ? NSLAM_DEC_MIDDLE : part == 1 ? NSLAM_DEC_FINE : NSLAM_DEC_COLOR;
+    const float* src = a.c.packed[d] + XyzPack{d == NSLAM_DEC_FINE ? 2 : 1}.V();
+    for (int i = threadIdx.x; i < 740; i += 64) vsec[i] = src[i];
+    __syncthreads();
+  }
+  const int lane = threadIdx.x;
+  const int64_t idx = tile * 32 + (lane & 31);
+  const Pt q = load_point(a, idx);
+  if (part == 1) {
+    fwd_part_fine<STAGE>(a, q, tile, idx, lane, vsec);
+  } else if (part == 0) {
+    fwd_part_middle(a, q, tile, idx, lane, occ_mid, vsec);
+  } else if (STAGE == NSLAM_STAGE_COLOR) {
+    fwd_part_color<TAPE>(a, q, tile, idx, lane, vsec);
+  }
+  TL(0, 1, 0);
+}
+
 static __global__ __launch_bounds__(256) void k_occ_combine(float* __restrict__ raw, const float* __restrict__ occ_mid,
                                                      int64_t n) {
   const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
