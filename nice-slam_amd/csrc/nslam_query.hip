@@ -53,23 +53,34 @@ extern "C" int nslam_query_fwd_ws(const nslam_query_cfg* cfg, const double* pts,
     const char* e = getenv("NSLAM_FWD_PARTS");
     return e ? atoi(e) : 0;
   }();
-  static const int64_t wave_slots = [] {
+  static const int64_t n_cus = [] {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
       cus = 256;
-    return (int64_t)cus * 4 * 3;
+    return (int64_t)cus;
   }();
+  const int64_t wave_slots = n_cus * 4 * 3;
   const int64_t tiles = (n_pts + 31) / 32;
   const int color_parts = forced_parts == 2 || forced_parts == 3 ? forced_parts : (3 * tiles <= wave_slots ? 3 : 2);
   const dim3 b256(256);
-  // forward variant: NSLAM_FWD_MODE=units (one-wave workgroups per decoder-tile), dyn (a counter), parts
+  // forward variant: NSLAM_FWD_MODE=pc (producer / consumer waves, one persistent workgroup per CU),
+  // units (one-wave workgroups per decoder-tile), dyn (a counter), parts
   static const int mode = [] {
     const char* e = getenv("NSLAM_FWD_MODE");
     if (!e) return 1;
-    return !strcmp(e, "dyn") ? 2 : !strcmp(e, "parts") ? 0 : 1;
+    return !strcmp(e, "pc") ? 3 : !strcmp(e, "dyn") ? 2 : !strcmp(e, "parts") ? 0 : 1;
   }();
-  if (mode == 1) {
+  if (mode == 3) {
+    const int64_t units = tiles * (cfg->stage == NSLAM_STAGE_COLOR ? 3 : 2);
+    const dim3 g((unsigned)(units < n_cus ? units : n_cus)), b(64 * kPcWaves);
+    if (cfg->stage == NSLAM_STAGE_FINE)
+      hipLaunchKernelGGL((k_query_fwd_pc<NSLAM_STAGE_FINE, false>), g, b, 0, s, a, occ);
+    else if (cfg->act_tape)
+      hipLaunchKernelGGL((k_query_fwd_pc<NSLAM_STAGE_COLOR, true>), g, b, 0, s, a, occ);
+    else
+      hipLaunchKernelGGL((k_query_fwd_pc<NSLAM_STAGE_COLOR, false>), g, b, 0, s, a, occ);
+  } else if (mode == 1) {
     const int np = cfg->stage == NSLAM_STAGE_COLOR ? 3 : 2;
     const dim3 g((unsigned)(tiles * np)), b64(64);
     if (cfg->stage == NSLAM_STAGE_FINE)

@@ -154,6 +154,45 @@ __device__ __forceinline__ void gather_pair(const nslam_grid& gA, const nslam_gr
   }
 }
 
+// gather_tile's trilinear feature software-pipelined like gather_pair (corner k + 1's row loads in flight
+// while corner k is summed; the same sum order, so the same values) with its corners formed lazily
+__device__ __forceinline__ f32x16 gather_one(const nslam_grid& g, const Pt& q, int lane) {
+  const int h = lane >> 5;
+  const LazyCell A(g, q);
+  f32x16 acc = zero16();
+  auto load = [&](int k, f32x4 (&v)[4], float& w) {
+    const gptr_t<f32x4> rp =
+        as_global(reinterpret_cast<const f32x4*>(g.data + (size_t)(uint32_t)A.row(k, w) * NSLAM_C_DIM + 4 * h));
+    v[0] = rp[0];
+    v[1] = rp[2];
+    v[2] = rp[4];
+    v[3] = rp[6];
+  };
+  f32x4 va[4];
+  float wa;
+  load(0, va, wa);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    f32x4 na[4];
+    float nwa = 0.f;
+    if (k < 7) load(k + 1, na, nwa);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc[j] += va[0][j] * wa;
+      acc[4 + j] += va[1][j] * wa;
+      acc[8 + j] += va[2][j] * wa;
+      acc[12 + j] += va[3][j] * wa;
+    }
+    if (k < 7) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) va[i] = na[i];
+      wa = nwa;
+    }
+  }
+  return acc;
+}
+
 // ------------------------------------------------------------------------------------------
 // Fourier embedding (decoder.py:26-30): block b, reg r of lane (h,p) is dim k = 32b + F(r,h)
 // ------------------------------------------------------------------------------------------
@@ -444,17 +483,18 @@ __device__ __forceinline__ f32x16 xyz_forward(const float* __restrict__ pk, cons
 // (NC = 2) GEMMs as a FragPipe: each weight fragment is loaded while the previous GEMM runs, so no GEMM
 // waits for its fragment's L2 round trip.  The same products in the same order as xyz_forward.
 // (phases build: marks MK .. MK + 3 after the embedding GEMMs, layers 1-2, layer 3 and layer 4)
-template <int NC, bool TAPE, int MK = 5>
-__device__ __forceinline__ f32x16 xyz_forward_pf(const float* __restrict__ pk, const f32x16 (&cin)[NC],
-                                                 const float x[3], int lane, uint32_t m[5],
-                                                 float* __restrict__ tape, const float* vs) {
+// (E(b): embedding block b — sin(x B_b) formed here, or handed over by a producer wave, k_query_fwd_pc)
+template <int NC, bool TAPE, int MK = 5, class EmbFn>
+__device__ __forceinline__ f32x16 xyz_forward_pf_e(const float* __restrict__ pk, const f32x16 (&cin)[NC],
+                                                   const EmbFn& E, int lane, uint32_t m[5],
+                                                   float* __restrict__ tape, const float* vs) {
   const XyzPack L{NC};
   FragPipe fp(pk, L.L0(), lane);
   f32x16 a = vec_tile(vs + (L.Bias(0) - L.V()), lane);
   f32x16 a3 = vec_tile(vs + (L.Bias(3) - L.V()), lane);
 #pragma unroll
   for (int b = 0; b < 3; ++b) {
-    const f32x16 e = emb_tile<false, false>(vs + (L.FB() - L.V()), x, b, lane);
+    const f32x16 e = E(b);
     fp.gemm(a, e, L.L3() + b);
     fp.gemm(a3, e, b < 2 ? L.L0() + b + 1 : L.FC(0, 0));
   }
@@ -492,6 +532,14 @@ __device__ __forceinline__ f32x16 xyz_forward_pf(const float* __restrict__ pk, c
   if (TAPE) tape_store(tape, 4, h, lane);
   PHASE(0, MK + 3);
   return h;
+}
+template <int NC, bool TAPE, int MK = 5>
+__device__ __forceinline__ f32x16 xyz_forward_pf(const float* __restrict__ pk, const f32x16 (&cin)[NC],
+                                                 const float x[3], int lane, uint32_t m[5],
+                                                 float* __restrict__ tape, const float* vs) {
+  const XyzPack L{NC};
+  return xyz_forward_pf_e<NC, TAPE, MK>(
+      pk, cin, [&](int b) { return emb_tile<false, false>(vs + (L.FB() - L.V()), x, b, lane); }, lane, m, tape, vs);
 }
 
 // output_linear row j: sum_f Wo[j][f] h4[f] + bo[j]  (complete in both halves)
@@ -1487,6 +1535,218 @@ __global__ __launch_bounds__(64, 3) void k_query_fwd_units(QueryKArgs a, float* 
     fwd_part_middle(a, q, tile, idx, lane, occ_mid, vsec);
   } else if (STAGE == NSLAM_STAGE_COLOR) {
     fwd_part_color<TAPE>(a, q, tile, idx, lane, vsec);
+  }
+  TL(0, 1, 0);
+}
+
+// ------------------------------------------------------------------------------------------
+// Producer / consumer forward (round 5): the decoder-tile units of k_query_fwd_units, but each unit's
+// work split between two kinds of wave of one persistent workgroup per CU, so every SIMD holds both at
+// once and its MFMA pipe (consumers) and VALU / memory pipes (producers) run side by side:
+//   producer waves (4, one per SIMD): the unit's points, trilinear gathers (gather_pair / gather_tile)
+//     and Fourier embedding sin(x B_b) — exactly the units kernel's arithmetic — into an LDS slot, in
+//     the register layout (16 floats per lane per tile: one conflict-free ds_write_b128 per quad);
+//   consumer waves (8, two per SIMD): read a full slot into registers (3 embedding tiles + NC feature
+//     tiles), hand the slot back at once, then run the decoder's GEMM chain (xyz_forward_pf_e: the same
+//     products in the same order), masks, activation tape and outputs.
+// Slots form a ring of kPcSlots: position k (the CU's k-th unit) lives in slot k % kPcSlots; its
+// producer waits until position k - kPcSlots was read (pc_free), fills the slot and publishes k
+// (pc_full); its consumer waits for k, reads, releases.  Producers and consumers take positions from
+// two LDS counters in order, so the CU's waves balance among themselves; CU g owns the global units
+// g, g + G, g + 2G, ... (fine units first: the heaviest).  Every wave leaves when the counter passes
+// the CU's unit count, and every position below it is produced and consumed exactly once, so the
+// grid drains.  Flags are LDS words written after an explicit lgkmcnt(0) (the slot's data is in LDS
+// before the flag is) and polled with s_sleep.
+constexpr int kPcCons = 8, kPcProd = 4, kPcWaves = kPcCons + kPcProd;
+constexpr int kPcSlots = 7;
+constexpr int kPcTileF = 1024;                   // one register tile: 16 floats x 64 lanes
+constexpr int kPcSlotF = 5 * kPcTileF + 4;       // emb 0-2, features 3-4, header {unit, inside lo, hi}
+static_assert((kPcSlotF * 4) % 16 == 0, "slots stay 16-B aligned");
+
+__device__ __forceinline__ void pc_put(float* __restrict__ t, const f32x16& v, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    *reinterpret_cast<f32x4*>(t + i * 256 + lane * 4) = f32x4{v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
+}
+__device__ __forceinline__ f32x16 pc_get(const float* __restrict__ t, int lane) {
+  f32x16 v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x4 q = *reinterpret_cast<const f32x4*>(t + i * 256 + lane * 4);
+    v[4 * i] = q[0];
+    v[4 * i + 1] = q[1];
+    v[4 * i + 2] = q[2];
+    v[4 * i + 3] = q[3];
+  }
+  return v;
+}
+// LDS flag words (workgroup-visible): a store after every earlier LDS access of this wave has completed;
+// a poll whose value orders every later LDS access of this wave after it
+__device__ __forceinline__ void pc_flag_store(int* p, int v) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// (bounded: a wait that never ends — a broken invariant — gives up after ~10^8 cycles, so the launch
+// still drains and the wrong results show in the parity tests instead of a hung device)
+__device__ __forceinline__ void pc_flag_wait(const int* p, int v) {
+  for (int it = 0; it < (1 << 21); ++it) {
+    const int x = __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    if (x == v) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ int pc_take(int* ctr, int lane) {
+  int k = 0;
+  if (lane == 0) k = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return __builtin_amdgcn_readfirstlane(k);
+}
+
+// The producer's share of unit (part, tile) into slot sl: features (part 1: fine and middle), the
+// embedding of the part's decoder and the inside ballot — the units kernel's arithmetic
+template <int STAGE>
+__device__ __forceinline__ void pc_produce(const QueryKArgs& a, int part, int64_t tile, int64_t unit, int lane,
+                                           const float* vs, float* __restrict__ sl, int* full, int* freed, int k,
+                                           int s) {
+  const int64_t idx = tile * 32 + (lane & 31);
+  const Pt q = load_point(a, idx);
+  // the grids by opaque indices: their constants (extents, scales; float64) are formed per unit —
+  // hoisted out of the producer loop they would pin (and spill) registers for all of it
+  int gi = part == 1 ? NSLAM_DEC_FINE : part == 0 ? NSLAM_DEC_MIDDLE : NSLAM_DEC_COLOR, gm = NSLAM_DEC_MIDDLE;
+  asm volatile("" : "+s"(gi), "+s"(gm));
+  // the slot first (position k - kPcSlots has been read out of it); then every tile is stored as soon as
+  // it is formed — the features, then the embedding blocks one at a time — so at most one tile and the
+  // loads of one gather are in registers
+  pc_flag_wait(freed + s, k - kPcSlots);
+  pc_put(sl + 3 * kPcTileF, gather_one(a.c.grid[gi], q, lane), lane);
+  if (part == 1) {
+    __builtin_amdgcn_sched_barrier(0);
+    pc_put(sl + 4 * kPcTileF, gather_one(a.c.grid[gm], q, lane), lane);
+  }
+  const uint64_t in = __ballot(q.inside);
+  const float* B = vs + (XyzPack{1}.FB() - XyzPack{1}.V());  // (the same offset for NC = 2)
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    __builtin_amdgcn_sched_barrier(0);
+    pc_put(sl + b * kPcTileF, emb_tile<false, false>(B, q.x, b, lane), lane);
+  }
+  if (lane == 0) {
+    int* hd = reinterpret_cast<int*>(sl + 5 * kPcTileF);
+    hd[0] = (int)unit;
+    hd[1] = (int)(uint32_t)in;
+    hd[2] = (int)(uint32_t)(in >> 32);
+  }
+  pc_flag_store(full + s, k);
+}
+
+template <int STAGE, bool TAPE>
+__global__ __launch_bounds__(64 * kPcWaves, 1) void k_query_fwd_pc(QueryKArgs a, float* __restrict__ occ_mid) {
+  constexpr int NP = STAGE == NSLAM_STAGE_COLOR ? 3 : 2;
+  __shared__ __attribute__((aligned(16))) float vsec[3][kVecFloats];
+  __shared__ __attribute__((aligned(16))) float slots[kPcSlots * kPcSlotF];
+  __shared__ int full[kPcSlots], freed[kPcSlots], ctr[2];
+  {
+    const float* s0 = a.c.packed[NSLAM_DEC_MIDDLE] + XyzPack{1}.V();
+    const float* s1 = a.c.packed[NSLAM_DEC_FINE] + XyzPack{2}.V();
+    const float* s2 = NP == 3 ? a.c.packed[NSLAM_DEC_COLOR] + XyzPack{1}.V() : nullptr;
+    for (int i = threadIdx.x; i < 740; i += 64 * kPcWaves) {
+      vsec[0][i] = s0[i];
+      vsec[1][i] = s1[i];
+      if (NP == 3) vsec[2][i] = s2[i];
+    }
+    if (threadIdx.x < kPcSlots) {
+      full[threadIdx.x] = -1;
+      freed[threadIdx.x] = (int)threadIdx.x - kPcSlots;
+    }
+    if (threadIdx.x < 2) ctr[threadIdx.x] = 0;
+    __syncthreads();
+  }
+  const int64_t ntiles = (a.n + 31) / 32;
+  const int64_t U = ntiles * NP, G = gridDim.x, g = blockIdx.x;
+  const int K = (int)((U - g + G - 1) / G);  // this CU's units (the launch has G <= U)
+  const int w = wave_id(), lane0 = threadIdx.x & 63;
+  TL(0, 0, w >= kPcCons);
+  if (w >= kPcCons) {  // producer
+    for (;;) {
+      const int k = pc_take(&ctr[0], lane0);
+      if (k >= K) break;  // wave-uniform
+      // lane-derived addresses re-formed per unit (no hoisting)
+      int lane = lane0;
+      asm volatile("" : "+v"(lane));
+      const int64_t u = g + (int64_t)k * G;
+      const int part = u < ntiles ? 1 : u < 2 * ntiles ? 0 : 2;
+      const int64_t tile = u - (part == 1 ? 0 : part == 0 ? ntiles : 2 * ntiles);
+      const int s = k % kPcSlots;
+      pc_produce<STAGE>(a, part, tile, u, lane, vsec[part == 0 ? 0 : part == 1 ? 1 : 2], slots + s * kPcSlotF,
+                        full, freed, k, s);
+    }
+  } else {  // consumer
+    for (;;) {
+      const int k = pc_take(&ctr[1], lane0);
+      if (k >= K) break;  // wave-uniform
+      int lane = lane0;
+      asm volatile("" : "+v"(lane));
+      const int s = k % kPcSlots;
+      const float* sl = slots + s * kPcSlotF;
+      pc_flag_wait(full + s, k);
+      const int* hd = reinterpret_cast<const int*>(sl + 5 * kPcTileF);
+      const int64_t u = __builtin_amdgcn_readfirstlane(hd[0]);
+      const uint32_t inw = (uint32_t)hd[1 + (lane >> 5)];
+      const bool inside = (inw >> (lane & 31)) & 1u;
+      const int part = u < ntiles ? 1 : u < 2 * ntiles ? 0 : 2;
+      const int64_t tile = u - (part == 1 ? 0 : part == 0 ? ntiles : 2 * ntiles);
+      const int64_t idx = tile * 32 + (lane & 31);
+      const bool valid = idx < a.n;
+      const int h = lane >> 5;
+      // the embedding tiles are read where the chain uses them (one at a time in registers); the slot is
+      // handed back once the last one is in registers (the features are read into registers first)
+      const auto E = [&](int b) {
+        const f32x16 v = pc_get(sl + b * kPcTileF, lane);
+        if (b == 2) pc_flag_store(freed + s, k);
+        return v;
+      };
+      uint32_t m[5];
+      if (part == 1) {
+        const f32x16 cf[2] = {pc_get(sl + 3 * kPcTileF, lane), pc_get(sl + 4 * kPcTileF, lane)};
+        const XyzPack L{2};
+        const float* vs = vsec[1];
+        const f32x16 h4 = xyz_forward_pf_e<2, false>(a.c.packed[NSLAM_DEC_FINE], cf, E, lane, m, nullptr, vs);
+        save_masks(a, NSLAM_DEC_FINE, tile, m, lane);
+        float o = out_row(vs + (L.Wo() - L.V()), vs + (L.Bo() - L.V()), 0, h4, lane);
+        if (!inside) o = 0.f;
+        if (h == 0 && valid) {
+          if (STAGE == NSLAM_STAGE_COLOR) {
+            a.raw[idx * 4 + 3] = o;
+          } else {
+            f32x4 v = {0.f, 0.f, 0.f, o};
+            *reinterpret_cast<f32x4*>(a.raw + idx * 4) = v;
+          }
+        }
+      } else if (part == 0) {
+        const f32x16 cm[1] = {pc_get(sl + 3 * kPcTileF, lane)};
+        const XyzPack L{1};
+        const float* vs = vsec[0];
+        const f32x16 h4 = xyz_forward_pf_e<1, false>(a.c.packed[NSLAM_DEC_MIDDLE], cm, E, lane, m, nullptr, vs);
+        save_masks(a, NSLAM_DEC_MIDDLE, tile, m, lane);
+        float o = out_row(vs + (L.Wo() - L.V()), vs + (L.Bo() - L.V()), 0, h4, lane);
+        if (!inside) o = 100.f;
+        if (h == 0 && valid) occ_mid[idx] = o;
+      } else if (STAGE == NSLAM_STAGE_COLOR) {
+        const f32x16 cc[1] = {pc_get(sl + 3 * kPcTileF, lane)};
+        const XyzPack L{1};
+        const float* vs = vsec[2];
+        float* tp = TAPE ? a.c.act_tape + tile * kTapeFloats : nullptr;
+        const f32x16 h4 = xyz_forward_pf_e<1, TAPE, 12>(a.c.packed[NSLAM_DEC_COLOR], cc, E, lane, m, tp, vs);
+        save_masks(a, NSLAM_DEC_COLOR, tile, m, lane);
+        float o[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) o[j] = out_row(vs + (L.Wo() - L.V()), vs + (L.Bo() - L.V()), j, h4, lane);
+        if (h == 0 && valid) {
+#pragma unroll
+          for (int j = 0; j < 3; ++j) a.raw[idx * 4 + j] = o[j];
+        }
+      }
+    }
   }
   TL(0, 1, 0);
 }
