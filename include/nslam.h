@@ -42,6 +42,10 @@ enum {
 
 enum { NSLAM_STAGE_COARSE = 0, NSLAM_STAGE_MIDDLE = 1, NSLAM_STAGE_FINE = 2, NSLAM_STAGE_COLOR = 3 };
 enum { NSLAM_DEC_COARSE = 0, NSLAM_DEC_MIDDLE = 1, NSLAM_DEC_FINE = 2, NSLAM_DEC_COLOR = 3 };
+/* nslam_query_cfg.fwd_variant (ABI v18): UNITS = one one-wave workgroup per decoder and 32-point tile;
+ * PC = one persistent workgroup per CU whose producer waves gather and embed while its consumer waves
+ * run the decoder GEMM chains; PARTS = 4-wave workgroups of one decoder part. */
+enum { NSLAM_FWD_DEFAULT = 0, NSLAM_FWD_UNITS = 1, NSLAM_FWD_PC = 2, NSLAM_FWD_PARTS = 3 };
 
 /* One feature grid (src/NICE_SLAM.py:192-250) with the bound it is normalised against
  * (decoder.bound, src/NICE_SLAM.py:152-157; the coarse decoder uses bound*2). */
@@ -98,7 +102,10 @@ typedef struct nslam_query_cfg {
    * middle occupancy in ws (float [M]) instead of adding them in a separate pass: the consumer
    * adds it on read (nslam_loss_cfg.occ_add = ws), saving a launch per query. */
   int32_t defer_occ;
-  int32_t pad2_;
+  /* ABI v18: how nslam_query_fwd_ws spreads the fine / colour stage over the chip (NSLAM_FWD_*; 0 = the
+   * library's default).  Every variant computes the same values in the same order: bit-identical
+   * outputs, masks and activation tape. */
+  int32_t fwd_variant;
   /* ABI v9: activation tape of the colour decoder (NULL = none).  nslam_query_fwd[_ws] writes the
    * post-ReLU hidden tiles h0..h4 of every 32-point tile ([tile][layer][32 points][32 features]
    * float, nslam_query_tape_size(M) bytes; layout private to the library); with it and saved_masks the colour decoder's weight-gradient

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NSLAM_LIB") or os.path.join(_HERE, "libnslam.so")  # NSLAM_LIB: instrumented builds
 
 NSLAM_OK = 0
-ABI_VERSION = 17
+ABI_VERSION = 18
 STAGES = {"coarse": 0, "middle": 1, "fine": 2, "color": 3}
 DEC_COARSE, DEC_MIDDLE, DEC_FINE, DEC_COLOR = 0, 1, 2, 3
 
@@ -62,7 +62,7 @@ class NslamQueryCfg(ctypes.Structure):
         ("n_samples", ctypes.c_int64),
         ("saved_masks", ctypes.c_void_p),
         ("defer_occ", ctypes.c_int32),  # ABI v7
-        ("pad2_", ctypes.c_int32),
+        ("fwd_variant", ctypes.c_int32),  # ABI v18 (NSLAM_FWD_*)
         ("act_tape", ctypes.c_void_p),  # ABI v9: colour-decoder activation tape (NULL = none)
         ("g_h4", ctypes.c_void_p),  # ABI v17: colour decoder's d/dh4 [M][32] (NULL = none)
     ]

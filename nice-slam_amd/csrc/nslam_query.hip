@@ -64,13 +64,18 @@ extern "C" int nslam_query_fwd_ws(const nslam_query_cfg* cfg, const double* pts,
   const int64_t tiles = (n_pts + 31) / 32;
   const int color_parts = forced_parts == 2 || forced_parts == 3 ? forced_parts : (3 * tiles <= wave_slots ? 3 : 2);
   const dim3 b256(256);
-  // forward variant: NSLAM_FWD_MODE=pc (producer / consumer waves, one persistent workgroup per CU),
-  // units (one-wave workgroups per decoder-tile), dyn (a counter), parts
-  static const int mode = [] {
+  // forward variant: cfg->fwd_variant, else NSLAM_FWD_MODE=pc (producer / consumer waves, one persistent
+  // workgroup per CU), units (one-wave workgroups per decoder-tile), dyn (a counter; experiment), parts
+  static const int env_mode = [] {
     const char* e = getenv("NSLAM_FWD_MODE");
     if (!e) return 1;
     return !strcmp(e, "pc") ? 3 : !strcmp(e, "dyn") ? 2 : !strcmp(e, "parts") ? 0 : 1;
   }();
+  if (cfg->fwd_variant < 0 || cfg->fwd_variant > NSLAM_FWD_PARTS) return NSLAM_EINVAL;
+  const int mode = cfg->fwd_variant == NSLAM_FWD_UNITS ? 1
+                   : cfg->fwd_variant == NSLAM_FWD_PC  ? 3
+                   : cfg->fwd_variant == NSLAM_FWD_PARTS ? 0
+                                                         : env_mode;
   if (mode == 3) {
     const int64_t units = tiles * (cfg->stage == NSLAM_STAGE_COLOR ? 3 : 2);
     const dim3 g((unsigned)(units < n_cus ? units : n_cus)), b(64 * kPcWaves);

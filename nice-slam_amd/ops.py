@@ -488,6 +488,10 @@ class _GridSample(torch.autograd.Function):
 
 
 SPLIT_FWD = True  # decoder-parallel forward (nslam_query_fwd_ws); False: one wave runs every decoder
+# how nslam_query_fwd_ws spreads the decoders over the chip (nslam_query_cfg.fwd_variant, ABI v18):
+# 0 = the library's default, FWD_UNITS / FWD_PC / FWD_PARTS force one (the same values bit for bit)
+FWD_DEFAULT, FWD_UNITS, FWD_PC, FWD_PARTS = 0, 1, 2, 3
+FWD_VARIANT = FWD_DEFAULT
 
 
 def query_fwd_launch(cfg, pts, n, raw, split=None, defer_occ=False):
@@ -502,6 +506,7 @@ def query_fwd_launch(cfg, pts, n, raw, split=None, defer_occ=False):
         if wsb:
             ws = torch.empty(wsb, dtype=torch.uint8, device=raw.device)
             cfg.defer_occ = int(bool(defer_occ))
+            cfg.fwd_variant = FWD_VARIANT
             rc = lib().nslam_query_fwd_ws(ctypes.byref(cfg), ptr(pts), n, ptr(raw), ptr(ws), wsb,
                                           stream_ptr(raw.device))
             cfg.defer_occ = 0

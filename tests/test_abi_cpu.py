@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_strerror(pkg):
     L = pkg._lib.lib()
-    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 17
+    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 18
     assert L.nslam_strerror(0) == b"ok"
     assert b"invalid" in L.nslam_strerror(-1)
 

@@ -445,6 +445,43 @@ def test_sparse_exchange_single_rank_is_identity(tiny):
     assert ex.payload_bytes(keys, dn) == (sum(r.numel() for r in rows.values()) * 32 + d0.numel()) * 4
 
 
+@pytest.mark.parametrize("stage", ["fine", "color"])
+@pytest.mark.parametrize("n_per", [13, 1400])
+def test_forward_variants_bitexact(tiny, stage, n_per):
+    """Every nslam_query_fwd_ws variant (ABI v18 fwd_variant: one-wave units, the persistent producer /
+    consumer workgroups, 4-wave parts) forms the same values in the same order: raw, the saved ReLU
+    masks and the colour decoder's activation tape are bit-identical.  3 x 1400 rays x 48 samples =
+    6300 tiles, ~74 decoder units per CU: the producer / consumer ring wraps ~10 times; 3 x 13 rays: a
+    partial last tile and fewer units than CUs."""
+    sc, frames = _frames(tiny)
+    nice, c = _nice(sc)
+    eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    pix = torch.randint(96 * 128, (3 * n_per,), device=DEV, generator=g)
+    ro, rd, gd, gc, keep = P.ops.gather_rays(frames, pix, n_per, 96, 128, (0, 96, 0, 128), sc.fx, sc.fy, sc.cx,
+                                             sc.cy)
+    z = P.ops.sample_z(ro, rd, gd, sc.bound, 32, 16)
+    outs = {}
+    for v in (P.ops.FWD_UNITS, P.ops.FWD_PC, P.ops.FWD_PARTS):
+        P.ops.FWD_VARIANT = v
+        try:
+            raw = eng.query_fwd(stage, ro, rd, z, tape=True)
+            torch.cuda.synchronize()
+            outs[v] = (raw.clone(), eng._saved.clone(), None if eng._tape is None else eng._tape.clone())
+        finally:
+            P.ops.FWD_VARIANT = P.ops.FWD_DEFAULT
+    ref = outs[P.ops.FWD_UNITS]
+    assert bool(torch.isfinite(ref[0]).all())
+    ntiles = (z.numel() + 31) // 32
+    decs = [1, 2, 3] if stage == "color" else [1, 2]  # the masks the stage writes: [decoder][tile][5][64]
+    for v, o in outs.items():
+        assert torch.equal(o[0], ref[0]), v
+        m, mr = (x.view(torch.int16).view(4, ntiles, 5, 64)[decs] for x in (o[1], ref[1]))
+        assert torch.equal(m, mr), v
+        if stage == "color":
+            assert torch.equal(o[2], ref[2]), v
+
+
 @pytest.mark.parametrize("stage", ["middle", "fine", "color"])
 def test_decoder_parallel_forward_bitexact(tiny, stage):
     """nslam_query_fwd_ws (one decoder per workgroup + occupancy combine) == nslam_query_fwd

@@ -50,6 +50,15 @@ def analyse(name, t, parts=None):
     # per SIMD: waves received, max resident at once, busy span (first start .. last end)
     us, inv = np.unique(simd, return_inverse=True)
     cnt = np.bincount(inv)
+    if parts is not None:  # which tags (parts / roles) share a SIMD: "tag0 x tag1 x ..." -> SIMDs
+        pp = parts[ok]
+        tags = np.unique(pp)
+        combo = {}
+        for i in range(len(us)):
+            key = " ".join(f"{int((pp[inv == i] == v).sum())}" for v in tags)
+            combo[key] = combo.get(key, 0) + 1
+        print(f"   waves of tags {list(map(int, tags))} per SIMD: " +
+              ", ".join(f"[{k}]:{v}" for k, v in sorted(combo.items(), key=lambda e: -e[1])[:6]))
     print("   waves per SIMD: " + ", ".join(f"{k}:{v}" for k, v in zip(*np.unique(cnt, return_counts=True))))
     maxres, last_end = [], []
     for i in range(len(us)):
