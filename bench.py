@@ -200,14 +200,16 @@ class StepGraphs:
                 fn()
         torch.cuda.current_stream().wait_stream(side)
         self.single = []
+        # thread_local capture: RCCL's watchdog thread polls its work events while this thread captures
+        # (global mode makes that poll fail the capture: hipErrorStreamCaptureUnsupported)
         for _ in range(2):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 fn()
             self.single.append(g)
         self.block = max(2, block - block % 2)
         self.blockg = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.blockg):
+        with torch.cuda.graph(self.blockg, capture_error_mode="thread_local"):
             for _ in range(self.block):
                 fn()
         self.par = 0  # device-side parity relative to the capture start

@@ -193,6 +193,43 @@ __device__ __forceinline__ f32x16 gather_one(const nslam_grid& g, const Pt& q, i
   return acc;
 }
 
+// gather_tile's trilinear feature with NB corners' row loads issued together (8 / NB round trips of
+// memory latency instead of gather_one's 8 pipelined ones), summed in gather_tile's corner order (the
+// same values).  For a wave with nothing else in registers (the producer of k_query_fwd_pc).
+template <int NB>
+__device__ __forceinline__ f32x16 gather_nb(const nslam_grid& g, const Pt& q, int lane) {
+  const int h = lane >> 5;
+  const LazyCell A(g, q);
+  f32x16 acc = zero16();
+#pragma unroll
+  for (int k0 = 0; k0 < 8; k0 += NB) {
+    f32x4 v[NB][4];
+    float w[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const gptr_t<f32x4> rp = as_global(
+          reinterpret_cast<const f32x4*>(g.data + (size_t)(uint32_t)A.row(k0 + k, w[k]) * NSLAM_C_DIM + 4 * h));
+      v[k][0] = rp[0];
+      v[k][1] = rp[2];
+      v[k][2] = rp[4];
+      v[k][3] = rp[6];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[j] += v[k][0][j] * w[k];
+        acc[4 + j] += v[k][1][j] * w[k];
+        acc[8 + j] += v[k][2][j] * w[k];
+        acc[12 + j] += v[k][3][j] * w[k];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return acc;
+}
+
 // ------------------------------------------------------------------------------------------
 // Fourier embedding (decoder.py:26-30): block b, reg r of lane (h,p) is dim k = 32b + F(r,h)
 // ------------------------------------------------------------------------------------------
@@ -276,7 +313,18 @@ __device__ __forceinline__ void tl_mark(int slot, int end, long long tag) {
   }
 }
 #define TL(slot, end, tag) tl_mark(slot, end, tag)
+// add v << 8 into this wave's tag (after its start mark): e.g. the 10-ns ticks a wave spent waiting
+__device__ __forceinline__ void tl_add(int slot, unsigned long long v) {
+  const int64_t w_ = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0 && w_ < kTlWaves) g_tl[((size_t)slot * kTlWaves + w_) * 4 + 3] += v << 8;
+}
+#define TL_ADD(slot, v) tl_add(slot, v)
+#define TL_NOW() __builtin_amdgcn_s_memrealtime()
 #else
+#define TL_ADD(slot, v) \
+  do {                  \
+  } while (0)
+#define TL_NOW() 0ull
 #define TL(slot, end, tag) \
   do {                     \
   } while (0)
@@ -1558,6 +1606,9 @@ __global__ __launch_bounds__(64, 3) void k_query_fwd_units(QueryKArgs a, float* 
 // grid drains.  Flags are LDS words written after an explicit lgkmcnt(0) (the slot's data is in LDS
 // before the flag is) and polled with s_sleep.
 constexpr int kPcCons = 8, kPcProd = 4, kPcWaves = kPcCons + kPcProd;
+#ifndef NSLAM_PC_NB
+#define NSLAM_PC_NB 8  // corners whose row loads the producer issues together
+#endif
 constexpr int kPcSlots = 7;
 constexpr int kPcTileF = 1024;                   // one register tile: 16 floats x 64 lanes
 constexpr int kPcSlotF = 5 * kPcTileF + 4;       // emb 0-2, features 3-4, header {unit, inside lo, hi}
@@ -1589,11 +1640,13 @@ __device__ __forceinline__ void pc_flag_store(int* p, int v) {
 // (bounded: a wait that never ends — a broken invariant — gives up after ~10^8 cycles, so the launch
 // still drains and the wrong results show in the parity tests instead of a hung device)
 __device__ __forceinline__ void pc_flag_wait(const int* p, int v) {
+  const unsigned long long t0 = TL_NOW();
   for (int it = 0; it < (1 << 21); ++it) {
     const int x = __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
     if (x == v) break;
     __builtin_amdgcn_s_sleep(1);
   }
+  TL_ADD(0, TL_NOW() - t0);  // (timeline build: the wave's waiting time)
   asm volatile("" ::: "memory");
 }
 __device__ __forceinline__ int pc_take(int* ctr, int lane) {
@@ -1618,10 +1671,10 @@ __device__ __forceinline__ void pc_produce(const QueryKArgs& a, int part, int64_
   // it is formed — the features, then the embedding blocks one at a time — so at most one tile and the
   // loads of one gather are in registers
   pc_flag_wait(freed + s, k - kPcSlots);
-  pc_put(sl + 3 * kPcTileF, gather_one(a.c.grid[gi], q, lane), lane);
+  pc_put(sl + 3 * kPcTileF, gather_nb<NSLAM_PC_NB>(a.c.grid[gi], q, lane), lane);
   if (part == 1) {
     __builtin_amdgcn_sched_barrier(0);
-    pc_put(sl + 4 * kPcTileF, gather_one(a.c.grid[gm], q, lane), lane);
+    pc_put(sl + 4 * kPcTileF, gather_nb<NSLAM_PC_NB>(a.c.grid[gm], q, lane), lane);
   }
   const uint64_t in = __ballot(q.inside);
   const float* B = vs + (XyzPack{1}.FB() - XyzPack{1}.V());  // (the same offset for NC = 2)

@@ -89,7 +89,8 @@ def _run(world, rank, group=None, mode="allreduce", force=False, graph=False):
         losses.append(float(step().sum()))
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread_local: the RCCL watchdog thread's event polls must not invalidate the capture
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             rl = step()
         for _ in range(ITERS - 1):
             g.replay()

@@ -42,11 +42,15 @@ def analyse(name, t, parts=None):
     print("   end                         " + " ".join(f"p{p}={np.percentile((en - t0) * TICK_US, p):.1f}" for p in q))
     print("   lifetime                    " + " ".join(f"p{p}={np.percentile(life, p):.1f}" for p in q))
     if parts is not None:
+        waits = (parts[ok] >> 8) * TICK_US  # time the wave spent polling flags (k_query_fwd_pc), if recorded
+        parts = parts & 0xff
         pp = parts[ok]
         for v in np.unique(pp):
             lv = life[pp == v]
+            wv = waits[pp == v]
+            extra = f", waiting {wv.mean():.1f} us ({wv.sum() / lv.sum():.0%})" if wv.any() else ""
             print(f"     part {v}: {len(lv)} waves, lifetime p50 {np.median(lv):.1f} p90 {np.percentile(lv, 90):.1f}"
-                  f" mean {lv.mean():.1f} us")
+                  f" mean {lv.mean():.1f} us{extra}")
     # per SIMD: waves received, max resident at once, busy span (first start .. last end)
     us, inv = np.unique(simd, return_inverse=True)
     cnt = np.bincount(inv)
