@@ -230,17 +230,47 @@ __device__ __forceinline__ f32x16 vec_tile_g(const float* __restrict__ v, int la
   return t;
 }
 
+// ReLU and its mask on the float's bits (both equal `a > 0 ? a : +0` and `a > 0` for every non-NaN a,
+// -0 included): relu is one v_max_i32 per register, the mask bit one v_med3_i32 (clamp to [0, 1]) and
+// one v_lshl_or per register.  A float compare would produce a 64-bit lane mask per register in SGPRs
+// (16 per layer), which the forward's chains spilled into VGPR lanes.
 __device__ __forceinline__ f32x16 relu16(const f32x16& a) {
   f32x16 o;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) o[r] = a[r] > 0.f ? a[r] : 0.f;
+  for (int r = 0; r < 16; ++r) {
+    const int v = __builtin_bit_cast(int, (float)a[r]);
+    o[r] = __builtin_bit_cast(float, v > 0 ? v : 0);
+  }
   return o;
 }
 
+// bit R of m = (a > 0): clamp the bits to [0, 1] and shift-or it in, in one asm statement so the bit is
+// folded into m at once (as separate operations the compiler kept 16 bits live per layer)
+template <int R>
+__device__ __forceinline__ void mask_bit(uint32_t& m, float a) {
+  int t;
+  asm("v_med3_i32 %1, %2, 0, 1\n\tv_lshl_or_b32 %0, %1, %3, %0"
+      : "+v"(m), "=&v"(t)
+      : "v"(__builtin_bit_cast(int, a)), "n"(R));
+}
 __device__ __forceinline__ uint32_t mask16(const f32x16& a) {
   uint32_t m = 0;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) m |= (a[r] > 0.f ? 1u : 0u) << r;
+  mask_bit<0>(m, a[0]);
+  mask_bit<1>(m, a[1]);
+  mask_bit<2>(m, a[2]);
+  mask_bit<3>(m, a[3]);
+  mask_bit<4>(m, a[4]);
+  mask_bit<5>(m, a[5]);
+  mask_bit<6>(m, a[6]);
+  mask_bit<7>(m, a[7]);
+  mask_bit<8>(m, a[8]);
+  mask_bit<9>(m, a[9]);
+  mask_bit<10>(m, a[10]);
+  mask_bit<11>(m, a[11]);
+  mask_bit<12>(m, a[12]);
+  mask_bit<13>(m, a[13]);
+  mask_bit<14>(m, a[14]);
+  mask_bit<15>(m, a[15]);
   return m;
 }
 

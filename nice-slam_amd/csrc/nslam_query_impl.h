@@ -1609,6 +1609,9 @@ constexpr int kPcCons = 8, kPcProd = 4, kPcWaves = kPcCons + kPcProd;
 #ifndef NSLAM_PC_NB
 #define NSLAM_PC_NB 8  // corners whose row loads the producer issues together
 #endif
+#ifndef NSLAM_PC_DIAG
+#define NSLAM_PC_DIAG 0  // timing experiments only: 1 = consumers skip the chains, 2 = producers skip their work
+#endif
 constexpr int kPcSlots = 7;
 constexpr int kPcTileF = 1024;                   // one register tile: 16 floats x 64 lanes
 constexpr int kPcSlotF = 5 * kPcTileF + 4;       // emb 0-2, features 3-4, header {unit, inside lo, hi}
@@ -1671,6 +1674,15 @@ __device__ __forceinline__ void pc_produce(const QueryKArgs& a, int part, int64_
   // it is formed — the features, then the embedding blocks one at a time — so at most one tile and the
   // loads of one gather are in registers
   pc_flag_wait(freed + s, k - kPcSlots);
+#if NSLAM_PC_DIAG == 2  // timing experiment: producers publish without gathering or embedding
+  if (lane == 0) {
+    int* hd = reinterpret_cast<int*>(sl + 5 * kPcTileF);
+    hd[0] = (int)unit;
+    hd[1] = hd[2] = -1;
+  }
+  pc_flag_store(full + s, k);
+  return;
+#endif
   pc_put(sl + 3 * kPcTileF, gather_nb<NSLAM_PC_NB>(a.c.grid[gi], q, lane), lane);
   if (part == 1) {
     __builtin_amdgcn_sched_barrier(0);
@@ -1759,6 +1771,13 @@ __global__ __launch_bounds__(64 * kPcWaves, 1) void k_query_fwd_pc(QueryKArgs a,
         return v;
       };
       uint32_t m[5];
+#if NSLAM_PC_DIAG == 1  // timing experiment: consumers take and release slots without computing
+      if (u >= 0) {
+        f32x16 t = E(0) + E(1) + E(2) + pc_get(sl + 3 * kPcTileF, lane);
+        if (t[0] == 12345.f && h == 7) a.raw[0] = t[1];  // (never true: keeps the reads)
+        continue;
+      }
+#endif
       if (part == 1) {
         const f32x16 cf[2] = {pc_get(sl + 3 * kPcTileF, lane), pc_get(sl + 4 * kPcTileF, lane)};
         const XyzPack L{2};
