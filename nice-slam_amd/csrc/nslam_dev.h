@@ -274,10 +274,13 @@ __device__ __forceinline__ uint32_t mask16(const f32x16& a) {
   return m;
 }
 
+// g where bit r of m is set, else +0: a sign-extended bit field (v_bfe_i32: 0 or -1) ANDed into the bits
+// (no per-register compare, i.e. no SGPR lane mask per register)
 __device__ __forceinline__ f32x16 apply_mask(const f32x16& g, uint32_t m) {
   f32x16 o;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) o[r] = ((m >> r) & 1u) ? g[r] : 0.f;
+  for (int r = 0; r < 16; ++r)
+    o[r] = __builtin_bit_cast(float, __builtin_bit_cast(int, (float)g[r]) & __builtin_amdgcn_sbfe((int)m, r, 1));
   return o;
 }
 

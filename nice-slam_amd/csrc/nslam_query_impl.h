@@ -10,6 +10,8 @@
 //
 // Work decomposition: one wave = one tile of 32 points.  Each lane pair (l, l+32) owns one point;
 // the half h = l>>5 gathers/holds the 16 feature channels F(r,h) of that point (nslam_dev.h).
+#include <type_traits>
+
 #include "nslam_dev.h"
 
 // Everything lives in a named namespace: the per-decoder backward launchers are explicitly
@@ -314,15 +316,20 @@ __device__ __forceinline__ void tl_mark(int slot, int end, long long tag) {
 }
 #define TL(slot, end, tag) tl_mark(slot, end, tag)
 // add v << 8 into this wave's tag (after its start mark): e.g. the 10-ns ticks a wave spent waiting
-__device__ __forceinline__ void tl_add(int slot, unsigned long long v) {
+// (field f = 0: bits 8-31, f = 1: bits 32-55 — e.g. a producer's gather time)
+__device__ __forceinline__ void tl_add(int slot, unsigned long long v, int f = 0) {
   const int64_t w_ = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if ((threadIdx.x & 63) == 0 && w_ < kTlWaves) g_tl[((size_t)slot * kTlWaves + w_) * 4 + 3] += v << 8;
+  if ((threadIdx.x & 63) == 0 && w_ < kTlWaves) g_tl[((size_t)slot * kTlWaves + w_) * 4 + 3] += v << (8 + 24 * f);
 }
 #define TL_ADD(slot, v) tl_add(slot, v)
+#define TL_ADD1(slot, v) tl_add(slot, v, 1)
 #define TL_NOW() __builtin_amdgcn_s_memrealtime()
 #else
 #define TL_ADD(slot, v) \
   do {                  \
+  } while (0)
+#define TL_ADD1(slot, v) \
+  do {                   \
   } while (0)
 #define TL_NOW() 0ull
 #define TL(slot, end, tag) \
@@ -531,13 +538,48 @@ __device__ __forceinline__ f32x16 xyz_forward(const float* __restrict__ pk, cons
 // (NC = 2) GEMMs as a FragPipe: each weight fragment is loaded while the previous GEMM runs, so no GEMM
 // waits for its fragment's L2 round trip.  The same products in the same order as xyz_forward.
 // (phases build: marks MK .. MK + 3 after the embedding GEMMs, layers 1-2, layer 3 and layer 4)
-// (E(b): embedding block b — sin(x B_b) formed here, or handed over by a producer wave, k_query_fwd_pc)
-template <int NC, bool TAPE, int MK = 5, class EmbFn>
+// The weight-fragment blocks of xyz_forward_pf_e's GEMMs in issue order: L0_b / L3_b for b = 0..2, then
+// per layer i = 0..4 the NC fc_c.i blocks followed by the next layer's block (L1, L2, L3's h2 block, L4)
+template <int NC>
+__device__ __forceinline__ constexpr int frag_seq(int i) {
+  const XyzPack L{NC};
+  if (i < 6) return (i & 1) ? L.L3() + (i >> 1) : L.L0() + (i >> 1);
+  i -= 6;
+  const int layer = i / (NC + 1), j = i % (NC + 1);
+  if (j < NC) return L.FC(layer, j);
+  return layer == 0 ? L.L1() : layer == 1 ? L.L2() : layer == 2 ? L.L3() + 3 : L.L4();
+}
+// FragPipe with D fragments in flight: GEMM i runs while the fragments of GEMMs i+1 .. i+D load (the
+// block order is frag_seq's, so the call sites' `next` is not needed)
+template <int NC, int D>
+struct SeqPipe {
+  static constexpr int kN = 10 + 5 * NC;
+  const float* pk;
+  int lane, i;
+  Frag f[D];
+  __device__ __forceinline__ SeqPipe(const float* pk_, int, int lane_) : pk(pk_), lane(lane_), i(0) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) f[d] = load_frag(pk + frag_seq<NC>(d) * NSLAM_FRAG, lane);
+  }
+  __device__ __forceinline__ void gemm(f32x16& acc, const f32x16& x, int) {
+    const Frag cur = f[0];
+#pragma unroll
+    for (int d = 0; d + 1 < D; ++d) f[d] = f[d + 1];
+    if (i + D < kN) f[D - 1] = load_frag(pk + frag_seq<NC>(i + D) * NSLAM_FRAG, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    gemm_frag(acc, cur, x);
+    ++i;
+  }
+};
+
+// (E(b): embedding block b — sin(x B_b) formed here, or handed over by a producer wave, k_query_fwd_pc;
+//  FD: weight fragments in flight, 1 = FragPipe)
+template <int NC, bool TAPE, int MK = 5, int FD = 1, class EmbFn>
 __device__ __forceinline__ f32x16 xyz_forward_pf_e(const float* __restrict__ pk, const f32x16 (&cin)[NC],
                                                    const EmbFn& E, int lane, uint32_t m[5],
                                                    float* __restrict__ tape, const float* vs) {
   const XyzPack L{NC};
-  FragPipe fp(pk, L.L0(), lane);
+  typename std::conditional<FD == 1, FragPipe, SeqPipe<NC, FD>>::type fp(pk, L.L0(), lane);
   f32x16 a = vec_tile(vs + (L.Bias(0) - L.V()), lane);
   f32x16 a3 = vec_tile(vs + (L.Bias(3) - L.V()), lane);
 #pragma unroll
@@ -1605,12 +1647,19 @@ __global__ __launch_bounds__(64, 3) void k_query_fwd_units(QueryKArgs a, float* 
 // the CU's unit count, and every position below it is produced and consumed exactly once, so the
 // grid drains.  Flags are LDS words written after an explicit lgkmcnt(0) (the slot's data is in LDS
 // before the flag is) and polled with s_sleep.
-constexpr int kPcCons = 8, kPcProd = 4, kPcWaves = kPcCons + kPcProd;
+#ifndef NSLAM_PC_CONS
+#define NSLAM_PC_CONS 8  // consumer waves per workgroup (2 per SIMD)
+#endif
+constexpr int kPcCons = NSLAM_PC_CONS, kPcProd = 4, kPcWaves = kPcCons + kPcProd;
 #ifndef NSLAM_PC_NB
 #define NSLAM_PC_NB 8  // corners whose row loads the producer issues together
 #endif
+#ifndef NSLAM_PC_FD
+#define NSLAM_PC_FD 1  // weight fragments the consumers keep in flight
+#endif
 #ifndef NSLAM_PC_DIAG
-#define NSLAM_PC_DIAG 0  // timing experiments only: 1 = consumers skip the chains, 2 = producers skip their work
+#define NSLAM_PC_DIAG 0  // timing experiments only: 1 = consumers skip the chains, 2 = producers skip their
+                         // work, 3 / 4 = as 1 and the producers skip the embedding / the gathers
 #endif
 constexpr int kPcSlots = 7;
 constexpr int kPcTileF = 1024;                   // one register tile: 16 floats x 64 lanes
@@ -1683,18 +1732,24 @@ __device__ __forceinline__ void pc_produce(const QueryKArgs& a, int part, int64_
   pc_flag_store(full + s, k);
   return;
 #endif
+  const unsigned long long tg0 = TL_NOW();
+#if NSLAM_PC_DIAG != 4  // (timing experiment 4: no gathers)
   pc_put(sl + 3 * kPcTileF, gather_nb<NSLAM_PC_NB>(a.c.grid[gi], q, lane), lane);
   if (part == 1) {
     __builtin_amdgcn_sched_barrier(0);
     pc_put(sl + 4 * kPcTileF, gather_nb<NSLAM_PC_NB>(a.c.grid[gm], q, lane), lane);
   }
+#endif
+  TL_ADD1(0, TL_NOW() - tg0);  // (timeline build: the producer's gather time)
   const uint64_t in = __ballot(q.inside);
   const float* B = vs + (XyzPack{1}.FB() - XyzPack{1}.V());  // (the same offset for NC = 2)
+#if NSLAM_PC_DIAG != 3  // (timing experiment 3: no embedding)
 #pragma unroll
   for (int b = 0; b < 3; ++b) {
     __builtin_amdgcn_sched_barrier(0);
     pc_put(sl + b * kPcTileF, emb_tile<false, false>(B, q.x, b, lane), lane);
   }
+#endif
   if (lane == 0) {
     int* hd = reinterpret_cast<int*>(sl + 5 * kPcTileF);
     hd[0] = (int)unit;
@@ -1771,7 +1826,7 @@ __global__ __launch_bounds__(64 * kPcWaves, 1) void k_query_fwd_pc(QueryKArgs a,
         return v;
       };
       uint32_t m[5];
-#if NSLAM_PC_DIAG == 1  // timing experiment: consumers take and release slots without computing
+#if NSLAM_PC_DIAG == 1 || NSLAM_PC_DIAG >= 3  // timing experiment: consumers take and release slots only
       if (u >= 0) {
         f32x16 t = E(0) + E(1) + E(2) + pc_get(sl + 3 * kPcTileF, lane);
         if (t[0] == 12345.f && h == 7) a.raw[0] = t[1];  // (never true: keeps the reads)
@@ -1782,7 +1837,7 @@ __global__ __launch_bounds__(64 * kPcWaves, 1) void k_query_fwd_pc(QueryKArgs a,
         const f32x16 cf[2] = {pc_get(sl + 3 * kPcTileF, lane), pc_get(sl + 4 * kPcTileF, lane)};
         const XyzPack L{2};
         const float* vs = vsec[1];
-        const f32x16 h4 = xyz_forward_pf_e<2, false>(a.c.packed[NSLAM_DEC_FINE], cf, E, lane, m, nullptr, vs);
+        const f32x16 h4 = xyz_forward_pf_e<2, false, 5, NSLAM_PC_FD>(a.c.packed[NSLAM_DEC_FINE], cf, E, lane, m, nullptr, vs);
         save_masks(a, NSLAM_DEC_FINE, tile, m, lane);
         float o = out_row(vs + (L.Wo() - L.V()), vs + (L.Bo() - L.V()), 0, h4, lane);
         if (!inside) o = 0.f;
@@ -1798,7 +1853,7 @@ __global__ __launch_bounds__(64 * kPcWaves, 1) void k_query_fwd_pc(QueryKArgs a,
         const f32x16 cm[1] = {pc_get(sl + 3 * kPcTileF, lane)};
         const XyzPack L{1};
         const float* vs = vsec[0];
-        const f32x16 h4 = xyz_forward_pf_e<1, false>(a.c.packed[NSLAM_DEC_MIDDLE], cm, E, lane, m, nullptr, vs);
+        const f32x16 h4 = xyz_forward_pf_e<1, false, 5, NSLAM_PC_FD>(a.c.packed[NSLAM_DEC_MIDDLE], cm, E, lane, m, nullptr, vs);
         save_masks(a, NSLAM_DEC_MIDDLE, tile, m, lane);
         float o = out_row(vs + (L.Wo() - L.V()), vs + (L.Bo() - L.V()), 0, h4, lane);
         if (!inside) o = 100.f;
@@ -1808,7 +1863,7 @@ __global__ __launch_bounds__(64 * kPcWaves, 1) void k_query_fwd_pc(QueryKArgs a,
         const XyzPack L{1};
         const float* vs = vsec[2];
         float* tp = TAPE ? a.c.act_tape + tile * kTapeFloats : nullptr;
-        const f32x16 h4 = xyz_forward_pf_e<1, TAPE, 12>(a.c.packed[NSLAM_DEC_COLOR], cc, E, lane, m, tp, vs);
+        const f32x16 h4 = xyz_forward_pf_e<1, TAPE, 12, NSLAM_PC_FD>(a.c.packed[NSLAM_DEC_COLOR], cc, E, lane, m, tp, vs);
         save_masks(a, NSLAM_DEC_COLOR, tile, m, lane);
         float o[3];
 #pragma unroll

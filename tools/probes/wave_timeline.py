@@ -42,13 +42,16 @@ def analyse(name, t, parts=None):
     print("   end                         " + " ".join(f"p{p}={np.percentile((en - t0) * TICK_US, p):.1f}" for p in q))
     print("   lifetime                    " + " ".join(f"p{p}={np.percentile(life, p):.1f}" for p in q))
     if parts is not None:
-        waits = (parts[ok] >> 8) * TICK_US  # time the wave spent polling flags (k_query_fwd_pc), if recorded
+        waits = ((parts[ok] >> 8) & 0xffffff) * TICK_US  # time the wave spent polling flags (k_query_fwd_pc)
+        field1 = ((parts[ok] >> 32) & 0xffffff) * TICK_US  # a second timed phase (the pc producer's gathers)
         parts = parts & 0xff
         pp = parts[ok]
         for v in np.unique(pp):
             lv = life[pp == v]
             wv = waits[pp == v]
             extra = f", waiting {wv.mean():.1f} us ({wv.sum() / lv.sum():.0%})" if wv.any() else ""
+            f1 = field1[pp == v]
+            extra += f", gathering {f1.mean():.1f} us ({f1.sum() / lv.sum():.0%})" if f1.any() else ""
             print(f"     part {v}: {len(lv)} waves, lifetime p50 {np.median(lv):.1f} p90 {np.percentile(lv, 90):.1f}"
                   f" mean {lv.mean():.1f} us{extra}")
     # per SIMD: waves received, max resident at once, busy span (first start .. last end)
