@@ -2177,7 +2177,10 @@ inline int acc_floats_of(const nslam_dec_grad& dg) { return (int)((dg.count + 3)
 // need not wait for each other: the lean mask-only chain (grid gradient, d/dpts) and k_color_wgrad, a
 // split-K reduction over tile chunks of every weight block (one 8-wave workgroup per chunk; each
 // chunk's partial sums fill one slab), then k_slab_reduce over the chunks.  Workspace: the chunk slabs.
-constexpr int kCwTargetChunks = 256;  // one workgroup per CU
+#ifndef NSLAM_CW_CHUNKS
+#define NSLAM_CW_CHUNKS 256
+#endif
+constexpr int kCwTargetChunks = NSLAM_CW_CHUNKS;  // one workgroup per CU
 struct CwPlan {
   int64_t chunk_tiles;
   int nchunks;
