@@ -100,11 +100,18 @@ SPAN_KERNELS = {
     "query_bwd.middle+fine": ("k_dec_bwd_multi<false>",),
     "query_bwd.middle+fine+color": ("k_dec_bwd_multi<false>",),
 }
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r04_traffic.json")
-STRESS_TRAFFIC_FILE = os.path.join(REPO, "profiles", "r04_traffic_stress.json")
+def _latest_profile(suffix):
+    """profiles/rNN_<suffix> of the newest round that has one (the counters are collected per round)."""
+    import glob
+    found = sorted(glob.glob(os.path.join(REPO, "profiles", f"r[0-9][0-9]_{suffix}")))
+    return found[-1] if found else os.path.join(REPO, "profiles", f"r04_{suffix}")
+
+
+TRAFFIC_FILE = _latest_profile("traffic.json")
+STRESS_TRAFFIC_FILE = _latest_profile("traffic_stress.json")
 # SQ / GRBM counters of the same kernels (tools/gpu_counters.sh → tools/pmc_summary.py)
-PMC_FILE = os.path.join(REPO, "profiles", "r04_room0_pmc.txt")
-STRESS_PMC_FILE = os.path.join(REPO, "profiles", "r04_stress_pmc.txt")
+PMC_FILE = _latest_profile("room0_pmc.txt")
+STRESS_PMC_FILE = _latest_profile("stress_pmc.txt")
 
 
 def pmc_traffic(span, path=None):

@@ -572,14 +572,28 @@ struct SeqPipe {
   }
 };
 
+// no fragment pipeline: each GEMM loads its own fragment (gemm_acc), in frag_seq order
+template <int NC>
+struct NoPipe {
+  const float* pk;
+  int lane, i;
+  __device__ __forceinline__ NoPipe(const float* pk_, int, int lane_) : pk(pk_), lane(lane_), i(0) {}
+  __device__ __forceinline__ void gemm(f32x16& acc, const f32x16& x, int) {
+    gemm_acc(acc, pk + frag_seq<NC>(i) * NSLAM_FRAG, x, lane);
+    ++i;
+  }
+};
+
 // (E(b): embedding block b — sin(x B_b) formed here, or handed over by a producer wave, k_query_fwd_pc;
-//  FD: weight fragments in flight, 1 = FragPipe)
+//  FD: weight fragments in flight, 1 = FragPipe, 0 = none)
 template <int NC, bool TAPE, int MK = 5, int FD = 1, class EmbFn>
 __device__ __forceinline__ f32x16 xyz_forward_pf_e(const float* __restrict__ pk, const f32x16 (&cin)[NC],
                                                    const EmbFn& E, int lane, uint32_t m[5],
                                                    float* __restrict__ tape, const float* vs) {
   const XyzPack L{NC};
-  typename std::conditional<FD == 1, FragPipe, SeqPipe<NC, FD>>::type fp(pk, L.L0(), lane);
+  typename std::conditional<FD == 1, FragPipe,
+                            typename std::conditional<FD == 0, NoPipe<NC>, SeqPipe<NC, FD>>::type>::type fp(
+      pk, L.L0(), lane);
   f32x16 a = vec_tile(vs + (L.Bias(0) - L.V()), lane);
   f32x16 a3 = vec_tile(vs + (L.Bias(3) - L.V()), lane);
 #pragma unroll
@@ -623,12 +637,18 @@ __device__ __forceinline__ f32x16 xyz_forward_pf_e(const float* __restrict__ pk,
   PHASE(0, MK + 3);
   return h;
 }
+#ifndef NSLAM_UNITS_PAIR
+#define NSLAM_UNITS_PAIR 1  // the fine unit's two gathers software-pipelined together (0: one after the other)
+#endif
+#ifndef NSLAM_UNITS_FD
+#define NSLAM_UNITS_FD 1  // weight fragments in flight in the units / parts forward (0: none, 1: FragPipe)
+#endif
 template <int NC, bool TAPE, int MK = 5>
 __device__ __forceinline__ f32x16 xyz_forward_pf(const float* __restrict__ pk, const f32x16 (&cin)[NC],
                                                  const float x[3], int lane, uint32_t m[5],
                                                  float* __restrict__ tape, const float* vs) {
   const XyzPack L{NC};
-  return xyz_forward_pf_e<NC, TAPE, MK>(
+  return xyz_forward_pf_e<NC, TAPE, MK, NSLAM_UNITS_FD>(
       pk, cin, [&](int b) { return emb_tile<false, false>(vs + (L.FB() - L.V()), x, b, lane); }, lane, m, tape, vs);
 }
 
@@ -1425,7 +1445,12 @@ __device__ __forceinline__ void fwd_part_fine(const QueryKArgs& a, const Pt& q, 
   uint32_t m[5];
   PHASE(0, 2);
   f32x16 cf[2];
+#if NSLAM_UNITS_PAIR
   gather_pair(a.c.grid[NSLAM_DEC_FINE], a.c.grid[NSLAM_DEC_MIDDLE], q, lane, cf[0], cf[1]);
+#else
+  cf[0] = gather_one(a.c.grid[NSLAM_DEC_FINE], q, lane);
+  cf[1] = gather_one(a.c.grid[NSLAM_DEC_MIDDLE], q, lane);
+#endif
   PHASE(0, 3);
   const float* pk = a.c.packed[NSLAM_DEC_FINE];
   const XyzPack L{2};
@@ -1602,11 +1627,18 @@ __global__ __launch_bounds__(256, 3) void k_query_fwd_dyn(QueryKArgs a, float* _
 // the SIMDs (k_query_fwd_parts' 4-wave workgroups of middle-then-colour waves left the SIMDs that drew
 // two of them running ~25 us after the others: tools/probes/wave_timeline.py, profiles/r05_*).
 template <int STAGE, bool TAPE>
-__global__ __launch_bounds__(64, 3) void k_query_fwd_units(QueryKArgs a, float* __restrict__ occ_mid) {
+#ifndef NSLAM_UNITS_ORDER
+#define NSLAM_UNITS_ORDER 0  // dispatch order of the colour stage's units: 0 fine, middle, colour; 1 fine, colour, middle
+#endif
+#ifndef NSLAM_UNITS_LB
+#define NSLAM_UNITS_LB 3  // waves per SIMD the units kernel's register budget allows (4: <= 128 VGPRs)
+#endif
+__global__ __launch_bounds__(64, NSLAM_UNITS_LB) void k_query_fwd_units(QueryKArgs a, float* __restrict__ occ_mid) {
   const int64_t ntiles = (a.n + 31) / 32;
   const int64_t u = blockIdx.x;
-  const int part = u < ntiles ? 1 : u < 2 * ntiles ? 0 : 2;
-  const int64_t tile = u - (part == 1 ? 0 : part == 0 ? ntiles : 2 * ntiles);
+  const int j = u < ntiles ? 0 : u < 2 * ntiles ? 1 : 2;  // dispatch slot
+  const int part = j == 0 ? 1 : (NSLAM_UNITS_ORDER == 1 && STAGE == NSLAM_STAGE_COLOR) ? (j == 1 ? 2 : 0) : (j == 1 ? 0 : 2);
+  const int64_t tile = u - j * ntiles;
   TL(0, 0, part);
   // this unit's decoder vector section (biases, output rows, Fourier B), read by every layer
   __shared__ __attribute__((aligned(16))) float vsec[kVecFloats];
