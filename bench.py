@@ -16,6 +16,7 @@ import importlib
 import json
 import math
 import os
+import re
 import sys
 import time
 
@@ -159,10 +160,12 @@ def pmc_counters(span, path=None):
         if "(avg " in head:
             out["avg_us"] = float(head.split("(avg ")[1].split(" us")[0])
         for line in body.splitlines():
-            line = line.strip()
-            if line.startswith("("):
-                k, v = line.rsplit(" ", 1)
-                out[k.strip()[1:-1]] = float(v)
+            # "(name)   value   [(note)]": the derived figures of tools/pmc_summary.py
+            mt = re.match(r"^\((.+?)\)\s+([-+0-9.eE]+)(?:\s+\((.*)\))?\s*$", line.strip())
+            if mt:
+                out[mt.group(1)] = float(mt.group(2))
+                if mt.group(3):
+                    out[mt.group(1) + " note"] = mt.group(3)
         return out
     return None
 
