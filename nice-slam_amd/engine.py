@@ -112,6 +112,10 @@ class MappingEngine:
         # wave slot of the chip; a prefetch sampler wave resident on a SIMD leaves room for only two of
         # the forward's three)
         self.prefetch_at = os.environ.get("NSLAM_PREFETCH_AT", "start")
+        # the ray prefetch's stream: its own ("own") or the backward's first side stream ("lean")
+        self.prefetch_stream = os.environ.get("NSLAM_PREFETCH_STREAM", "own")
+        self.adam_merge = os.environ.get("NSLAM_ADAM_MERGE", "0") == "1"
+        self._wg_ev = None
         for k, v in c.items():
             if not v.is_contiguous(memory_format=torch.channels_last_3d):
                 raise ValueError(f"{k} must be channels-last (ops.channels_last)")
@@ -255,6 +259,9 @@ class MappingEngine:
         if not self.wgrad_first:
             units.sort(key=lambda u: u[0] == "wgrad")
         has_wgrad = any(u[0] == "wgrad" for u in units)
+        # NSLAM_ADAM_MERGE=1 (experiment): one Adam call after both branches, on the lean launch's stream
+        merge_adam = (self.adam_merge and has_wgrad and on_branch is not None and not ordered_branches
+                      and self.wgrad_first and concurrent and len(units) == 2 and units[1][0] == "lean")
         wgrad_st = None
         main = torch.cuda.current_stream(z.device)
         par = concurrent and len(units) > 1
@@ -281,6 +288,10 @@ class MappingEngine:
                                                          st.cuda_stream)
                         check(rc, "nslam_color_wgrad")
                         wgrad_st = st  # (its update waits for the lean launch: see below)
+                        if merge_adam:
+                            if self._wg_ev is None:
+                                self._wg_ev = torch.cuda.Event()
+                            self._wg_ev.record(st)
                     elif kind == "lean":
                         lc = _lib.NslamQueryCfg.from_buffer_copy(cfg)  # grids (and d/dpts) only
                         gps = (ctypes.c_void_p * 4)()
@@ -299,7 +310,12 @@ class MappingEngine:
                             self._lean_ev = torch.cuda.Event()
                         if has_wgrad and not ordered_branches:
                             self._lean_ev.record(st)
-                        if on_branch is not None:
+                        if on_branch is not None and merge_adam:
+                            # every update of the iteration in one Adam call on this stream, once the
+                            # weight-gradient branch (its slab reduction; its colour-grid gathers) is done
+                            st.wait_event(self._wg_ev)
+                            on_branch(names, part="all")
+                        elif on_branch is not None:
                             # the grids of this launch — but the colour grid, which k_color_wgrad reads (its
                             # colour feature) and which is updated on that branch once both are done.  A
                             # trainable decoder here without a weight-gradient branch (no points) still
@@ -325,7 +341,7 @@ class MappingEngine:
                 if pts_grad and st is not main:
                     for name in names:
                         gp[name].record_stream(st)
-            if has_wgrad and on_branch is not None:
+            if has_wgrad and on_branch is not None and not merge_adam:
                 # the colour grid and the colour decoder, on the weight-gradient branch after its kernel
                 # and after the lean launch (the colour grid's gradient; and no Adam may rewrite the grid
                 # while k_color_wgrad still gathers from it)
@@ -431,7 +447,14 @@ class MappingEngine:
             self._parity ^= 1
             main = torch.cuda.current_stream(self.device)
             if self._pre_stream is None:
-                self._pre_stream = torch.cuda.Stream(self.device)
+                if self.prefetch_stream == "lean":
+                    # the backward's first side stream (the mask-only launch's): one side queue fewer in
+                    # the iteration's graph; the prefetch is done long before that stream's backward work
+                    if not self._side:
+                        self._side.append(torch.cuda.Stream(self.device))
+                    self._pre_stream = self._side[0]
+                else:
+                    self._pre_stream = torch.cuda.Stream(self.device)
             side = self._pre_stream
 
             def launch_prefetch():

@@ -1,0 +1,14 @@
+# A/B: prefetch on the lean stream (shared) alone and with one merged Adam call on that stream
+set -o pipefail
+D=gpurun_out/r5p; mkdir -p $D; export TMPDIR=/tmp
+NSLAM_PREFETCH_STREAM=lean NSLAM_ADAM_MERGE=1 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_fused.py tests/test_gpu_loop.py -k "engine or loop or mapper" > $D/tests.log 2>&1 || { tail -40 $D/tests.log; exit 1; }
+tail -1 $D/tests.log
+run() {  # name [env]
+  env $2 timeout -k 10 200 python -u bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-stress --no-bulk --no-frames > $D/$1.json 2> $D/$1.err || { tail -20 $D/$1.err; exit 1; }
+  python -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); k=d['kernels_ms']; print(sys.argv[2], round(d['ms_per_step'],4), 'ms', {x: k.get(x) for x in ('query_fwd','query_bwd.color_wgrad','query_bwd.middle+fine+color','adam')})" $D/$1.json "$1"
+}
+for r in 1 2 3; do
+run own_$r "NSLAM_PREFETCH_STREAM=own"
+run shared_$r "NSLAM_PREFETCH_STREAM=lean"
+run sharedmerge_$r "NSLAM_PREFETCH_STREAM=lean NSLAM_ADAM_MERGE=1"
+done
