@@ -112,9 +112,13 @@ class MappingEngine:
         # wave slot of the chip; a prefetch sampler wave resident on a SIMD leaves room for only two of
         # the forward's three)
         self.prefetch_at = os.environ.get("NSLAM_PREFETCH_AT", "start")
-        # the ray prefetch's stream: its own ("own") or the backward's first side stream ("lean")
-        self.prefetch_stream = os.environ.get("NSLAM_PREFETCH_STREAM", "own")
-        self.adam_merge = os.environ.get("NSLAM_ADAM_MERGE", "0") == "1"
+        # the ray prefetch's stream: the backward's first side stream ("lean", default: one side queue
+        # fewer in a captured iteration) or its own ("own"); and one Adam call for the whole update on that
+        # stream once both backward branches are done (NSLAM_ADAM_MERGE=1, default) instead of one per
+        # branch (0).  A/B, round 5: 0.2177 / 0.2150 / 0.2129 ms per room0 iteration (own, lean, lean +
+        # merged Adam; medians of 3 alternating rounds, profiles/r05_experiments/ab_defaults.txt)
+        self.prefetch_stream = os.environ.get("NSLAM_PREFETCH_STREAM", "lean")
+        self.adam_merge = os.environ.get("NSLAM_ADAM_MERGE", "1") == "1"
         self._wg_ev = None
         for k, v in c.items():
             if not v.is_contiguous(memory_format=torch.channels_last_3d):
@@ -259,7 +263,7 @@ class MappingEngine:
         if not self.wgrad_first:
             units.sort(key=lambda u: u[0] == "wgrad")
         has_wgrad = any(u[0] == "wgrad" for u in units)
-        # NSLAM_ADAM_MERGE=1 (experiment): one Adam call after both branches, on the lean launch's stream
+        # NSLAM_ADAM_MERGE=1: one Adam call after both branches, on the lean launch's stream
         merge_adam = (self.adam_merge and has_wgrad and on_branch is not None and not ordered_branches
                       and self.wgrad_first and concurrent and len(units) == 2 and units[1][0] == "lean")
         wgrad_st = None
