@@ -277,9 +277,13 @@ def test_engine_prefetch_matches_serial(tiny):
     and the kept-ray counter covers one batch ahead."""
     sc, frames = _frames(tiny)
     out = {}
-    for pre in (False, True):
+    # (prefetch, its stream, one merged Adam): serial; the round-5 default (the prefetch on the mask-only
+    # launch's stream, one Adam after both branches); round 4's (its own stream, per-branch Adam)
+    for key in ((False, "lean", True), (True, "lean", True), (True, "own", False)):
+        pre, pst, merge = key
         nice, c = _nice(sc)
         eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV)
+        eng.prefetch_stream, eng.adam_merge = pst, merge
         opt = P.ops.FusedAdam([{"params": [eng.decs["color"].param], "lr": 0.005}] +
                               [{"params": [c[k]], "lr": 0.005} for k in ("grid_middle", "grid_fine", "grid_color")])
         kept = torch.zeros(1, dtype=torch.int64, device=DEV)
@@ -289,14 +293,18 @@ def test_engine_prefetch_matches_serial(tiny):
                                   seed=11, n_kept=kept, prefetch=pre)
             losses.append(rl.clone())
         torch.cuda.synchronize()
-        out[pre] = (losses, {k: v.detach().clone() for k, v in c.items()}, eng.decs["color"].param.detach().clone(),
-                    int(kept))
-    for a, b in zip(out[False][0], out[True][0]):
-        assert rel_l2(b, a) < 1e-5
-    for k in out[False][1]:
-        assert rel_l2(out[True][1][k], out[False][1][k]) < 1e-5, k
-    assert rel_l2(out[True][2], out[False][2]) < 1e-5
-    assert out[True][3] >= out[False][3] > 0  # prefetch has drawn (and counted) one batch more
+        out[key] = (losses, {k: v.detach().clone() for k, v in c.items()}, eng.decs["color"].param.detach().clone(),
+                    int(kept), sorted(float(st["step"]) for st in opt.state.values()))
+    ref = out[(False, "lean", True)]
+    for key in ((True, "lean", True), (True, "own", False)):
+        o = out[key]
+        for a, b in zip(ref[0], o[0]):
+            assert rel_l2(b, a) < 1e-5, key
+        for k in ref[1]:
+            assert rel_l2(o[1][k], ref[1][k]) < 1e-5, (key, k)
+        assert rel_l2(o[2], ref[2]) < 1e-5, key
+        assert o[3] >= ref[3] > 0, key  # prefetch has drawn (and counted) one batch more
+        assert o[4] == ref[4] == [4.0] * 4, key
 
 
 def test_engine_per_branch_adam_matches_single_adam(tiny):
