@@ -119,6 +119,9 @@ class MappingEngine:
         # merged Adam; medians of 3 alternating rounds, profiles/r05_experiments/ab_defaults.txt)
         self.prefetch_stream = os.environ.get("NSLAM_PREFETCH_STREAM", "lean")
         self.adam_merge = os.environ.get("NSLAM_ADAM_MERGE", "1") == "1"
+        # where the merged Adam runs: after the mask-only launch on its side stream ("side") or on the
+        # main stream after the join ("main", experiment)
+        self.adam_on = os.environ.get("NSLAM_ADAM_ON", "side")
         self._wg_ev = None
         for k, v in c.items():
             if not v.is_contiguous(memory_format=torch.channels_last_3d):
@@ -263,6 +266,7 @@ class MappingEngine:
         if not self.wgrad_first:
             units.sort(key=lambda u: u[0] == "wgrad")
         has_wgrad = any(u[0] == "wgrad" for u in units)
+        merged_names = None
         # NSLAM_ADAM_MERGE=1: one Adam call after both branches, on the lean launch's stream
         merge_adam = (self.adam_merge and has_wgrad and on_branch is not None and not ordered_branches
                       and self.wgrad_first and concurrent and len(units) == 2 and units[1][0] == "lean")
@@ -314,7 +318,9 @@ class MappingEngine:
                             self._lean_ev = torch.cuda.Event()
                         if has_wgrad and not ordered_branches:
                             self._lean_ev.record(st)
-                        if on_branch is not None and merge_adam:
+                        if on_branch is not None and merge_adam and self.adam_on == "main":
+                            merged_names = names  # (the merged Adam runs on the main stream after the join)
+                        elif on_branch is not None and merge_adam:
                             # every update of the iteration in one Adam call on this stream, once the
                             # weight-gradient branch (its slab reduction; its colour-grid gathers) is done
                             st.wait_event(self._wg_ev)
@@ -354,6 +360,11 @@ class MappingEngine:
                     on_branch(["color"], part="all")
             for st in used:
                 main.wait_stream(st)
+            if merged_names is not None:
+                # NSLAM_ADAM_ON=main: the merged update on the main stream after the join (the weight
+                # gradients ran on it; the join covers the lean launch), so the next iteration's forward
+                # follows it on the same queue
+                on_branch(merged_names, part="all")
         if not pts_grad:
             return None
         parts = [gp[d] for d in decs]
