@@ -111,7 +111,8 @@ typedef struct nslam_query_cfg {
    * float, nslam_query_tape_size(M) bytes; layout private to the library); with it and saved_masks the colour decoder's weight-gradient
    * backward reads them instead of recomputing its forward (Mapper.py:503). */
   float* act_tape;
-  /* ABI v17: cotangent of the colour decoder's last hidden layer h4, [M][32] float32 (NULL = none),
+  /* ABI v17: cotangent of the colour decoder's last hidden layer h4, [M][32] float32, 16-byte aligned
+   * (else NSLAM_EINVAL; NULL = none),
    * added to its output layer's Woᵀg in every backward of the colour decoder.  A direct caller of
    * MLP(color=True) (decoder.py:154-159,198-203) forms the 4th output row h4·Wo[3] + bo[3] itself
    * (NICE.forward overwrites that row, decoder.py:341) and passes d/dh4 here. */

@@ -7,7 +7,7 @@ The directory name is not a Python identifier: import with importlib.import_modu
 """
 import sys as _sys
 
-from . import _lib, common, config, datasets, decoder, distributed, engine, mapper, ops, packing, renderer, slam, tracker  # noqa: F401,E501
+from . import _lib, common, datasets, decoder, distributed, engine, mapper, ops, packing, renderer, slam, tracker  # noqa: F401,E501
 from .datasets import get_dataset  # noqa: F401
 from .decoder import NICE, MLP, MLP_no_xyz  # noqa: F401
 from .mapper import Mapper  # noqa: F401
@@ -16,6 +16,5 @@ from .tracker import Tracker  # noqa: F401
 
 _sys.modules.setdefault("nice_slam_amd", _sys.modules[__name__])
 
-__all__ = ["NICE", "MLP", "MLP_no_xyz", "Renderer", "Tracker", "Mapper", "get_dataset", "common", "config",
-           "datasets", "decoder",
+__all__ = ["NICE", "MLP", "MLP_no_xyz", "Renderer", "Tracker", "Mapper", "get_dataset", "common", "datasets", "decoder",
            "distributed", "mapper", "ops", "packing", "renderer", "slam", "tracker"]

@@ -66,12 +66,14 @@ extern "C" int nslam_query_fwd_ws(const nslam_query_cfg* cfg, const double* pts,
   const dim3 b256(256);
   // forward variant: cfg->fwd_variant, else NSLAM_FWD_MODE=pc (producer / consumer waves, one persistent
   // workgroup per CU), units (one-wave workgroups per decoder-tile), dyn (a counter; experiment), parts
+  // (an unrecognised NSLAM_FWD_MODE is an error, not a silent fallback: a typo must not change the kernel)
   static const int env_mode = [] {
     const char* e = getenv("NSLAM_FWD_MODE");
-    if (!e) return 1;
-    return !strcmp(e, "pc") ? 3 : !strcmp(e, "dyn") ? 2 : !strcmp(e, "parts") ? 0 : 1;
+    if (!e || !*e || !strcmp(e, "units")) return 1;
+    return !strcmp(e, "pc") ? 3 : !strcmp(e, "dyn") ? 2 : !strcmp(e, "parts") ? 0 : -1;
   }();
   if (cfg->fwd_variant < 0 || cfg->fwd_variant > NSLAM_FWD_PARTS) return NSLAM_EINVAL;
+  if (cfg->fwd_variant == NSLAM_FWD_DEFAULT && env_mode < 0) return NSLAM_EINVAL;
   const int mode = cfg->fwd_variant == NSLAM_FWD_UNITS ? 1
                    : cfg->fwd_variant == NSLAM_FWD_PC  ? 3
                    : cfg->fwd_variant == NSLAM_FWD_PARTS ? 0

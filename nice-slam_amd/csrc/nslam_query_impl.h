@@ -1689,10 +1689,6 @@ constexpr int kPcCons = NSLAM_PC_CONS, kPcProd = 4, kPcWaves = kPcCons + kPcProd
 #ifndef NSLAM_PC_FD
 #define NSLAM_PC_FD 1  // weight fragments the consumers keep in flight
 #endif
-#ifndef NSLAM_PC_DIAG
-#define NSLAM_PC_DIAG 0  // timing experiments only: 1 = consumers skip the chains, 2 = producers skip their
-                         // work, 3 / 4 = as 1 and the producers skip the embedding / the gathers
-#endif
 constexpr int kPcSlots = 7;
 constexpr int kPcTileF = 1024;                   // one register tile: 16 floats x 64 lanes
 constexpr int kPcSlotF = 5 * kPcTileF + 4;       // emb 0-2, features 3-4, header {unit, inside lo, hi}
@@ -1721,13 +1717,15 @@ __device__ __forceinline__ void pc_flag_store(int* p, int v) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// (bounded: a wait that never ends — a broken invariant — gives up after ~10^8 cycles, so the launch
-// still drains and the wrong results show in the parity tests instead of a hung device)
+// (bounded: a wait that never ends — a broken invariant; one unit's hand-over takes microseconds — traps
+// after ~2^24 polls (~0.5 s) instead of letting the wave go on with a slot it does not own: the launch
+// fails loudly, the caller's next HIP call reports the error, and nothing is silently corrupted)
 __device__ __forceinline__ void pc_flag_wait(const int* p, int v) {
-  const unsigned long long t0 = TL_NOW();
-  for (int it = 0; it < (1 << 21); ++it) {
+  [[maybe_unused]] const unsigned long long t0 = TL_NOW();
+  for (int it = 0;; ++it) {
     const int x = __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
     if (x == v) break;
+    if (it == (1 << 24)) __builtin_trap();
     __builtin_amdgcn_s_sleep(1);
   }
   TL_ADD(0, TL_NOW() - t0);  // (timeline build: the wave's waiting time)
@@ -1755,33 +1753,20 @@ __device__ __forceinline__ void pc_produce(const QueryKArgs& a, int part, int64_
   // it is formed — the features, then the embedding blocks one at a time — so at most one tile and the
   // loads of one gather are in registers
   pc_flag_wait(freed + s, k - kPcSlots);
-#if NSLAM_PC_DIAG == 2  // timing experiment: producers publish without gathering or embedding
-  if (lane == 0) {
-    int* hd = reinterpret_cast<int*>(sl + 5 * kPcTileF);
-    hd[0] = (int)unit;
-    hd[1] = hd[2] = -1;
-  }
-  pc_flag_store(full + s, k);
-  return;
-#endif
-  const unsigned long long tg0 = TL_NOW();
-#if NSLAM_PC_DIAG != 4  // (timing experiment 4: no gathers)
+  [[maybe_unused]] const unsigned long long tg0 = TL_NOW();
   pc_put(sl + 3 * kPcTileF, gather_nb<NSLAM_PC_NB>(a.c.grid[gi], q, lane), lane);
   if (part == 1) {
     __builtin_amdgcn_sched_barrier(0);
     pc_put(sl + 4 * kPcTileF, gather_nb<NSLAM_PC_NB>(a.c.grid[gm], q, lane), lane);
   }
-#endif
   TL_ADD1(0, TL_NOW() - tg0);  // (timeline build: the producer's gather time)
   const uint64_t in = __ballot(q.inside);
   const float* B = vs + (XyzPack{1}.FB() - XyzPack{1}.V());  // (the same offset for NC = 2)
-#if NSLAM_PC_DIAG != 3  // (timing experiment 3: no embedding)
 #pragma unroll
   for (int b = 0; b < 3; ++b) {
     __builtin_amdgcn_sched_barrier(0);
     pc_put(sl + b * kPcTileF, emb_tile<false, false>(B, q.x, b, lane), lane);
   }
-#endif
   if (lane == 0) {
     int* hd = reinterpret_cast<int*>(sl + 5 * kPcTileF);
     hd[0] = (int)unit;
@@ -1858,13 +1843,6 @@ __global__ __launch_bounds__(64 * kPcWaves, 1) void k_query_fwd_pc(QueryKArgs a,
         return v;
       };
       uint32_t m[5];
-#if NSLAM_PC_DIAG == 1 || NSLAM_PC_DIAG >= 3  // timing experiment: consumers take and release slots only
-      if (u >= 0) {
-        f32x16 t = E(0) + E(1) + E(2) + pc_get(sl + 3 * kPcTileF, lane);
-        if (t[0] == 12345.f && h == 7) a.raw[0] = t[1];  // (never true: keeps the reads)
-        continue;
-      }
-#endif
       if (part == 1) {
         const f32x16 cf[2] = {pc_get(sl + 3 * kPcTileF, lane), pc_get(sl + 4 * kPcTileF, lane)};
         const XyzPack L{2};
@@ -2193,6 +2171,8 @@ inline int check_cfg(const nslam_query_cfg* c, bool bwd) {
   if (c->rays_o) {
     if (!c->rays_d || !c->z_vals || c->n_samples <= 0) return NSLAM_EINVAL;
   }
+  // the h4 cotangent is read as float4 rows (add_gh4, k_color_wgrad): 16-byte aligned
+  if (c->g_h4 && (((uintptr_t)c->g_h4) & 15) != 0) return NSLAM_EINVAL;
   return NSLAM_OK;
 }
 

@@ -96,21 +96,34 @@ class SparseGradExchange:
         self.force = force_collectives
         self.pack = pack or ops.rows_pack
         self.unpack = unpack or ops.rows_unpack
-        offs, off = {}, 0
-        for k, v in engine.c.items():  # flat buffer order = engine.ggrad order
-            offs[k] = off
-            off += v.numel() // 32
-        self.rows = {k: (r.to(torch.int64) + offs[k]).to(torch.int32) for k, r in rows.items()}
+        self.rows = self._flat_rows(rows)
         self._plan = {}
         self._gen = getattr(engine, "layout_gen", 0)
 
+    def _flat_rows(self, rows):
+        """{grid key: int32 rows offset into the engine's flat (dense) grid-gradient buffer}."""
+        offs, off = {}, 0
+        for k, v in self.engine.c.items():  # flat buffer order = engine.ggrad order
+            offs[k] = off
+            off += v.numel() // 32
+        return {k: (r.to(torch.int64) + offs[k]).to(torch.int32) for k, r in rows.items()}
+
     def validate(self, engine, keys, dnames):
         """engine.MappingEngine.iteration calls this before it enqueues anything: the cached plans hold
-        views of the engine's gradient buffers, which set_rows reallocates."""
+        views of the engine's gradient buffers, which set_rows reallocates.  After set_rows, a grid this
+        exchange sums by row list must be compact in the engine's new rows (whose compact buffer then
+        carries exactly the rows Adam reads); a grid that went back to a dense gradient would be summed
+        on the old rows while Adam reads others — the ranks would diverge silently, so that raises."""
         if engine is not self.engine:
             raise ValueError("SparseGradExchange: built for another engine")
         gen = getattr(engine, "layout_gen", 0)
         if gen != self._gen:
+            cur = getattr(engine, "rows", {})
+            stale = sorted(k for k in self.rows if k not in cur)
+            if stale:
+                raise RuntimeError(f"SparseGradExchange: the engine's gradient rows changed (set_rows) and {stale} "
+                                   "no longer have compact gradients; build a new exchange for the new rows")
+            self.rows = self._flat_rows(cur)
             self._plan.clear()  # (views of the old buffers)
             self._gen = gen
 

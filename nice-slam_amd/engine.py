@@ -35,6 +35,15 @@ from .common import get_camera_from_tensor
 _GRID_OF = {"coarse": "grid_coarse", "middle": "grid_middle", "fine": "grid_fine", "color": "grid_color"}
 
 
+def _env_choice(name, default, allowed):
+    """An engine topology knob from the environment, checked against its allowed values (a typo raises
+    instead of silently selecting another stream topology)."""
+    v = os.environ.get(name, default)
+    if v not in allowed:
+        raise ValueError(f"{name}={v!r}: expected one of {sorted(allowed)}")
+    return v
+
+
 class FlatDecoder:
     """A decoder's parameters re-bound as views of one flat float32 buffer (named_parameters
     order = the nslam_dec_grad layout) with a trailing zero slot, so packing is one gather into a
@@ -102,7 +111,7 @@ class MappingEngine:
         self.concurrent = True
         # concurrent backward: enqueue the colour weight-gradient branch before the grid-gradient one
         # (its workgroups are dispatched first and hold one slot per CU; the lean launch fills the rest)
-        self.wgrad_first = os.environ.get("NSLAM_WGRAD_FIRST", "1") == "1"
+        self.wgrad_first = _env_choice("NSLAM_WGRAD_FIRST", "1", ("0", "1")) == "1"
         # every mask-only decoder backward as ONE launch (ABI v10); False: one nslam_query_bwd_decoder
         # launch per decoder (the library then runs a colour tape backward's two kernels in sequence)
         self.merge = True
@@ -111,17 +120,17 @@ class MappingEngine:
         # forward) or "after_fwd" (beside the loss and the backward: the forward's waves then have every
         # wave slot of the chip; a prefetch sampler wave resident on a SIMD leaves room for only two of
         # the forward's three)
-        self.prefetch_at = os.environ.get("NSLAM_PREFETCH_AT", "start")
+        self.prefetch_at = _env_choice("NSLAM_PREFETCH_AT", "start", ("start", "after_fwd"))
         # the ray prefetch's stream: the backward's first side stream ("lean", default: one side queue
         # fewer in a captured iteration) or its own ("own"); and one Adam call for the whole update on that
         # stream once both backward branches are done (NSLAM_ADAM_MERGE=1, default) instead of one per
         # branch (0).  A/B, round 5: 0.2177 / 0.2150 / 0.2129 ms per room0 iteration (own, lean, lean +
         # merged Adam; medians of 3 alternating rounds, profiles/r05_experiments/ab_defaults.txt)
-        self.prefetch_stream = os.environ.get("NSLAM_PREFETCH_STREAM", "lean")
-        self.adam_merge = os.environ.get("NSLAM_ADAM_MERGE", "1") == "1"
+        self.prefetch_stream = _env_choice("NSLAM_PREFETCH_STREAM", "lean", ("lean", "own"))
+        self.adam_merge = _env_choice("NSLAM_ADAM_MERGE", "1", ("0", "1")) == "1"
         # where the merged Adam runs: after the mask-only launch on its side stream ("side") or on the
         # main stream after the join ("main", experiment)
-        self.adam_on = os.environ.get("NSLAM_ADAM_ON", "side")
+        self.adam_on = _env_choice("NSLAM_ADAM_ON", "side", ("side", "main"))
         self._wg_ev = None
         for k, v in c.items():
             if not v.is_contiguous(memory_format=torch.channels_last_3d):
@@ -462,9 +471,11 @@ class MappingEngine:
             self._parity ^= 1
             main = torch.cuda.current_stream(self.device)
             if self._pre_stream is None:
-                if self.prefetch_stream == "lean":
-                    # the backward's first side stream (the mask-only launch's): one side queue fewer in
-                    # the iteration's graph; the prefetch is done long before that stream's backward work
+                if self.prefetch_stream == "lean" and self.wgrad_first and self.concurrent:
+                    # the backward's first side stream (the mask-only launch's, with the weight-gradient
+                    # branch enqueued first on the main stream): one side queue fewer in the iteration's
+                    # graph; the prefetch is done long before that stream's backward work.  In any other
+                    # topology that side stream carries the weight-gradient branch: the prefetch gets its own
                     if not self._side:
                         self._side.append(torch.cuda.Stream(self.device))
                     self._pre_stream = self._side[0]
