@@ -2,13 +2,19 @@
 
 python bench.py [--gpus N --steps K --warmup W]   (N>1: launched by torch.distributed.run)
 
-One step = one colour-stage mapping iteration of Mapper.optimize_map (src/Mapper.py:391-519) on
-synthetic room0 data resident in HBM (configs/Replica/room0.yaml bound, replica.yaml camera,
+One step (the headline `value`) = one colour-stage iteration of the mapping engine that
+Mapper.optimize_map's inner loop runs on (engine.MappingEngine.iteration: src/Mapper.py:391-519's
+body), on synthetic room0 data resident in HBM (configs/Replica/room0.yaml bound, replica.yaml camera,
 mapping.pixels=1000 over a 5-frame window, 32 stratified + 16 surface samples):
-  pixel sampling + rays (5 frames × 200) → inside-mask prefilter → sampler kernel → fused
-  query kernel (middle+fine+colour decoders, 3 grid lookups) → compositing kernel → mapping loss →
-  backward (compositing bwd + 3 fused decoder bwd launches: grid-gradient atomics + colour-decoder
-  weight gradients) → [N>1: RCCL all-reduce of the gradients] → Adam step on grids + colour decoder.
+  pixel draws + rays (5 frames × 200, in the gather kernel) → inside-mask prefilter → sampler kernel →
+  fused query kernel (middle+fine+colour decoders, 3 grid lookups) → loss kernel (compositing + mapping
+  loss + their backward) → backward (one mask-only launch for the grid gradients ‖ the colour decoder's
+  weight gradients) → [N>1: RCCL all-reduce of the frustum-row gradients] → Adam on the frustum rows +
+  colour decoder — replayed from hipGraphs.
+The reference entry points are timed in their own legs: "optimize_map" (Mapper.optimize_map per call,
+60 iterations, BA off / on, against the bare engine's iterations of the same stage mix), "scene0000_ba"
+(configs[2]: optimize_map with bundle adjustment, 5000 px) and "room0_slam_loop" (measured frames/s of
+Tracker.track_frame every frame + Mapper.optimize_map every 5th frame).
 Weak scaling: every rank maps its own 1000 rays; value = all ranks' ray-samples / max rank time.
 """
 import argparse
@@ -60,6 +66,11 @@ STRESS = dict(ROOM0, bound=[[0.0, 7.9]] * 3, bound_divisible=0.5,
 APARTMENT = dict(ROOM0, bound=[[-5.8, 11.3], [-4.0, 4.5], [-7.9, 4.9]], bound_divisible=0.32,
                  H=720, W=1280, fx=607.4694213867188, fy=607.4534912109375, cx=636.9967041015625,
                  cy=369.2689514160156, pixels=5000, window=5, coarse=True)
+# configs[2] (BASELINE.json): ScanNet scene0000 (configs/ScanNet/scene0000.yaml bound, scannet.yaml camera
+# after crop_edge 10), 5000 pixels over a 5-frame window (4 keyframes + the current frame) x 48 samples,
+# bundle adjustment of the 4 non-oldest cameras
+SCENE0000 = dict(ROOM0, bound=[[-2.0, 11.0], [-2.0, 11.5], [-2.0, 5.5]], bound_divisible=0.32,
+                 H=460, W=620, fx=577.590698, fy=578.729797, cx=308.905426, cy=232.683609, pixels=5000, window=5)
 FLOP_FWD_PER_SAMPLE = 2 * (15479 + 20599 + 15575)   # SURVEY §8(a10) MACs, colour stage
 FLOP_FINE_STAGE_PER_POINT = 2 * (15479 + 20599)          # fine stage: middle + fine decoders
 BYTES_FWD_PER_SAMPLE = 3 * 1024                      # 3 trilinear lookups × 8 corners × 128 B
@@ -879,6 +890,156 @@ def room0_frame_rate(scene, reps=100):
                     "tracker and mapper overlapped as the reference's processes (max of the two)"}
 
 
+def nice_slam_cfg(cfg, tracking_edge=100):
+    """The reference's configs/nice_slam.yaml tracking / mapping keys with a scene's camera and pixel
+    counts (configs/Replica/replica.yaml, configs/ScanNet/scannet.yaml): what Tracker / Mapper read."""
+    st = {"coarse": {"decoders_lr": 0.0, "coarse_lr": 0.001, "middle_lr": 0.0, "fine_lr": 0.0, "color_lr": 0.0},
+          "middle": {"decoders_lr": 0.0, "coarse_lr": 0.0, "middle_lr": 0.1, "fine_lr": 0.0, "color_lr": 0.0},
+          "fine": {"decoders_lr": 0.0, "coarse_lr": 0.0, "middle_lr": 0.005, "fine_lr": 0.005, "color_lr": 0.0},
+          "color": {"decoders_lr": 0.005, "coarse_lr": 0.0, "middle_lr": 0.005, "fine_lr": 0.005, "color_lr": 0.005}}
+    return {"coarse": False, "occupancy": True, "scale": 1,
+            "rendering": {"N_samples": cfg["n_strat"], "N_surface": cfg["n_surf"], "N_importance": 0, "lindisp": False,
+                          "perturb": 0.0},
+            "tracking": {"lr": 0.001, "device": "cuda:0", "iters": 10, "gt_camera": False, "pixels": 200,
+                         "seperate_LR": False, "w_color_loss": 0.5, "ignore_edge_W": tracking_edge,
+                         "ignore_edge_H": tracking_edge, "handle_dynamic": True, "use_color_in_tracking": True,
+                         "const_speed_assumption": True},
+            "mapping": {"device": "cuda:0", "fix_fine": True, "BA_cam_lr": 0.001, "fix_color": False,
+                        "pixels": cfg["pixels"], "iters": 60, "w_color_loss": cfg["w_color"], "fine_iter_ratio": 0.6,
+                        "middle_iter_ratio": 0.4, "mapping_window_size": cfg["window"],
+                        "frustum_feature_selection": True, "keyframe_selection_method": "overlap", "stage": st}}
+
+
+def slam_state(scene):
+    """What Tracker / Mapper read from the reference's NICE_SLAM object, over a scene's tensors."""
+    from types import SimpleNamespace
+    cfg = scene.cfg
+    return SimpleNamespace(nice=True, bound=scene.bound, H=cfg["H"], W=cfg["W"], fx=cfg["fx"], fy=cfg["fy"],
+                           cx=cfg["cx"], cy=cfg["cy"], shared_decoders=scene.nice, shared_c=scene.grids,
+                           renderer=scene.renderer, estimate_c2w_list=torch.zeros(4, 4, 4),
+                           gt_c2w_list=torch.zeros(4, 4, 4), mapping_idx=torch.zeros(1).int())
+
+
+def _pose4(c2w):
+    return torch.cat([c2w, torch.tensor([[0, 0, 0, 1.0]], device=c2w.device)], 0)
+
+
+def optimize_map_leg(dev, cfg, ba, calls=6, warm=2, iters=60):
+    """Mapper.optimize_map (the reference entry point, Mapper.py:230-540) timed per call on the fused
+    engine: `iters` joint iterations (middle 25 / fine 12 / colour 23 of 60), overlap keyframe selection
+    over 4 keyframes (+ the last one and the current frame: a 5-frame window), frustum masks per call,
+    a fresh Adam per call, BA of the 4 non-oldest cameras when `ba`.  Wall time of `calls` calls after
+    `warm` (whose first captures the stage graphs), synchronised around."""
+    P = pkg()
+    scene = Room0Scene(dev, 0, cfg=dict(cfg), path="autograd")  # data only (grids, decoders, frames)
+    for t in scene.grids.values():
+        t.requires_grad_(False)
+    mcfg = nice_slam_cfg(cfg)
+    mp = P.Mapper(mcfg, None, slam_state(scene))
+    mp.BA = ba
+    F = cfg["window"]
+    kf = [{"gt_c2w": _pose4(scene.c2w[f]), "idx": 50 * f, "depth": scene.depth[f], "color": scene.color[f],
+           "est_c2w": _pose4(scene.c2w[f])} for f in range(F - 1)]
+    kf_list = [50 * f for f in range(F - 1)]
+    cur = _pose4(scene.c2w[F - 1])
+
+    def call(k):
+        return mp.optimize_map(iters, 1.0, 50 * F + 5 * k, scene.color[F - 1], scene.depth[F - 1], cur, kf, kf_list,
+                               cur.clone())
+    for k in range(warm):
+        call(k)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(calls):
+        call(warm + k)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / calls
+    res = {"ms_per_call": dt * 1e3, "ms_per_iteration": dt * 1e3 / iters, "iterations_per_call": iters,
+           "calls": calls, "graphs_cached": len(mp._graphs), "bundle_adjustment": ba,
+           "pixels": cfg["pixels"], "window": F}
+    del mp, scene
+    torch.cuda.empty_cache()
+    return res
+
+
+def engine_stage_ms(dev, cfg, reps=50):
+    """The bare engine (engine.MappingEngine.iteration, hipGraph blocks) per stage at a config's shape:
+    what an optimize_map iteration of that stage costs without the drop-in's per-call work."""
+    scene = Room0Scene(dev, 0, cfg=dict(cfg), path="fused")
+    out = {}
+    for stage in ("middle", "fine", "color"):
+        out[stage], _ = graph_time(scene, lambda: scene.step(stage=stage), reps)
+    out["schedule_60"] = (25 * out["middle"] + 12 * out["fine"] + 23 * out["color"]) / 60.0
+    del scene
+    torch.cuda.empty_cache()
+    return {k: round(v, 4) for k, v in out.items()}
+
+
+def slam_loop(dev, cfg=ROOM0, frames=60, warm_frames=10):
+    """Measured room0 frames/s (BASELINE metric): the reference's per-frame work in one process on one
+    stream — Tracker.track_frame every frame (10 camera iterations x 200 pixels, edges 100 px) and
+    Mapper.optimize_map every 5th frame (60 iterations x 1000 pixels, 5-frame overlap window, frustum
+    masks, BA of 4 cameras: the steady state after 4 keyframes, Mapper.run's every_frame / BA rule,
+    Mapper.py:591-606), the tracker re-snapshotting the map after each mapping call (Tracker.py:130-142).
+    Frames cycle through 5 synthetic keyframe views; the pose guess is the ground truth nudged by 2 cm.
+    Wall time over `frames` frames after `warm_frames`, synchronised around."""
+    P = pkg()
+    scene = Room0Scene(dev, 0, cfg=dict(cfg), path="autograd")
+    for t in scene.grids.values():
+        t.requires_grad_(False)
+    mcfg = nice_slam_cfg(cfg)
+    slam = slam_state(scene)
+    tr = P.Tracker(mcfg, None, slam)
+    mp = P.Mapper(mcfg, None, slam)
+    F = cfg["window"]
+    kf = [{"gt_c2w": _pose4(scene.c2w[f]), "idx": 50 * f, "depth": scene.depth[f], "color": scene.color[f],
+           "est_c2w": _pose4(scene.c2w[f])} for f in range(F)]
+    kf_list = [50 * f for f in range(F)]
+    nudge = torch.tensor([0.02, -0.01, 0.015], device=dev)
+    stats = {"track_ms": [], "map_ms": []}
+
+    def frame(i, timed_parts=False):
+        f = i % F
+        gt = _pose4(scene.c2w[f])
+        pre = gt.clone()
+        pre[:3, 3] += nudge
+        t0 = time.perf_counter()
+        est = tr.track_frame(i + 1, scene.color[f], scene.depth[f], gt, pre_c2w=pre)
+        if timed_parts:
+            torch.cuda.synchronize()
+            stats["track_ms"].append((time.perf_counter() - t0) * 1e3)
+        if i % 5 == 0:
+            t0 = time.perf_counter()
+            mp.BA = len(kf_list) > 4
+            out = mp.optimize_map(60, 1.0, i + 1, scene.color[f], scene.depth[f], gt, kf, kf_list, est)
+            slam.mapping_idx[0] = i + 1  # the tracker snapshots the new map before its next frame
+            if timed_parts:
+                torch.cuda.synchronize()
+                stats["map_ms"].append((time.perf_counter() - t0) * 1e3)
+            return out
+        return est
+
+    for i in range(warm_frames):
+        frame(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(warm_frames, warm_frames + frames):
+        frame(i)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    for i in range(warm_frames + frames, warm_frames + frames + 10):  # component times (synchronised)
+        frame(i, timed_parts=True)
+    res = {"frames_per_s": frames / dt, "ms_per_frame": dt / frames * 1e3, "frames": frames,
+           "track_frame_ms": sum(stats["track_ms"]) / len(stats["track_ms"]),
+           "optimize_map_ms": sum(stats["map_ms"]) / max(len(stats["map_ms"]), 1),
+           "tracker_graphs": len(tr._graphs), "mapper_graphs": len(mp._graphs),
+           "workload": "room0 synthetic: track_frame every frame (10 x 200 px), optimize_map every 5th frame "
+                       "(60 x 1000 px, window 5, frustum masks, BA), one process, one stream, measured wall time"}
+    del tr, mp, scene
+    torch.cuda.empty_cache()
+    return res
+
+
 def leg_main(leg):
     """One auxiliary measurement in this (child) process on cuda:0; prints one JSON object."""
     dev = torch.device("cuda", 0)
@@ -890,6 +1051,24 @@ def leg_main(leg):
         res = frame_io(dev)
     elif leg == "apartment":
         res = apartment_iterations(dev)
+    elif leg == "optimize_map":
+        res = {"engine_ms_per_iteration": engine_stage_ms(dev, ROOM0),
+               "optimize_map": optimize_map_leg(dev, ROOM0, ba=False),
+               "optimize_map_ba": optimize_map_leg(dev, ROOM0, ba=True)}
+        for k in ("optimize_map", "optimize_map_ba"):
+            res[k]["vs_engine_schedule"] = res[k]["ms_per_iteration"] / res["engine_ms_per_iteration"]["schedule_60"]
+        res["workload"] = ("Replica room0: Mapper.optimize_map(60 iterations, 1000 px over a 5-frame window) per call "
+                           "vs the bare engine's iterations of the same stage mix (25 middle / 12 fine / 23 colour)")
+    elif leg == "scene0000":
+        res = {"engine_ms_per_iteration": engine_stage_ms(dev, SCENE0000),
+               "optimize_map_ba": optimize_map_leg(dev, SCENE0000, ba=True)}
+        om = res["optimize_map_ba"]
+        om["vs_engine_schedule"] = om["ms_per_iteration"] / res["engine_ms_per_iteration"]["schedule_60"]
+        om["ray_samples_per_s_upper"] = SCENE0000["pixels"] * 48 / (om["ms_per_iteration"] * 1e-3)
+        res["workload"] = ("configs[2] ScanNet scene0000: 460x620, Mapper.optimize_map with BA over a 5-frame window "
+                           "(4 cameras), 5000 px x 48 samples, 60 iterations per call")
+    elif leg == "slam_loop":
+        res = slam_loop(dev)
     else:
         scene = Room0Scene(dev, 0, cfg=dict(ROOM0), path="fused")
         for _ in range(3):
@@ -941,7 +1120,8 @@ def main():
                          "(identities), captured in the hipGraph like an N>1 job's")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="draw + sample each iteration's rays inside it (no overlap with the previous backward)")
-    ap.add_argument("--leg", choices=("frames", "stress", "stress_iter", "bulk", "frame_io", "apartment"), default=None,
+    ap.add_argument("--leg", choices=("frames", "stress", "stress_iter", "bulk", "frame_io", "apartment", "optimize_map",
+                                      "scene0000", "slam_loop"), default=None,
                     help="run one auxiliary measurement and print its JSON (bench.py spawns these itself)")
     args = ap.parse_args()
     global PREFETCH, EXCHANGE, FORCE_EXCHANGE
@@ -1072,6 +1252,9 @@ def main():
         # box ended in a host heap abort inside a later leg) cannot take the headline line with it
         if world == 1 and not args.no_frames and args.path == "fused":
             out["room0"] = run_leg("frames")
+            out["room0_slam_loop"] = run_leg("slam_loop")
+            out["optimize_map"] = run_leg("optimize_map")
+            out["scene0000_ba"] = run_leg("scene0000")
             out["apartment"] = run_leg("apartment")
         if world == 1 and not args.no_stress:
             out["grid_query_stress"] = run_leg("stress")

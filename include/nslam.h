@@ -311,6 +311,12 @@ typedef struct nslam_adam_seg {
    * stays current without a re-pack pass.  mirror == NULL: no mirror. */
   const int32_t* mirror_idx;
   float* mirror;
+  /* ABI v19: NULL, or a DEVICE int64: the segment updates only its first min(*n_live, n) rows (row-masked)
+   * or elements (dense).  A frustum selection made on the device (Mapper.optimize_map's per-call mask,
+   * Mapper.py:314-333) then needs no host read-back of its size: the segment, its Adam state and its
+   * launch are sized for the capacity n (every voxel of the grid), so a captured hipGraph of the
+   * iteration stays valid for every later call's selection. */
+  const int64_t* n_live;
 } nslam_adam_seg;
 /* ticket: NULL = the step counts advance in a second single-wave launch; else a device uint32
  * (zero-initialised, re-armed by the call itself) with which the update kernel's last workgroup
@@ -349,6 +355,22 @@ int nslam_cam_grad(const float* cam, const float* c2w, const double* g_pts, cons
 int nslam_cam_grad_parts(const float* cam, const float* c2w, const double* const* g_pts, int32_t n_parts,
                          const double* z_vals, const float* rays_d, int64_t n_rays, int32_t n_samples, float* g_cam,
                          double* ws, uint32_t* ticket, void* stream);
+
+/* ABI v19.  The camera gradients of bundle adjustment (Mapper.py:346-363, 441-448, 503): n_cams
+ * cameras, camera k's rays being rays [ray_begin[k], ray_begin[k] + n_rays_per) of the batch (one frame
+ * of the mapping window each).  cams [n_cams][7] and g_cam [n_cams][7] contiguous f32; c2w: camera k's
+ * pose rendered with at c2w + k * c2w_stride floats ([3,4] row-major rows of 4); g_pts as in
+ * nslam_cam_grad_parts (1..4 buffers over the whole batch, summed per point in buffer order), z_vals /
+ * rays_d over the whole batch.  ray_begin: HOST array.  One launch, up to 32 workgroups per camera;
+ * ws: n_cams * NSLAM_CAM_GRAD_WS_DOUBLES doubles; tickets: n_cams device uint32 zeroed once (re-armed by
+ * the call).  Per camera the arithmetic and order are nslam_cam_grad_parts' over its slice: the same
+ * values bit for bit. */
+int nslam_cam_grad_batch(const float* cams, const float* c2w, int64_t c2w_stride, int32_t n_cams,
+                         const int64_t* ray_begin, int64_t n_rays_per, const double* const* g_pts, int32_t n_parts,
+                         const double* z_vals, const float* rays_d, int64_t n_rays, int32_t n_samples, float* g_cam,
+                         double* ws, uint32_t* tickets, void* stream);
+/* ABI v19: nslam_cam_pose for n cameras in one launch: c2w + k * c2w_stride = get_camera_from_tensor(cams[k]). */
+int nslam_cam_pose_batch(const float* cams, float* c2w, int64_t c2w_stride, int32_t n, void* stream);
 
 /* ABI v9.  c2w [3,4] f32 = get_camera_from_tensor(cam [7]) (common.py:137-176, quad2rotation's
  * products and differences, no FMA contraction), one thread.  |q|² is summed ((w²+x²)+y²)+z²;

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NSLAM_LIB") or os.path.join(_HERE, "libnslam.so")  # NSLAM_LIB: instrumented builds
 
 NSLAM_OK = 0
-ABI_VERSION = 18
+ABI_VERSION = 19
 STAGES = {"coarse": 0, "middle": 1, "fine": 2, "color": 3}
 DEC_COARSE, DEC_MIDDLE, DEC_FINE, DEC_COLOR = 0, 1, 2, 3
 
@@ -103,6 +103,7 @@ class NslamAdamSeg(ctypes.Structure):
         ("pad_", ctypes.c_int32),
         ("mirror_idx", ctypes.c_void_p),  # ABI v7: packed-copy slots [n][2] of a dense segment
         ("mirror", ctypes.c_void_p),
+        ("n_live", ctypes.c_void_p),  # ABI v19: device int64 live count (NULL = n)
     ]
 
 
@@ -115,7 +116,8 @@ EXPORTS = (
     "nslam_workspace_size", "nslam_strerror", "nslam_abi_version", "nslam_gather_rays", "nslam_render_loss",
     "nslam_render_loss_workspace_size", "nslam_adam_step", "nslam_rows_pack", "nslam_rows_unpack",
     "nslam_query_fwd_ws", "nslam_query_fwd_workspace_size", "nslam_cam_grad", "nslam_cam_pose",
-    "nslam_query_tape_size", "nslam_color_wgrad", "nslam_cam_grad_parts",
+    "nslam_query_tape_size", "nslam_color_wgrad", "nslam_cam_grad_parts", "nslam_cam_grad_batch",
+    "nslam_cam_pose_batch",
 )
 
 _lib = None
@@ -177,6 +179,9 @@ def lib():
         L.nslam_cam_grad.argtypes = [vp, vp, vp, vp, vp, i64, i32, vp, vp]
         L.nslam_cam_grad_parts.argtypes = [vp, vp, ctypes.POINTER(vp), i32, vp, vp, i64, i32, vp, vp, vp, vp]
         L.nslam_cam_pose.argtypes = [vp, vp, vp]
+        L.nslam_cam_grad_batch.argtypes = [vp, vp, i64, i32, ctypes.POINTER(i64), i64, ctypes.POINTER(vp), i32, vp, vp,
+                                           i64, i32, vp, vp, vp, vp]
+        L.nslam_cam_pose_batch.argtypes = [vp, vp, i64, i32, vp]
         if L.nslam_abi_version() != ABI_VERSION:
             raise RuntimeError(f"libnslam.so ABI {L.nslam_abi_version()} != {ABI_VERSION}: rebuild it")
         _lib = L

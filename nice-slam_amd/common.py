@@ -123,6 +123,34 @@ def get_tensor_from_camera(RT, Tquad=False):
     return out.to(dev) if dev is not None else out
 
 
+def camera_tensors(RT):
+    """get_tensor_from_camera for a batch of poses [B, 3|4, 4] on their device, without a host round trip:
+    the same branch rule and float64 arithmetic as get_tensor_from_camera (rotation → quaternion
+    (w,x,y,z) normalised, w >= 0, then T), as float32 [B, 7]."""
+    M = RT.detach().to(torch.float64)
+    R, T = M[:, :3, :3], M[:, :3, 3]
+    r00, r01, r02 = R[:, 0, 0], R[:, 0, 1], R[:, 0, 2]
+    r10, r11, r12 = R[:, 1, 0], R[:, 1, 1], R[:, 1, 2]
+    r20, r21, r22 = R[:, 2, 0], R[:, 2, 1], R[:, 2, 2]
+    tr = r00 + r11 + r22
+    cands = []
+    s = 2.0 * torch.sqrt((tr + 1.0).clamp_min(0))
+    cands.append(torch.stack([0.25 * s, (r21 - r12) / s, (r02 - r20) / s, (r10 - r01) / s], -1))
+    s = 2.0 * torch.sqrt((1.0 + r00 - r11 - r22).clamp_min(0))
+    cands.append(torch.stack([(r21 - r12) / s, 0.25 * s, (r01 + r10) / s, (r02 + r20) / s], -1))
+    s = 2.0 * torch.sqrt((1.0 + r11 - r00 - r22).clamp_min(0))
+    cands.append(torch.stack([(r02 - r20) / s, (r01 + r10) / s, 0.25 * s, (r12 + r21) / s], -1))
+    s = 2.0 * torch.sqrt((1.0 + r22 - r00 - r11).clamp_min(0))
+    cands.append(torch.stack([(r10 - r01) / s, (r02 + r20) / s, (r12 + r21) / s, 0.25 * s], -1))
+    c0 = (tr > 0)[:, None]
+    c1 = ((r00 > r11) & (r00 > r22))[:, None]
+    c2 = (r11 > r22)[:, None]
+    q = torch.where(c0, cands[0], torch.where(c1, cands[1], torch.where(c2, cands[2], cands[3])))
+    q = q / torch.sqrt((q * q).sum(-1, keepdim=True))
+    q = torch.where(q[:, :1] < 0, -q, q)
+    return torch.cat([q, T], -1).float()
+
+
 def raw2outputs_nerf_color(raw, z_vals, rays_d, occupancy=False, device="cuda:0"):
     """src/common.py:204-245 → (depth, var, rgb, weights); occupancy mode on the HIP kernel.
 

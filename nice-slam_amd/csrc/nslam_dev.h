@@ -543,6 +543,8 @@ template <int R, class CoefFn>
 __device__ __forceinline__ void adam_segment_block(const nslam_adam_seg& sg, const CoefFn& coef, int64_t lb,
                                                    int zero_grad, int tid, int nthreads) {
   typedef float f4 __attribute__((ext_vector_type(4)));
+  // ABI v19: a segment sized for a capacity may carry its live row / element count on the device
+  const int64_t n_seg = sg.n_live ? (*sg.n_live < sg.n ? *sg.n_live : sg.n) : sg.n;
   if (!sg.rows) {
     int64_t e[R];
     float p[R], m[R], v[R], g[R];
@@ -550,7 +552,7 @@ __device__ __forceinline__ void adam_segment_block(const nslam_adam_seg& sg, con
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       e[k] = (lb * R + k) * nthreads + tid;
-      if (e[k] < sg.n) {
+      if (e[k] < n_seg) {
         p[k] = sg.param[e[k]];
         m[k] = sg.exp_avg[e[k]];
         v[k] = sg.exp_avg_sq[e[k]];
@@ -563,7 +565,7 @@ __device__ __forceinline__ void adam_segment_block(const nslam_adam_seg& sg, con
     const AdamCoef c = coef();
 #pragma unroll
     for (int k = 0; k < R; ++k) {
-      if (e[k] >= sg.n) continue;
+      if (e[k] >= n_seg) continue;
       adam_one(p[k], g[k], m[k], v[k], c);
       sg.param[e[k]] = p[k];
       sg.exp_avg[e[k]] = m[k];
@@ -586,7 +588,7 @@ __device__ __forceinline__ void adam_segment_block(const nslam_adam_seg& sg, con
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       ri[k] = (lb * R + k) * rows_per_block + tid / q;
-      ok[k] = lane_ok && ri[k] < sg.n;
+      ok[k] = lane_ok && ri[k] < n_seg;
       any |= ok[k];
     }
     if (!any) return;

@@ -482,12 +482,14 @@ struct CamPartsArgs {
   uint32_t* ticket;
 };
 
-__global__ __launch_bounds__(kCamThreads) void k_cam_grad_parts(CamPartsArgs a) {
+// workgroup wg of nwg of one camera's gradient (k_cam_grad_parts: the whole grid; k_cam_grad_batch: the
+// x extent of the grid row of camera blockIdx.y)
+__device__ __forceinline__ void cam_grad_parts_body(const CamPartsArgs& a, unsigned wg, unsigned nwg) {
   double acc[12];
 #pragma unroll
   for (int k = 0; k < 12; ++k) acc[k] = 0.0;
   const int np = (int)(a.n * a.S);
-  for (int p = blockIdx.x * kCamThreads + threadIdx.x; p < np; p += gridDim.x * kCamThreads) {
+  for (int p = wg * kCamThreads + threadIdx.x; p < np; p += nwg * kCamThreads) {
     const int r = p / a.S;
     const double zs = a.z[p];
     double g[3];
@@ -520,7 +522,7 @@ __global__ __launch_bounds__(kCamThreads) void k_cam_grad_parts(CamPartsArgs a) 
   if (threadIdx.x < 12) {  // fixed-order sum over the waves, published as this workgroup's partial
     double t = 0.0;
     for (int w = 0; w < kCamThreads / 64; ++w) t += red[threadIdx.x][w];
-    a.ws[blockIdx.x * 12 + threadIdx.x] = t;
+    a.ws[wg * 12 + threadIdx.x] = t;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -528,7 +530,7 @@ __global__ __launch_bounds__(kCamThreads) void k_cam_grad_parts(CamPartsArgs a) 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t tk = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    red[0][0] = tk == gridDim.x - 1 ? 1.0 : 0.0;  // "I am last", through the one LDS array
+    red[0][0] = tk == nwg - 1 ? 1.0 : 0.0;  // "I am last", through the one LDS array
   }
   __syncthreads();
   if (red[0][0] == 0.0) return;
@@ -540,12 +542,54 @@ __global__ __launch_bounds__(kCamThreads) void k_cam_grad_parts(CamPartsArgs a) 
   __syncthreads();
   double t = 0.0;
   if (threadIdx.x < 12)  // the workgroups' partials in workgroup order: deterministic
-    for (unsigned w = 0; w < gridDim.x; ++w) t += a.ws[w * 12 + threadIdx.x];
+    for (unsigned w = 0; w < nwg; ++w) t += a.ws[w * 12 + threadIdx.x];
   __syncthreads();
   if (threadIdx.x < 12) red[threadIdx.x][0] = t;
   __syncthreads();
   if (threadIdx.x != 0) return;
   cam_grad_epilogue(a.cam, a.c2w, red, a.g_cam);
+}
+
+__global__ __launch_bounds__(kCamThreads) void k_cam_grad_parts(CamPartsArgs a) { cam_grad_parts_body(a, blockIdx.x, gridDim.x); }
+
+// ABI v19: every bundle-adjustment camera of the window in one launch (grid row blockIdx.y = camera)
+struct CamBatchArgs {
+  const float* cams;
+  const float* c2w;
+  int64_t c2w_stride;
+  int64_t r0[NSLAM_MAX_FRAMES];  // first ray of each camera's slice
+  int64_t n_per;
+  const double* gp[4];
+  int32_t nbuf;
+  const double* z;
+  const float* rd;
+  int32_t S;
+  float* g_cam;
+  double* ws;
+  uint32_t* tickets;
+};
+
+__global__ __launch_bounds__(kCamThreads) void k_cam_grad_batch(CamBatchArgs b) {
+  const int k = (int)blockIdx.y;
+  int64_t r0 = 0;
+#pragma unroll
+  for (int i = 0; i < NSLAM_MAX_FRAMES; ++i)  // selects, not a dynamic index into the by-value argument
+    if (i == k) r0 = b.r0[i];
+  CamPartsArgs a{};
+  a.cam = b.cams + 7 * k;
+  a.c2w = b.c2w + b.c2w_stride * k;
+  const int64_t p0 = r0 * b.S;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a.gp[i] = i < b.nbuf ? b.gp[i] + p0 * 3 : nullptr;
+  a.nbuf = b.nbuf;
+  a.z = b.z + p0;
+  a.rd = b.rd + r0 * 3;
+  a.n = b.n_per;
+  a.S = b.S;
+  a.g_cam = b.g_cam + 7 * k;
+  a.ws = b.ws + (int64_t)k * kCamParts * 12;
+  a.ticket = b.tickets + k;
+  cam_grad_parts_body(a, blockIdx.x, gridDim.x);
 }
 
 }  // namespace
@@ -591,10 +635,47 @@ extern "C" int nslam_cam_grad_parts(const float* cam, const float* c2w, const do
   return e == hipSuccess ? NSLAM_OK : NSLAM_EHIP - (int)e;
 }
 
+extern "C" int nslam_cam_grad_batch(const float* cams, const float* c2w, int64_t c2w_stride, int32_t n_cams,
+                                    const int64_t* ray_begin, int64_t n_rays_per, const double* const* g_pts,
+                                    int32_t n_parts, const double* z_vals, const float* rays_d, int64_t n_rays,
+                                    int32_t n_samples, float* g_cam, double* ws, uint32_t* tickets, void* stream) {
+  if (!cams || !c2w || !g_cam || !ws || !tickets || !ray_begin || n_cams < 1 || n_cams > NSLAM_MAX_FRAMES)
+    return NSLAM_EINVAL;
+  if (c2w_stride < 12 || n_rays_per < 0 || n_rays < 0 || n_samples <= 0) return NSLAM_EINVAL;
+  if (n_parts < 1 || n_parts > 4 || !g_pts) return NSLAM_EINVAL;
+  if (n_rays > 0 && (!z_vals || !rays_d)) return NSLAM_EINVAL;
+  for (int b = 0; b < n_parts; ++b)
+    if (!g_pts[b]) return NSLAM_EINVAL;
+  // every slice inside the batch (the kernel reads exactly [ray_begin, ray_begin + n_rays_per) of it)
+  for (int k = 0; k < n_cams; ++k)
+    if (ray_begin[k] < 0 || ray_begin[k] + n_rays_per > n_rays) return NSLAM_EINVAL;
+  if (n_rays * (int64_t)n_samples * 3 >= (int64_t(1) << 31)) return NSLAM_EUNSUPPORTED;
+  CamBatchArgs b{};
+  b.cams = cams;
+  b.c2w = c2w;
+  b.c2w_stride = c2w_stride;
+  for (int k = 0; k < n_cams; ++k) b.r0[k] = ray_begin[k];
+  b.n_per = n_rays_per;
+  for (int i = 0; i < n_parts; ++i) b.gp[i] = g_pts[i];
+  b.nbuf = n_parts;
+  b.z = z_vals;
+  b.rd = rays_d;
+  b.S = n_samples;
+  b.g_cam = g_cam;
+  b.ws = ws;
+  b.tickets = tickets;
+  const int64_t np = n_rays_per * (int64_t)n_samples;
+  int64_t wg = (np + kCamThreads - 1) / kCamThreads;
+  wg = wg < 1 ? 1 : (wg > kCamParts ? kCamParts : wg);
+  hipLaunchKernelGGL(k_cam_grad_batch, dim3((unsigned)wg, (unsigned)n_cams), dim3(kCamThreads), 0,
+                     reinterpret_cast<hipStream_t>(stream), b);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? NSLAM_OK : NSLAM_EHIP - (int)e;
+}
+
 namespace {
 
-__global__ __launch_bounds__(64) void k_cam_pose(const float* __restrict__ cam, float* __restrict__ c2w) {
-  if (threadIdx.x != 0) return;
+__device__ __forceinline__ void cam_pose_one(const float* __restrict__ cam, float* __restrict__ c2w) {
   const float qr = cam[0], qi = cam[1], qj = cam[2], qk = cam[3];
   const float two_s = 2.0f / (((qr * qr + qi * qi) + qj * qj) + qk * qk);
   const float R[9] = {1.0f - two_s * (qj * qj + qk * qk), two_s * (qi * qj - qk * qr), two_s * (qi * qk + qj * qr),
@@ -606,11 +687,28 @@ __global__ __launch_bounds__(64) void k_cam_pose(const float* __restrict__ cam, 
   }
 }
 
+__global__ __launch_bounds__(64) void k_cam_pose(const float* __restrict__ cam, float* __restrict__ c2w) {
+  if (threadIdx.x == 0) cam_pose_one(cam, c2w);
+}
+
+__global__ __launch_bounds__(64) void k_cam_pose_batch(const float* __restrict__ cams, float* __restrict__ c2w,
+                                                       int64_t stride, int n) {
+  if ((int)threadIdx.x < n) cam_pose_one(cams + 7 * threadIdx.x, c2w + stride * threadIdx.x);
+}
+
 }  // namespace
 
 extern "C" int nslam_cam_pose(const float* cam, float* c2w, void* stream) {
   if (!cam || !c2w) return NSLAM_EINVAL;
   hipLaunchKernelGGL(k_cam_pose, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), cam, c2w);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? NSLAM_OK : NSLAM_EHIP - (int)e;
+}
+
+extern "C" int nslam_cam_pose_batch(const float* cams, float* c2w, int64_t c2w_stride, int32_t n, void* stream) {
+  if (!cams || !c2w || n < 1 || n > 64 || c2w_stride < 12) return NSLAM_EINVAL;
+  hipLaunchKernelGGL(k_cam_pose_batch, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), cams, c2w,
+                     c2w_stride, (int)n);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? NSLAM_OK : NSLAM_EHIP - (int)e;
 }

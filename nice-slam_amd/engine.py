@@ -198,6 +198,54 @@ class MappingEngine:
             self.ggrad_pad[k] = self.gbuf[off:off + sizes[k]]
             off += sizes[k]
 
+    def bind_masks(self, masks):
+        """Per-call frustum selection on the device, without a host read-back and without moving any
+        buffer (Mapper.optimize_map's fused path: Mapper.py:314-333 each call).
+
+        masks: {grid key: bool [X, Y, Z] (mapper.frustum_mask) or None = every voxel}.  On the first call
+        (or a new key set) every listed grid gets a compact gradient sized for its CAPACITY (all of its
+        voxels) plus a persistent row list, slot map and live row count; every call then rewrites those
+        three in place from the masks (a cumsum compaction).  Adam segments carry the live count (ABI v19
+        nslam_adam_seg.n_live, FusedAdam group "n_live"), so nothing an iteration launches depends on the
+        selection's size: a hipGraph captured for one call replays for the next.  The compact gradients
+        stay zero between iterations (the backward writes only live rows, Adam zeroes every row it reads).
+        Returns {grid key: live row count (device int64 [1])}."""
+        keys = tuple(sorted(masks))
+        if getattr(self, "_cap_keys", None) != keys:
+            self._cap = {}
+            rows = {}
+            for k in keys:
+                n = self.c[k].numel() // 32
+                full = torch.empty(n + 1, dtype=torch.int32, device=self.device)  # [n]: the dummy target
+                full[:n] = torch.arange(n, dtype=torch.int32, device=self.device)
+                self._cap[k] = (full, torch.full((1,), n, dtype=torch.int64, device=self.device),
+                                torch.arange(n, dtype=torch.int32, device=self.device))
+                rows[k] = full[:n]
+            self.set_rows(rows, pad_rows=1)
+            self._cap_keys = keys
+            self.gall.zero_()
+            self._clean = True
+        for k in keys:
+            full, n_live, ar = self._cap[k]
+            n = ar.numel()
+            m = masks[k]
+            if m is None:
+                full[:n].copy_(ar)
+                self.slot[k].copy_(ar)
+                n_live.fill_(n)
+                continue
+            m = m.permute(2, 1, 0).reshape(-1)  # [X, Y, Z] -> channels-last voxel order z*Y*X + y*X + x
+            idx = torch.cumsum(m, 0, dtype=torch.int32) - 1
+            self.slot[k].copy_(torch.where(m, idx, torch.full_like(idx, -1)))
+            full.scatter_(0, torch.where(m, idx, torch.full_like(idx, n)).long(), ar)
+            n_live.copy_(idx[-1:].to(torch.int64) + 1)
+        return {k: self._cap[k][1] for k in keys}
+
+    def live_rows(self, key):
+        """(row list, live count) of a grid bound by bind_masks: the FusedAdam group's "rows" / "n_live"."""
+        full, n_live, ar = self._cap[key]
+        return full[:ar.numel()], n_live
+
     # -- query in ray form ---------------------------------------------------------------------
     def _cfg(self, stage, ro, rd, z, grid_grads, dec_grads):
         decs = ops._DEC_FOR_STAGE[stage]
@@ -385,6 +433,13 @@ class MappingEngine:
         return out
 
     # -- one iteration ---------------------------------------------------------------------------
+    def draws(self, seed, world=1, rank=0):
+        """The in-kernel pixel draws (ops.PixelDraws) of stream `seed`, made on first use."""
+        key = (seed, world, rank)
+        if self._draws is None or self._draws[0] != key:
+            self._draws = (key, ops.PixelDraws(seed, self.device, world, rank, with_max=world > 1))
+        return self._draws[1]
+
     def grads_for(self, stage, trainable_decoders):
         """(grid keys, decoder names) that receive gradients in `stage` (Mapper.py:335-341)."""
         decs = ops._DEC_FOR_STAGE[stage]
@@ -400,7 +455,7 @@ class MappingEngine:
 
     def iteration(self, stage, frames, pix, n_per, hw, intrinsics, optimizer, trainable_decoders=("color",),
                   gt_max=None, allreduce=None, use_gt_in_sampler=True, exchange=None, n_kept=None, seed=0,
-                  world=1, rank=0, prefetch=False):
+                  world=1, rank=0, prefetch=False, post_bwd=None):
         """One mapping iteration; returns (ray_loss f64 [N], keep uint8 [N]) as device tensors.
 
         frames: [(depth, color, c2w)] of the window; pix: int64 [len(frames)*n_per] randint
@@ -424,18 +479,18 @@ class MappingEngine:
         by bundle adjustment — tracked by the tensors' identity and version counters) discards it
         and draws its own batch.  With prefetch the returned `keep` is a persistent buffer, valid
         until the next iteration() call (which overwrites it): clone it to keep it longer.
+        post_bwd(g_pts parts, rays_o, rays_d, z): the backward also forms d loss / d pts (every decoder's
+        share, a list of [N*S, 3] float64) and this runs on the main stream once the whole backward is
+        done, before the main-stream Adam — bundle adjustment's camera gradients and camera step
+        (Mapper.py:346-363, 503-504).  Camera poses that change in place make prefetch invalid: pass
+        prefetch=False with it.
         """
         H, W = hw
         fx, fy, cx, cy = intrinsics
         keys, dnames = self.grads_for(stage, trainable_decoders)
         if exchange is not None and hasattr(exchange, "validate"):
             exchange.validate(self, keys, dnames)  # raises before anything of the iteration is enqueued
-        draw = None
-        if pix is None:
-            key = (seed, world, rank)
-            if self._draws is None or self._draws[0] != key:
-                self._draws = (key, ops.PixelDraws(seed, self.device, world, rank, with_max=world > 1))
-            draw = self._draws[1]
+        draw = self.draws(seed, world, rank) if pix is None else None
 
         def rays(out=None):  # pixels → rays + inside mask, then the sampler (Mapper.py:457-484, Renderer.py:82-174)
             ro, rd, gd, gc, keep = ops.gather_rays(frames, pix, n_per, H, W, (0, H, 0, W), fx, fy, cx, cy,
@@ -452,7 +507,7 @@ class MappingEngine:
                              out=None if out is None else out[5])
             return [ro, rd, gd, gc, keep, z]
 
-        prefetch = prefetch and pix is None
+        prefetch = prefetch and pix is None and post_bwd is None
         side = None
         if prefetch:
             # A prefetched batch is only valid for the very frames (images and poses, unmodified) it was
@@ -532,7 +587,8 @@ class MappingEngine:
                 if sub:
                     optimizer.step(grads=sub, zero_grad=clean)
 
-        self.query_bwd(stage, ro, rd, z, g_raw, keys, dnames, on_branch=on_branch, ordered_branches=sharded)
+        gps = self.query_bwd(stage, ro, rd, z, g_raw, keys, dnames, on_branch=on_branch, ordered_branches=sharded,
+                             pts_grad=post_bwd is not None, pts_parts=True)
         if sharded:
             pass
         elif exchange is not None:  # frustum-compacted all-reduce (distributed.SparseGradExchange)
@@ -541,6 +597,8 @@ class MappingEngine:
             allreduce([self.gbuf] + [self.decs[n].grad for n in dnames])
         if side is not None:  # join: the next call reads the prefetched set
             main.wait_stream(side)
+        if post_bwd is not None:
+            post_bwd(gps if isinstance(gps, list) else [gps], ro, rd, z)
         if on_branch is None:
             optimizer.step(grads=grads, zero_grad=clean)
         self._clean = clean and (not sharded or exchange.leaves_clean)
@@ -611,17 +669,20 @@ class TrackingEngine:
         h0, h1, w0, w1 = self.window
         return (h1 - h0) * (w1 - w0)
 
-    def iteration(self, cam, depth, color, pix, optimizer):
+    def iteration(self, cam, depth, color, pix, optimizer, n=None, seed=0):
         """One camera iteration on frame (depth [H,W], color [H,W,3]) with pixel draws `pix`
-        (int64 [n], select_uv indices into the edge-cropped window).  cam: [7] leaf tensor whose
-        .grad the optimizer reads.  Returns the loss (device f64 scalar) of the pose BEFORE the step."""
+        (int64 [n], select_uv indices into the edge-cropped window), or pix=None: n pixels drawn inside
+        the gather kernel (uniform over the window, stream `seed`; capturable in a hipGraph).  cam: [7]
+        leaf tensor whose .grad the optimizer reads.  Returns the loss (device f64 scalar) of the pose
+        BEFORE the step."""
         fx, fy, cx, cy = self.intr
-        n = pix.numel()
+        n = pix.numel() if pix is not None else int(n)
+        draw = self.eng.draws(seed) if pix is None else None
         if self._c2w is None:
             self._c2w = torch.empty(3, 4, dtype=torch.float32, device=cam.device)
         c2w = ops.cam_pose(cam.detach(), self._c2w)  # get_camera_from_tensor in one launch
         ro, rd, gd, gc, keep = ops.gather_rays([(depth, color, c2w)], pix, n, self.H, self.W, self.window,
-                                               fx, fy, cx, cy, self.bound)
+                                               fx, fy, cx, cy, self.bound, draw=draw)
         z = ops.sample_z(ro, rd, gd, self.bound, self.n_strat, self.n_surf)
         # the fine + middle occupancy sum is formed by the loss kernel as it reads raw (no combine pass)
         raw = self.eng.query_fwd("color", ro, rd, z, defer_occ=True)

@@ -2,14 +2,26 @@
 
 `optimize_map` keeps the reference's signature and semantics (Mapper.py:230-540): staged
 middle → fine → colour schedule, Adam re-created per call, frustum-masked grid parameters,
-optional bundle adjustment of keyframe cameras.  Differences (none changes the maths):
+optional bundle adjustment of keyframe cameras.  It runs on the fused mapping engine
+(engine.MappingEngine: one gather / sampler / forward / loss / backward / Adam chain of HIP launches
+per iteration, no autograd) — `Mapper.fused = False` selects the autograd drop-in of the same loop.
+Differences from the reference (none changes the maths):
   * keyframe images stay resident on the device (the reference copies them host→device every
     iteration, Mapper.py:439-440);
   * the frustum voxel mask (Mapper.py:93-164) is computed with torch on the device; cv2.remap's
     bilinear lookup is emulated including its 1/32-pixel fixed-point positions and zero border
     (OpenCV is not installed: parity with cv2 itself is unpinned);
-  * decoder parameters that are not optimised get requires_grad=False for the call, so the
-    fused backward skips their (never used) weight gradients.
+  * the masked grid vectors are not copied in and out of the grids every iteration
+    (Mapper.py:394-401, 511-519): Adam updates the selected voxels in place, with state for them
+    alone — the same elementwise update; the optimiser's state is reset per call (a fresh Adam);
+  * the inside-mask prefilter (Mapper.py:469-481) gives dropped rays zero loss weight instead of
+    compacting them (their gradients are exactly zero; the sampler's batch max sees kept rays only);
+  * pixel draws: through common.select_uv (torch.randint, eager) when it is replaced (tests pin the
+    draws that way) or a generator is given; otherwise drawn inside the gather kernel (uniform over
+    the image like select_uv, a counter-based stream instead of torch's Philox) so that each stage's
+    iterations are captured ONCE in a hipGraph and replayed by every later call of the same shape
+    (the window's frames are copied into persistent slots, the frustum selection is bound on the
+    device with capacity-sized buffers: engine.MappingEngine.bind_masks).
 The mapping loop driver (Mapper.run, Mapper.py:542-657) is out of scope (dataset/meshing/ckpt glue).
 """
 from __future__ import annotations
@@ -17,7 +29,12 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from .common import get_camera_from_tensor, get_samples, get_tensor_from_camera, random_select
+from . import common as _common
+from . import ops
+from .common import camera_tensors, get_camera_from_tensor, get_samples, get_tensor_from_camera, random_select
+
+_SELECT_UV = _common.select_uv  # the product's own pixel selection (a replacement one forces eager draws)
+_STAGE_GROUPS = ("decoders", "coarse", "middle", "fine", "color")
 
 
 def _remap_bilinear(img, u, v):
@@ -107,6 +124,16 @@ class Mapper(object):
         self.generator = generator
         self.stage = "middle"
         self.loss_history = None  # set to [] to record per-iteration losses (detached, no host sync)
+        self.fused = True   # optimize_map on engine.MappingEngine (False: the autograd drop-in)
+        self.graphs = True  # fused path with device draws: each stage's iterations as one cached hipGraph
+        self._eng = None
+        self._fopt = None
+        self._cam = {}      # number of BA cameras -> (cams, grad, ws, tickets, FusedAdam)
+        self._slots = None  # (depth [F,H,W], color [F,H,W,3], c2w [F,4,4]) of the window
+        self._graphs = {}
+        # the device draws' stream key (from torch's CPU generator, so torch.manual_seed pins it)
+        self._draw_seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        self.calls = 0
 
     # ------------------------------------------------------------------------------------------
     def get_mask_from_c2w(self, c2w, key, val_shape, depth):
@@ -162,6 +189,241 @@ class Mapper(object):
     def optimize_map(self, num_joint_iters, lr_factor, idx, cur_gt_color, cur_gt_depth, gt_cur_c2w, keyframe_dict,
                      keyframe_list, cur_c2w):
         """Mapping iterations (Mapper.py:230-540); returns the BA-updated cur_c2w or None."""
+        self.calls += 1
+        if self.fused:
+            return self._optimize_map_fused(num_joint_iters, lr_factor, idx, cur_gt_color, cur_gt_depth, gt_cur_c2w,
+                                            keyframe_dict, keyframe_list, cur_c2w)
+        return self._optimize_map_autograd(num_joint_iters, lr_factor, idx, cur_gt_color, cur_gt_depth, gt_cur_c2w,
+                                           keyframe_dict, keyframe_list, cur_c2w)
+
+    # ------------------------------------------------------------------------------------------
+    def _select_window(self, keyframe_dict, keyframe_list, cur_gt_color, cur_gt_depth, cur_c2w):
+        """optimize_frame (keyframe ids, -1 = the current frame) and the oldest one (Mapper.py:256-272,
+        346-349)."""
+        if len(keyframe_dict) == 0:
+            optimize_frame = []
+        elif self.keyframe_selection_method == "global":
+            optimize_frame = random_select(len(self.keyframe_dict) - 1, self.mapping_window_size - 2)
+        else:
+            optimize_frame = self.keyframe_selection_overlap(cur_gt_color, cur_gt_depth, cur_c2w, keyframe_dict[:-1],
+                                                             self.mapping_window_size - 2)
+        oldest_frame = None
+        if len(keyframe_list) > 0:
+            optimize_frame = optimize_frame + [len(keyframe_list) - 1]
+            oldest_frame = min(optimize_frame)
+        optimize_frame += [-1]
+        return optimize_frame, oldest_frame
+
+    def _stage_of(self, joint_iter, num_joint_iters):
+        """Mapper.py:403-411."""
+        if self.coarse_mapper:
+            return "coarse"
+        if joint_iter <= int(num_joint_iters * self.middle_iter_ratio):
+            return "middle"
+        if joint_iter <= int(num_joint_iters * self.fine_iter_ratio):
+            return "fine"
+        return "color"
+
+    def _grid_keys(self):
+        return ["grid_coarse"] if self.coarse_mapper else [k for k in ("grid_middle", "grid_fine", "grid_color")
+                                                          if k in self.c]
+
+    def engine(self):
+        """The persistent MappingEngine over the shared grids and decoders (built on first use)."""
+        if self._eng is None:
+            from .engine import MappingEngine
+            c = {k: self.c[k] for k in self._grid_keys()}
+            r = self.renderer
+            self._eng = MappingEngine(self.decoders, c, self.bound, r.N_samples, r.N_surface, lindisp=r.lindisp,
+                                      w_color=self.w_color_loss, device=self.device)
+        return self._eng
+
+    def _trainable(self):
+        """Decoders in the optimiser's "decoders" group (Mapper.py:335-341)."""
+        return tuple(n for n, fixed in (("fine", self.fix_fine), ("color", self.fix_color)) if not fixed)
+
+    def _optimizer(self, eng):
+        """The persistent FusedAdam of the fused path: groups decoders / coarse / middle / fine / colour as
+        the reference's (Mapper.py:365-389); grid groups hold the frustum rows with their live count."""
+        if self._fopt is None:
+            dec = [eng.decs[n].param for n in self._trainable() if n in eng.decs]
+            groups = [{"params": dec, "lr": 0.0}]
+            for name in _STAGE_GROUPS[1:]:
+                k = "grid_" + name
+                if k in eng.c:
+                    rows, n_live = eng.live_rows(k)
+                    groups.append({"params": [eng.c[k]], "lr": 0.0, "rows": rows, "n_live": n_live})
+                else:
+                    groups.append({"params": [], "lr": 0.0})
+            self._fopt = ops.FusedAdam(groups)
+        return self._fopt
+
+    def _cam_state(self, n):
+        """Persistent BA camera buffers for n cameras: cams [n,7], their gradient, the camera-gradient
+        workspace / tickets, and their Adam (the reference's param group 5, Mapper.py:386-389)."""
+        if n not in self._cam:
+            dev = self.device
+            cams = torch.zeros(n, 7, dtype=torch.float32, device=dev)
+            grad = torch.zeros(n, 7, dtype=torch.float32, device=dev)
+            ws = torch.zeros(n * ops.CAM_GRAD_WS_DOUBLES, dtype=torch.float64, device=dev)
+            tickets = torch.zeros(n, dtype=torch.int32, device=dev)
+            self._cam[n] = (cams, grad, ws, tickets, ops.FusedAdam([{"params": [cams], "lr": 0.0}]))
+        return self._cam[n]
+
+    def _window_slots(self, F):
+        if self._slots is None or self._slots[0].shape[0] < F:
+            dev, H, W = self.device, self.H, self.W
+            n = max(F, self.mapping_window_size)
+            self._slots = (torch.zeros(n, H, W, dtype=torch.float32, device=dev),
+                           torch.zeros(n, H, W, 3, dtype=torch.float32, device=dev),
+                           torch.eye(4, dtype=torch.float32, device=dev).repeat(n, 1, 1))
+            self._graphs.clear()  # (captured against the old slots)
+        return self._slots
+
+    def _optimize_map_fused(self, num_joint_iters, lr_factor, idx, cur_gt_color, cur_gt_depth, gt_cur_c2w,
+                            keyframe_dict, keyframe_list, cur_c2w):
+        """optimize_map on the fused engine (see the module docstring)."""
+        dev = self.device
+        H, W = self.H, self.W
+        cur_gt_depth = cur_gt_depth.to(dev).float()
+        cur_gt_color = cur_gt_color.to(dev).float()
+        cur_c2w = cur_c2w.to(dev).float()
+        optimize_frame, oldest_frame = self._select_window(keyframe_dict, keyframe_list, cur_gt_color, cur_gt_depth,
+                                                           cur_c2w)
+        F = len(optimize_frame)
+        n_per = self.mapping_pixels // F
+        eng = self.engine()
+        for d in eng.decs.values():  # parameters may have been assigned since the last call
+            d.repack()
+        # window slots: the oldest frame (fixed under BA) first, then the others in optimize_frame order
+        order = list(optimize_frame)
+        if self.BA and oldest_frame is not None:
+            order.remove(oldest_frame)
+            order.insert(0, oldest_frame)
+        depth_s, color_s, c2w_s = self._window_slots(F)
+        for s, fr in enumerate(order):
+            if fr == -1:
+                d, c, m = cur_gt_depth, cur_gt_color, cur_c2w
+            else:
+                d, c = self._frame_images(keyframe_dict[fr])
+                m = keyframe_dict[fr]["est_c2w"].to(dev).float()
+            depth_s[s].copy_(d)
+            color_s[s].copy_(c)
+            c2w_s[s, :m.shape[0]].copy_(m)
+        frames = [(depth_s[s], color_s[s], c2w_s[s]) for s in range(F)]
+        c0 = 1 if (self.BA and oldest_frame is not None) else 0
+        ncam = (F - c0) if self.BA else 0
+        # frustum selection of this call (Mapper.py:314-333), bound on the device
+        keys = self._grid_keys()
+        masks = {k: (self.get_mask_from_c2w(cur_c2w, k, self.c[k].shape[2:], cur_gt_depth)
+                     if self.frustum_feature_selection else None) for k in keys}
+        eng.bind_masks(masks)
+        opt = self._optimizer(eng)
+        cam = None
+        if ncam:  # the 7-vectors of the optimised frames (Mapper.py:349-363)
+            cams, cgrad, cws, ctk, copt = cam = self._cam_state(ncam)
+            cams0 = camera_tensors(c2w_s[c0:F])
+            cams.copy_(cams0)
+
+        def post_bwd(gps, ro, rd, z):  # BA: camera gradients of every optimised frame, then their Adam step
+            ops.cam_grad_batch(cams, c2w_s[c0:F], [(c0 + k) * n_per for k in range(ncam)], n_per, gps, z, rd, cgrad,
+                               cws, ctk)
+            copt.step(grads={cams: cgrad})
+
+        device_draws = _common.select_uv is _SELECT_UV and self.generator is None
+        intr = (self.fx, self.fy, self.cx, self.cy)
+        tdec = self._trainable()
+        ar = torch.arange(H * W, device=dev) if not device_draws else None
+
+        def iteration(stage, record=None):
+            if ncam:
+                ops.cam_pose_batch(cams, c2w_s[c0:F])  # get_camera_from_tensor of every BA camera
+            pix = None
+            if not device_draws:  # select_uv per frame, in optimize_frame order (Mapper.py:437-467)
+                pix = torch.empty(F * n_per, dtype=torch.int64, device=dev)
+                for fr in optimize_frame:
+                    s = order.index(fr)
+                    pix[s * n_per:(s + 1) * n_per] = _common.select_uv(ar, ar, n_per, ar, ar.view(-1, 1).expand(-1, 3),
+                                                                       device=dev, generator=self.generator)[0]
+            ray_loss, _ = eng.iteration(stage, frames, pix, n_per, (H, W), intr, opt, trainable_decoders=tdec,
+                                        use_gt_in_sampler=not self.coarse_mapper, seed=self._draw_seed,
+                                        post_bwd=post_bwd if ncam else None)
+            if record is not None:
+                record(ray_loss)
+
+        def set_lr(stage, zero=False):
+            st = self.cfg["mapping"]["stage"][stage]
+            for gi, name in enumerate(_STAGE_GROUPS):
+                opt.param_groups[gi]["lr"] = 0.0 if zero else st[name + "_lr"] * lr_factor
+            if cam is not None:
+                copt.param_groups[0]["lr"] = self.BA_cam_lr if (stage == "color" and not zero) else 0.0
+
+        # the call's schedule as runs of one stage (Mapper.py:403-421)
+        runs = []
+        for it in range(num_joint_iters):
+            stg = self._stage_of(it, num_joint_iters)
+            if runs and runs[-1][0] == stg:
+                runs[-1][1] += 1
+            else:
+                runs.append([stg, 1])
+        hist = self.loss_history
+        use_graphs = self.graphs and device_draws
+        plan = []
+        if use_graphs:
+            # the warm-up iterations below draw pixels too: the draw stream is rewound afterwards, so a call
+            # draws the same pixels whether its graphs were cached or just captured (and as the eager path)
+            ctr = eng.draws(self._draw_seed).counter
+            ctr0 = ctr.clone()
+            for stg, n in runs:
+                key = (stg, n, F, n_per, c0, ncam, float(lr_factor), hist is not None, tdec)
+                if key not in self._graphs:
+                    # one zero-lr eager iteration (the maps do not move; lazily made streams, events, tickets
+                    # and draw counters exist before capture), then the capture itself (nothing runs)
+                    set_lr(stg, zero=True)
+                    iteration(stg)
+                    set_lr(stg)
+                    losses = torch.zeros(n, dtype=torch.float64, device=dev) if hist is not None else None
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                        for i in range(n):
+                            iteration(stg, None if losses is None else (lambda rl, i=i: losses[i].copy_(rl.sum())))
+                    self._graphs[key] = (g, losses)
+                plan.append((stg, n, self._graphs[key]))
+            ctr.copy_(ctr0)
+        # a fresh Adam for this call (Mapper.py:365-389): zero moments and step counts
+        opt.reset_state()
+        if cam is not None:
+            copt.reset_state()
+            cams.copy_(cams0)
+        if use_graphs:
+            for stg, n, (g, losses) in plan:
+                self.stage = stg
+                g.replay()
+                if hist is not None:
+                    hist.extend(losses.clone().unbind())
+        else:
+            for stg, n in runs:
+                self.stage = stg
+                set_lr(stg)
+                for _ in range(n):
+                    iteration(stg, None if hist is None else (lambda rl: hist.append(rl.sum())))
+        if not ncam:
+            return None
+        # BA write-back (Mapper.py:521-540): the optimised poses of the keyframes and the current frame
+        bottom = torch.tensor([[0, 0, 0, 1.0]], dtype=torch.float32, device=dev)
+        out = ops.cam_pose_batch(cams.detach().clone(), torch.empty(ncam, 3, 4, dtype=torch.float32, device=dev))
+        for k in range(ncam):
+            fr = order[c0 + k]
+            c2w = torch.cat([out[k], bottom], 0)
+            if fr == -1:
+                cur_c2w = c2w
+            else:
+                keyframe_dict[fr]["est_c2w"] = c2w.clone()
+        return cur_c2w
+
+    def _optimize_map_autograd(self, num_joint_iters, lr_factor, idx, cur_gt_color, cur_gt_depth, gt_cur_c2w,
+                               keyframe_dict, keyframe_list, cur_c2w):
+        """The autograd drop-in of optimize_map (Mapper.py:230-540 line for line, HIP ops under autograd)."""
         H, W, fx, fy, cx, cy = self.H, self.W, self.fx, self.fy, self.cx, self.cy
         c, cfg, device = self.c, self.cfg, self.device
         bottom = torch.tensor([[0, 0, 0, 1.0]], dtype=torch.float32, device=device)

@@ -674,6 +674,47 @@ def cam_grad_parts(cam, c2w, g_pts, z, rd, out, ws, ticket):
     return out
 
 
+CAM_GRAD_WS_DOUBLES = 32 * 12  # NSLAM_CAM_GRAD_WS_DOUBLES
+
+
+def cam_pose_batch(cams, c2w):
+    """nslam_cam_pose_batch (ABI v19): c2w[k, :3, :4] = get_camera_from_tensor(cams[k]) for cams [n, 7] f32
+    and c2w [n, 3 or 4, 4] f32 (both contiguous), one launch."""
+    n = cams.shape[0]
+    if cams.dtype != torch.float32 or cams.dim() != 2 or cams.shape[1] != 7 or not cams.is_contiguous():
+        raise ValueError("cam_pose_batch: cams must be a contiguous float32 [n, 7]")
+    if (c2w.dtype != torch.float32 or c2w.dim() != 3 or c2w.shape[0] != n or c2w.shape[1] not in (3, 4)
+            or c2w.shape[2] != 4 or not c2w.is_contiguous()):
+        raise ValueError("cam_pose_batch: c2w must be a contiguous float32 [n, 3|4, 4]")
+    with _span("cam_pose"):
+        rc = lib().nslam_cam_pose_batch(ptr(cams), ptr(c2w), c2w.shape[1] * 4, n, stream_ptr(cams.device))
+    check(rc, "nslam_cam_pose_batch")
+    return c2w
+
+
+def cam_grad_batch(cams, c2w, ray_begin, n_per, g_pts, z, rd, out, ws, tickets):
+    """nslam_cam_grad_batch (ABI v19): out [n, 7] = d loss / d cams [n, 7] of the bundle-adjustment cameras,
+    camera k's rays being [ray_begin[k], ray_begin[k] + n_per) of the batch (z [N, S] f64, rd [N, 3] f32,
+    g_pts: list of [N*S, 3] f64 d/dpts shares); c2w [n, 3|4, 4] the poses rendered with; ws f64
+    [n * 384], tickets int32 [n] zeroed once (persistent per caller)."""
+    n = cams.shape[0]
+    N, S = z.shape
+    for t, dt, shp in ((cams, torch.float32, (n, 7)), (z, torch.float64, (N, S)), (rd, torch.float32, (N, 3)),
+                       (out, torch.float32, (n, 7)), (ws, torch.float64, (n * CAM_GRAD_WS_DOUBLES,)),
+                       (tickets, torch.int32, (n,))) + tuple((g, torch.float64, (N * S, 3)) for g in g_pts):
+        if t.dtype != dt or tuple(t.shape) != shp or not t.is_contiguous():
+            raise ValueError(f"cam_grad_batch: expected contiguous {dt} {shp}, got {t.dtype} {tuple(t.shape)}")
+    if c2w.dtype != torch.float32 or c2w.dim() != 3 or c2w.shape[0] != n or not c2w.is_contiguous():
+        raise ValueError("cam_grad_batch: c2w must be a contiguous float32 [n, 3|4, 4]")
+    rb = (ctypes.c_int64 * n)(*[int(r) for r in ray_begin])
+    bufs = (ctypes.c_void_p * len(g_pts))(*[ptr(g) for g in g_pts])
+    with _span("cam_grad"):
+        rc = lib().nslam_cam_grad_batch(ptr(cams), ptr(c2w), c2w.shape[1] * 4, n, rb, int(n_per), bufs, len(g_pts),
+                                        ptr(z), ptr(rd), N, S, ptr(out), ptr(ws), ptr(tickets), stream_ptr(cams.device))
+    check(rc, "nslam_cam_grad_batch")
+    return out
+
+
 def render_loss(raw, z, gt_depth, gt_color, keep=None, mode="mapper", use_color=True, handle_dynamic=False,
                 w_color=0.2, want_grad=True, occ_add=None):
     """Mapper/Tracker rendering loss fused with compositing and its backward (see nslam.h).
@@ -797,6 +838,8 @@ class FusedAdam:
                         raise ValueError("row-masked Adam needs channels-last grid and grad")
                     s.rows, s.n, s.row_len = ptr(rows), rows.numel(), p.shape[1]
                     s.grad_rows = int(compact)
+                    if g.get("n_live") is not None:  # ABI v19: rows sized for a capacity, live count on the device
+                        s.n_live = ptr(g["n_live"])
                 else:  # elementwise over storage: any dense layout shared by param, grad and state
                     dense = p.is_contiguous() or p.is_contiguous(memory_format=torch.channels_last_3d)
                     if not (dense and gr.stride() == p.stride() and st["exp_avg"].stride() == p.stride()):
@@ -866,6 +909,24 @@ class FusedAdam:
             rc = lib().nslam_adam_step(arr, len(segs), b1, b2, self.eps, int(bool(zero_grad)), ptr(ticket),
                                        stream_ptr(self.device))
         check(rc, "nslam_adam_step")
+
+    @torch.no_grad()
+    def reset_state(self):
+        """Zero every parameter's Adam state (moments and step count) in place: the optimiser then behaves
+        as a freshly built one (Mapper.optimize_map re-creates its Adam per call, Mapper.py:365-389), while
+        the state buffers — which captured hipGraphs hold by address — stay where they are."""
+        for st in self.state.values():
+            st["exp_avg"].zero_()
+            st["exp_avg_sq"].zero_()
+            st["step"].zero_()
+
+    def prepare(self, grads=None):
+        """Create (eagerly, outside any graph capture) the Adam state and the step ticket of the parameter
+        subset a step(grads) would update, so the step can be captured in a hipGraph."""
+        segs = self.segments(grads)
+        key = tuple(id(p) for _, p, _ in segs)
+        if segs and key not in self._tickets:
+            self._tickets[key] = torch.zeros(1, dtype=torch.int32, device=self.device)
 
     def zero_grad(self, set_to_none=True):
         for g in self.param_groups:

@@ -11,7 +11,10 @@ import copy
 import numpy as np
 import torch
 
-from .common import get_camera_from_tensor, get_samples, get_tensor_from_camera
+from . import common as _common
+from .common import camera_tensors, get_camera_from_tensor, get_samples, get_tensor_from_camera
+
+_SELECT_UV = _common.select_uv
 
 
 class Tracker(object):
@@ -49,7 +52,11 @@ class Tracker(object):
         self.decoders = None
         self._bound_dev = None
         self.fused = True     # track_frame on engine.TrackingEngine (no host sync per iteration)
+        self.graphs = True    # fused, no generator: a frame's camera loop is one cached hipGraph (device draws)
         self._engine = None
+        self._fstate = None   # persistent buffers of the captured camera loop
+        self._graphs = {}
+        self._draw_seed = int(torch.randint(0, 2 ** 62, (1,)).item())
 
     def _inside_mask(self, rays_o, rays_d, gt_depth):
         """Tracker.py:95-100: keep rays whose AABB exit distance >= gt depth."""
@@ -90,15 +97,32 @@ class Tracker(object):
         return loss.item()
 
     def update_para_from_mapping(self):
-        """Tracker.py:130-142: snapshot the mapper's decoders and grids (no gradients needed)."""
+        """Tracker.py:130-142: snapshot the mapper's decoders and grids (no gradients needed).  The first
+        snapshot is a deep copy; later ones are copied into it in place, so the tracking engine (and the
+        hipGraphs captured over it) stay bound to the same buffers."""
         if self.mapping_idx[0] != self.prev_mapping_idx:
-            self.decoders = copy.deepcopy(self.shared_decoders).to(self.device)
-            # tracking optimises the camera only: decoder/grid gradients are never used
-            self.decoders.requires_grad_(False)
-            for key, val in self.shared_c.items():
-                self.c[key] = val.detach().clone().to(self.device)
+            same = (self.decoders is not None and set(self.c) == set(self.shared_c)
+                    and all(self.c[k].shape == v.shape and self.c[k].stride() == v.stride()
+                            for k, v in self.shared_c.items()))
+            if same:
+                with torch.no_grad():
+                    for a, b in zip(self.decoders.parameters(), self.shared_decoders.parameters()):
+                        a.copy_(b)
+                    for key, val in self.shared_c.items():
+                        self.c[key].copy_(val)
+                if self._engine is not None:
+                    for d in self._engine.eng.decs.values():  # the MFMA-packed copies of the new weights
+                        d.repack()
+            else:
+                self.decoders = copy.deepcopy(self.shared_decoders).to(self.device)
+                # tracking optimises the camera only: decoder/grid gradients are never used
+                self.decoders.requires_grad_(False)
+                for key, val in self.shared_c.items():
+                    self.c[key] = val.detach().clone().to(self.device)
+                self._engine = None  # re-bound to the new snapshot on first use
+                self._fstate = None
+                self._graphs.clear()
             self.prev_mapping_idx = self.mapping_idx[0].clone()
-            self._engine = None  # re-bound to the new snapshot on first use
 
     def engine(self):
         """TrackingEngine over the current decoder/grid snapshot."""
@@ -123,11 +147,13 @@ class Tracker(object):
             return gt_c2w.clone()
         if self.const_speed_assumption and prev2_c2w is not None:
             pre = pre_c2w.float().to(device)
-            delta = pre @ prev2_c2w.to(device).float().inverse()
+            delta = pre @ torch.linalg.inv_ex(prev2_c2w.to(device).float())[0]  # (no error check: no sync)
             est = delta @ pre
         else:
             est = pre_c2w.to(device)
-        camera_tensor = get_tensor_from_camera(est.detach()).to(device)
+        # (on the device: no host round trip per frame)
+        camera_tensor = camera_tensors(est.detach().float()[None])[0] if self.fused else \
+            get_tensor_from_camera(est.detach()).to(device)
         if self.seperate_LR:
             T = camera_tensor[-3:].clone().requires_grad_(True)
             quad = camera_tensor[:4].clone().requires_grad_(True)
@@ -151,10 +177,15 @@ class Tracker(object):
     def _track_fused(self, camera_tensor, gt_color, gt_depth):
         """The camera loop of track_frame (Tracker.py:225-250) on the TrackingEngine: the best pose
         (lowest pre-step loss → the pose right after that step, as the reference keeps it) is
-        selected on the device; one host sync at the end."""
+        selected on the device; no host sync.  Without a generator the pixels are drawn in the gather
+        kernel and the whole loop is ONE hipGraph, captured on the first frame and replayed on every
+        later one (the frame is copied into persistent slots; a fresh Adam per frame by resetting its
+        state).  With a generator (pinned draws): torch.randint per iteration, eager."""
         from .ops import FusedAdam
         eng = self.engine()
         device = self.device
+        if self.graphs and self.generator is None and _common.select_uv is _SELECT_UV:
+            return self._track_graph(eng, camera_tensor, gt_color, gt_depth)
         cam = camera_tensor.detach().clone().requires_grad_(True)
         opt = FusedAdam([{"params": [cam], "lr": self.cam_lr}])
         best = cam.detach().clone()
@@ -169,3 +200,52 @@ class Tracker(object):
             best = torch.where(better, cam.detach(), best)
         bottom = torch.tensor([[0, 0, 0, 1.0]], dtype=torch.float32, device=device)
         return torch.cat([get_camera_from_tensor(best), bottom], 0)
+
+    def _track_graph(self, eng, camera_tensor, gt_color, gt_depth):
+        from .ops import FusedAdam
+        dev = self.device
+        st = self._fstate
+        if st is None:
+            cam = torch.zeros(7, dtype=torch.float32, device=dev).requires_grad_(True)
+            st = self._fstate = {
+                "depth": torch.zeros(self.H, self.W, dtype=torch.float32, device=dev),
+                "color": torch.zeros(self.H, self.W, 3, dtype=torch.float32, device=dev),
+                "cam": cam, "opt": FusedAdam([{"params": [cam], "lr": self.cam_lr}]),
+                "best": torch.zeros(7, dtype=torch.float32, device=dev),
+                "best_loss": torch.zeros((), dtype=torch.float64, device=dev)}
+        cam, opt, best, best_loss = st["cam"], st["opt"], st["best"], st["best_loss"]
+        st["depth"].copy_(gt_depth)
+        st["color"].copy_(gt_color)
+        n, iters = self.tracking_pixels, self.num_cam_iters
+
+        def loop():
+            for _ in range(iters):
+                loss = eng.iteration(cam, st["depth"], st["color"], None, opt, n=n, seed=self._draw_seed)
+                better = loss < best_loss
+                best_loss.copy_(torch.where(better, loss, best_loss))
+                best.copy_(torch.where(better, cam.detach(), best))
+
+        key = (iters, n)
+        if key not in self._graphs:
+            # one zero-lr eager iteration (camera grad, Adam ticket, draw counter made before capture);
+            # the draw stream is rewound, so the frame draws as it would have eagerly
+            ctr = eng.eng.draws(self._draw_seed).counter
+            ctr0 = ctr.clone()
+            with torch.no_grad():
+                cam.copy_(camera_tensor)
+            opt.param_groups[0]["lr"] = 0.0
+            eng.iteration(cam, st["depth"], st["color"], None, opt, n=n, seed=self._draw_seed)
+            opt.param_groups[0]["lr"] = self.cam_lr
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                loop()
+            self._graphs[key] = g
+            ctr.copy_(ctr0)
+        with torch.no_grad():
+            cam.copy_(camera_tensor)
+            best.copy_(camera_tensor)
+        best_loss.fill_(float("inf"))
+        opt.reset_state()
+        self._graphs[key].replay()
+        bottom = torch.tensor([[0, 0, 0, 1.0]], dtype=torch.float32, device=dev)
+        return torch.cat([get_camera_from_tensor(best.clone()), bottom], 0)

@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_strerror(pkg):
     L = pkg._lib.lib()
-    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 18
+    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 19
     assert L.nslam_strerror(0) == b"ok"
     assert b"invalid" in L.nslam_strerror(-1)
 
@@ -219,3 +219,29 @@ def test_v15_cam_grad_parts_validates_without_gpu(pkg):
     assert L.nslam_cam_grad_parts(64, 64, bufs, 3, 64, 64, 10, 48, 64, 64, 64, None) == -1         # a NULL part
     bufs[1] = 64
     assert L.nslam_cam_grad_parts(64, 64, bufs, 3, 64, 64, (1 << 31) // 3 // 48 + 1, 48, 64, 64, 64, None) == -2
+
+
+def test_v19_cam_batch_validates_without_gpu(pkg):
+    """nslam_cam_grad_batch / nslam_cam_pose_batch reject bad camera counts, strides, buffers and ray slices
+    outside the batch before any launch."""
+    L = pkg._lib.lib()
+    bufs = (ctypes.c_void_p * 4)(64, 64, 64, 64)
+    rb = (ctypes.c_int64 * 2)(0, 100)
+    args = lambda **k: dict(dict(cams=64, c2w=64, stride=16, n=2, rb=rb, per=100, bufs=bufs, parts=3, z=64, rd=64,  # noqa: E731
+                                 N=200, S=48, out=64, ws=64, tk=64), **k)
+
+    def call(a):
+        return L.nslam_cam_grad_batch(a["cams"], a["c2w"], a["stride"], a["n"], a["rb"], a["per"], a["bufs"],
+                                      a["parts"], a["z"], a["rd"], a["N"], a["S"], a["out"], a["ws"], a["tk"], None)
+    assert call(args(n=0)) == -1                       # no cameras
+    assert call(args(n=33)) == -1                      # more than NSLAM_MAX_FRAMES
+    assert call(args(stride=8)) == -1                  # a c2w stride shorter than a [3,4] pose
+    assert call(args(tk=None)) == -1                   # no tickets
+    assert call(args(ws=None)) == -1                   # no workspace
+    assert call(args(parts=5)) == -1                   # too many d/dpts parts
+    assert call(args(per=101)) == -1                   # camera 1's slice ends past the batch
+    assert call(args(rb=None)) == -1                   # no slice table
+    assert call(args(N=(1 << 31) // 3 // 48 + 1, per=100)) == -2
+    assert L.nslam_cam_pose_batch(None, 64, 16, 2, None) == -1
+    assert L.nslam_cam_pose_batch(64, 64, 16, 0, None) == -1
+    assert L.nslam_cam_pose_batch(64, 64, 8, 2, None) == -1

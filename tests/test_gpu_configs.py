@@ -1,6 +1,9 @@
 """The BASELINE.json configurations run through the FUSED mapping engine (the bench's path) and
 compared elementwise with the oracle on the same inputs:
 
+  configs[0] Demo: configs/Demo/demo.yaml bound and camera (480x640, crop_edge 10), 200 pixels x 32
+             samples with N_surface 0, one mapping iteration — the engine's iteration per stage and
+             Mapper.optimize_map(1) (the reference schedule puts iteration 0 in the middle stage).
   configs[2] ScanNet scene0000: 5000 pixels × 48 samples over a 5-frame window, colour stage,
              frustum-compacted grid gradients (MappingEngine.iteration) — and bundle adjustment
              with a 5-frame window through the Mapper drop-in (4 cameras optimised, the oldest
@@ -180,6 +183,95 @@ def test_scene0000_color_iteration_5000_rays():
     assert ok, report
 
 
+DEMO_CAM = dict(H=460, W=620, fx=577.590698, fy=578.729797, cx=308.905426, cy=232.683609)  # demo.yaml, crop 10
+DEMO_BOUND = [[0.0, 6.5], [0.0, 4.0], [0.0, 3.5]]                                          # demo.yaml:28
+
+
+@pytest.mark.parametrize("stage", ["middle", "fine", "color"])
+def test_demo_iteration_200x32(stage):
+    """configs[0] as stated: Demo grids (coarse [1,32,3,4,6] ... fine [1,32,21,25,41]), one frame x 200
+    pixels, 32 stratified samples and N_surface 0 (no surface samples although gt depth is given), one
+    engine mapping iteration of `stage` with frustum-compacted gradients vs the oracle."""
+    cam = DEMO_CAM
+    bound, grids, sd, frames = build_scene(DEMO_BOUND, cam, 1, seed=51, coarse=True)
+    assert [list(grids[k].shape) for k in ("grid_coarse", "grid_middle", "grid_fine")] == \
+        [[1, 32, 3, 4, 6], [1, 32, 10, 12, 20], [1, 32, 21, 25, 41]]
+    n_per = 200
+    pix = torch.randint(cam["H"] * cam["W"], (n_per,), generator=torch.Generator().manual_seed(52))
+    nice = product_nice(sd, bound, coarse=True)
+    gdev = {k: v.to(DEV).contiguous(memory_format=torch.channels_last_3d) for k, v in grids.items()
+            if k != "grid_coarse"}
+    fdev = [(d.to(DEV), c.to(DEV), m.to(DEV)) for d, c, m in frames]
+    rows = frustum_rows(frames, gdev, bound, cam)
+    trainable = ("color",) if stage == "color" else ()
+    eng, snap, ray_loss, keep = run_engine(nice, gdev, bound, fdev, pix, n_per, cam, stage, rows, 32, 0, trainable)
+    ro, rd, gd, gc, k_ref = oracle_batch(frames, pix, n_per, cam, bound)
+    assert torch.equal(keep.bool().cpu(), k_ref) and ro.shape[0] > 150
+    loss, g, dec, _ = oracle_step(sd, {k: v for k, v in grids.items() if k != "grid_coarse"}, ro, rd, gd, gc, stage,
+                                  bound, 32, 0, trainable)
+    report = {"loss_rel": abs(float(ray_loss.sum()) - loss) / loss, "rays": int(ro.shape[0])}
+    ok = report["loss_rel"] < 1e-5
+    for k in g:
+        ok &= check(report, k, snap[k], compact(g[k], rows[k]), TOL[k])
+    if trainable:
+        ok &= check(report, "color_decoder", snap["dec.color"], decoder_flat(nice, "color", dec), TOL["decoder"])
+    print(json.dumps(report, indent=1))
+    assert ok, report
+
+
+def test_demo_optimize_map_one_iteration(monkeypatch):
+    """configs[0]: Mapper.optimize_map(num_joint_iters=1) on the fused path at Demo shapes, 200 pixels x 32
+    samples (N_surface 0): iteration 0 is a middle-stage iteration (Mapper.py:403-411; middle lr 0.1),
+    frustum selection on.  Oracle replica: the same draws, Adam on the middle grid with the gradient
+    outside the mask zeroed (≡ Adam on the masked vector)."""
+    from test_gpu_dropins import base_cfg
+    cam = DEMO_CAM
+    bound, grids, sd, frames = build_scene(DEMO_BOUND, cam, 1, seed=53, coarse=True)
+    grids = {k: v for k, v in grids.items() if k != "grid_coarse"}
+    cfg = base_cfg()
+    cfg["mapping"].update(pixels=200, frustum_feature_selection=True)
+    cfg["rendering"].update(N_samples=32, N_surface=0)
+    nice = product_nice(sd, bound, coarse=True)
+    from types import SimpleNamespace
+    slam = SimpleNamespace(nice=True, bound=bound, H=cam["H"], W=cam["W"], fx=cam["fx"], fy=cam["fy"], cx=cam["cx"],
+                           cy=cam["cy"], shared_decoders=nice,
+                           shared_c={k: v.to(DEV).contiguous(memory_format=torch.channels_last_3d)
+                                     for k, v in grids.items()},
+                           estimate_c2w_list=torch.zeros(4, 4, 4), gt_c2w_list=torch.zeros(4, 4, 4),
+                           mapping_idx=torch.zeros(1).int())
+    slam.renderer = P.Renderer(cfg, None, slam)
+    mp = P.Mapper(cfg, None, slam)
+    assert mp.fused
+    mp.loss_history = []
+    fp = FixedPixels(seed=54)
+    monkeypatch.setattr(P.common, "select_uv", fp)
+    d, c, m = frames[0]
+    out = mp.optimize_map(1, 1.0, 0, c, d, m, [], [], m.clone())
+    torch.cuda.synchronize()
+    assert out is None and mp.stage == "middle"
+    # oracle replica (window [-1]: no keyframes; 200 pixels of the current frame)
+    mask = P.mapper.frustum_mask(m.to(DEV), "grid_middle", grids["grid_middle"].shape[2:], d.to(DEV), bound,
+                                 cam["H"], cam["W"], cam["fx"], cam["fy"], cam["cx"], cam["cy"])
+    mask = mask.permute(2, 1, 0)[None, None].expand(1, 32, -1, -1, -1).cpu()
+    go = {k: v.clone().requires_grad_(k == "grid_middle") for k, v in grids.items()}
+    opt = torch.optim.Adam([go["grid_middle"]], lr=cfg["mapping"]["stage"]["middle"]["middle_lr"])
+    ro, rd, gd, gc, _ = oracle_batch(frames, fp.log[0], 200, cam, bound)
+    dd, _, cc = orc.render_batch_ray(sd, go, rd, ro, "middle", bound, gd, n_strat=32, n_surf=0)
+    loss = orc.mapper_loss(dd, cc, gd, gc, "middle")
+    loss.backward()
+    go["grid_middle"].grad *= mask
+    opt.step()
+    np.testing.assert_allclose([float(x) for x in mp.loss_history], [float(loss)], rtol=1e-5)
+    got = slam.shared_c["grid_middle"].detach().cpu() - grids["grid_middle"]
+    ref = go["grid_middle"].detach() - grids["grid_middle"]
+    assert float(got[~mask].abs().max()) == 0.0
+    r = rel_l2(got, ref)
+    print({"grid_middle_update_rel_l2": r, "selected": int(mask[0, 0].sum())})
+    assert r < 1e-3, r
+    for k in ("grid_fine", "grid_color"):  # not optimised in the middle stage
+        assert torch.equal(slam.shared_c[k].detach().cpu(), grids[k])
+
+
 def test_apartment_coarse_iteration():
     """configs[3]: the coarse mapper's iteration on the fused engine (stage 'coarse', gt_depth=None
     in the sampler so 32 stratified samples, loss on depth only, coarse grid gradients; the
@@ -240,13 +332,16 @@ def test_stress_color_iteration_65536x64():
     assert ok, report
 
 
-def test_scene0000_bundle_adjustment_window5(monkeypatch):
+@pytest.mark.parametrize("path", ["fused", "autograd"])
+def test_scene0000_bundle_adjustment_window5(monkeypatch, path):
     """configs[2]: Mapper.optimize_map with BA over a 5-frame window at scene0000 shapes and 5000
     pixels: 4 keyframes + the current frame, window [0, 1, 2] (overlap selection stubbed: it is
     pinned separately) + the last keyframe (3) + the current frame; frame 0 (oldest) stays fixed,
     4 cameras get Adam steps at BA_cam_lr in the colour stage.  3 iterations: middle, middle,
     colour (Mapper.py:403-421).  Oracle replica: the same draws, frustum-masked grid updates
-    (Adam with the gradient outside the mask zeroed ≡ Adam on the masked vector)."""
+    (Adam with the gradient outside the mask zeroed ≡ Adam on the masked vector).
+    path "fused": the mapping engine with the batched camera gradient (nslam_cam_grad_batch) and the
+    camera Adam on the device; "autograd": the autograd drop-in."""
     from test_gpu_dropins import base_cfg
     cam = SCANNET_CAM
     bound, grids, sd, frames = build_scene([[-2.0, 11.0], [-2.0, 11.5], [-2.0, 5.5]], cam, 5, seed=91)
@@ -265,6 +360,7 @@ def test_scene0000_bundle_adjustment_window5(monkeypatch):
     slam.renderer = P.Renderer(cfg, None, slam)
     mp = P.Mapper(cfg, None, slam)
     mp.BA = True
+    mp.fused = path == "fused"
     mp.loss_history = []
     monkeypatch.setattr(mp, "keyframe_selection_overlap", lambda *a, **k: [0, 1, 2])
     fp = FixedPixels(seed=93)
@@ -281,6 +377,15 @@ def test_scene0000_bundle_adjustment_window5(monkeypatch):
             return super().step(*a, **k)
 
     monkeypatch.setattr(torch.optim, "Adam", CapturingAdam)
+    fused_step = P.ops.FusedAdam.step
+
+    def capturing_fused_step(self, grads=None, zero_grad=False):  # the fused path's camera Adam
+        for p, g in (grads or {}).items():
+            if tuple(p.shape) == (4, 7) and self.group_of(p)["lr"] > 0:
+                cam_grads.append([r.detach().float().cpu().clone() for r in g])
+        return fused_step(self, grads=grads, zero_grad=zero_grad)
+
+    monkeypatch.setattr(P.ops.FusedAdam, "step", capturing_fused_step)
     kf = [{"gt_c2w": m, "idx": 10 * i, "depth": d, "color": c, "est_c2w": m.clone()}
           for i, (d, c, m) in enumerate(frames[:4])]
     cur_d, cur_c, cur_m = frames[4]
