@@ -288,13 +288,23 @@ class Mapper(object):
         cur_gt_depth = cur_gt_depth.to(dev).float()
         cur_gt_color = cur_gt_color.to(dev).float()
         cur_c2w = cur_c2w.to(dev).float()
+        eng = self.engine()
+        for d in eng.decs.values():  # parameters may have been assigned since the last call
+            d.repack()
+        # Everything that does not depend on the keyframe selection is enqueued first: the selection reads
+        # its overlap scores back to the host (the reference's numpy ranking), and what is queued before
+        # that read overlaps the previous call's iterations still running on the device.
+        # The frustum selection of this call (Mapper.py:314-333), bound on the device:
+        keys = self._grid_keys()
+        masks = {k: (self.get_mask_from_c2w(cur_c2w, k, self.c[k].shape[2:], cur_gt_depth)
+                     if self.frustum_feature_selection else None) for k in keys}
+        eng.bind_masks(masks)
+        opt = self._optimizer(eng)
+        opt.reset_state()  # a fresh Adam for this call (Mapper.py:365-389): zero moments and step counts
         optimize_frame, oldest_frame = self._select_window(keyframe_dict, keyframe_list, cur_gt_color, cur_gt_depth,
                                                            cur_c2w)
         F = len(optimize_frame)
         n_per = self.mapping_pixels // F
-        eng = self.engine()
-        for d in eng.decs.values():  # parameters may have been assigned since the last call
-            d.repack()
         # window slots: the oldest frame (fixed under BA) first, then the others in optimize_frame order
         order = list(optimize_frame)
         if self.BA and oldest_frame is not None:
@@ -313,12 +323,6 @@ class Mapper(object):
         frames = [(depth_s[s], color_s[s], c2w_s[s]) for s in range(F)]
         c0 = 1 if (self.BA and oldest_frame is not None) else 0
         ncam = (F - c0) if self.BA else 0
-        # frustum selection of this call (Mapper.py:314-333), bound on the device
-        keys = self._grid_keys()
-        masks = {k: (self.get_mask_from_c2w(cur_c2w, k, self.c[k].shape[2:], cur_gt_depth)
-                     if self.frustum_feature_selection else None) for k in keys}
-        eng.bind_masks(masks)
-        opt = self._optimizer(eng)
         cam = None
         if ncam:  # the 7-vectors of the optimised frames (Mapper.py:349-363)
             cams, cgrad, cws, ctk, copt = cam = self._cam_state(ncam)
@@ -369,6 +373,7 @@ class Mapper(object):
         hist = self.loss_history
         use_graphs = self.graphs and device_draws
         plan = []
+        warmed = False
         if use_graphs:
             # the warm-up iterations below draw pixels too: the draw stream is rewound afterwards, so a call
             # draws the same pixels whether its graphs were cached or just captured (and as the eager path)
@@ -381,6 +386,7 @@ class Mapper(object):
                     # and draw counters exist before capture), then the capture itself (nothing runs)
                     set_lr(stg, zero=True)
                     iteration(stg)
+                    warmed = True
                     set_lr(stg)
                     losses = torch.zeros(n, dtype=torch.float64, device=dev) if hist is not None else None
                     g = torch.cuda.CUDAGraph()
@@ -390,8 +396,8 @@ class Mapper(object):
                     self._graphs[key] = (g, losses)
                 plan.append((stg, n, self._graphs[key]))
             ctr.copy_(ctr0)
-        # a fresh Adam for this call (Mapper.py:365-389): zero moments and step counts
-        opt.reset_state()
+        if warmed:  # (the warm-up steps moved the Adam state)
+            opt.reset_state()
         if cam is not None:
             copt.reset_state()
             cams.copy_(cams0)

@@ -279,11 +279,15 @@ def test_engine_prefetch_matches_serial(tiny):
     out = {}
     # (prefetch, its stream, one merged Adam): serial; the round-5 default (the prefetch on the mask-only
     # launch's stream, one Adam after both branches); round 4's (its own stream, per-branch Adam)
-    for key in ((False, "lean", True), (True, "lean", True), (True, "own", False)):
-        pre, pst, merge = key
+    # (+ round 6's lean_main topology: the prefetch ahead of the weight gradients on the side stream, whose
+    # event the caller's stream waits for before Adam — no join)
+    variants = ((False, "lean", True, "wgrad_main"), (True, "lean", True, "wgrad_main"), (True, "own", False, "wgrad_main"),
+                (True, "lean", True, "lean_main"))
+    for key in variants:
+        pre, pst, merge, topo = key
         nice, c = _nice(sc)
         eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV)
-        eng.prefetch_stream, eng.adam_merge = pst, merge
+        eng.prefetch_stream, eng.adam_merge, eng.topology = pst, merge, topo
         opt = P.ops.FusedAdam([{"params": [eng.decs["color"].param], "lr": 0.005}] +
                               [{"params": [c[k]], "lr": 0.005} for k in ("grid_middle", "grid_fine", "grid_color")])
         kept = torch.zeros(1, dtype=torch.int64, device=DEV)
@@ -295,8 +299,8 @@ def test_engine_prefetch_matches_serial(tiny):
         torch.cuda.synchronize()
         out[key] = (losses, {k: v.detach().clone() for k, v in c.items()}, eng.decs["color"].param.detach().clone(),
                     int(kept), sorted(float(st["step"]) for st in opt.state.values()))
-    ref = out[(False, "lean", True)]
-    for key in ((True, "lean", True), (True, "own", False)):
+    ref = out[variants[0]]
+    for key in variants[1:]:
         o = out[key]
         for a, b in zip(ref[0], o[0]):
             assert rel_l2(b, a) < 1e-5, key
@@ -337,11 +341,12 @@ def test_engine_branch_order_and_concurrency_keep_the_map(tiny):
     the same map, decoder, packed copy and Adam steps (grid atomics order aside)."""
     sc, frames = _frames(tiny)
     out = {}
-    for variant in ("first", "second", "serial"):
+    for variant in ("first", "second", "serial", "lean_main"):
         nice, c = _nice(sc)
         eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV)
         eng.wgrad_first = variant != "second"
         eng.concurrent = variant != "serial"
+        eng.topology = "lean_main" if variant == "lean_main" else "wgrad_main"
         opt = P.ops.FusedAdam([{"params": [eng.decs["color"].param], "lr": 0.005}] +
                               [{"params": [c[k]], "lr": 0.005} for k in ("grid_middle", "grid_fine", "grid_color")])
         for it in range(3):
@@ -352,7 +357,7 @@ def test_engine_branch_order_and_concurrency_keep_the_map(tiny):
         out[variant] = ({k: v.detach().clone() for k, v in c.items()}, eng.decs["color"].param.detach().clone(),
                         eng.decs["color"].packed.clone(), sorted(float(st["step"]) for st in opt.state.values()))
     b = out["serial"]
-    for v in ("first", "second"):
+    for v in ("first", "second", "lean_main"):
         a = out[v]
         for k in a[0]:
             assert rel_l2(a[0][k], b[0][k]) < 1e-5, (v, k)

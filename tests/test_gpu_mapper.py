@@ -109,3 +109,39 @@ def test_coarse_mapper_fused_matches_autograd(tiny, monkeypatch):
     assert rel_l2(gf, ga) < 1e-3, rel_l2(gf, ga)
     # only the coarse grid is optimised by the coarse mapper
     assert max(other_f.values()) == 0.0 and max(other_a.values()) == 0.0
+
+
+def test_tracker_graph_matches_eager_device_draws(tiny):
+    """Tracker.track_frame's captured camera loop (one hipGraph per frame, device draws) == the same loop
+    run eagerly on the tracking engine with the same draw stream — bit for bit (the camera chain is
+    deterministic: no float atomics), on the frame that captures the graph and on one that replays it."""
+    cfg = base_cfg()
+    sc = Scene(tiny)
+    c2w = torch.cat([sc.c2w, torch.tensor([[0, 0, 0, 1.0]])], 0).cuda()
+    pres = []
+    for d in (0.02, -0.015):
+        pre = c2w.clone()
+        pre[:3, 3] += d
+        pres.append(pre)
+    tr = P.Tracker(cfg, None, sc.slam(cfg))
+    tr._draw_seed = 77
+    got = [tr.track_frame(k + 1, sc.color.cuda(), sc.depth.cuda(), c2w, pre_c2w=pre) for k, pre in enumerate(pres)]
+    assert len(tr._graphs) == 1
+    # eager replica: the same engine calls, draws from the same stream (counter 0, advancing per iteration)
+    tr2 = P.Tracker(cfg, None, sc.slam(cfg))
+    tr2.update_para_from_mapping()
+    eng = tr2.engine()
+    ref = []
+    for pre in pres:
+        cam = P.common.camera_tensors(pre[None])[0].clone().requires_grad_(True)
+        opt = P.ops.FusedAdam([{"params": [cam], "lr": cfg["tracking"]["lr"]}])
+        best, best_loss = cam.detach().clone(), torch.full((), float("inf"), dtype=torch.float64, device="cuda")
+        for _ in range(cfg["tracking"]["iters"]):
+            loss = eng.iteration(cam, sc.depth.cuda(), sc.color.cuda(), None, opt, n=cfg["tracking"]["pixels"], seed=77)
+            better = loss < best_loss
+            best_loss = torch.where(better, loss, best_loss)
+            best = torch.where(better, cam.detach(), best)
+        ref.append(torch.cat([P.common.get_camera_from_tensor(best), torch.tensor([[0, 0, 0, 1.0]], device="cuda")]))
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b), (a - b).abs().max()
+    assert not torch.equal(got[0], pres[0])  # the loop moved the pose
