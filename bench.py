@@ -954,9 +954,23 @@ def optimize_map_leg(dev, cfg, ba, calls=6, warm=2, iters=60):
         call(warm + k)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / calls
+    # where a call's time goes: extra calls with phase marks (host clock; HIP events on the stream)
+    mp.timing = []
+    for k in range(3):
+        call(warm + calls + k)
+    torch.cuda.synchronize()
+    ph = ("masks", "selected", "window", "iterations")
+    prev = ["t0"] + list(ph[:-1])
+    host = {p: sum((t[p] - t[q]) * 1e3 for t in mp.timing) / len(mp.timing) for p, q in zip(ph, prev)}
+    gpu = {p: sum(t["ev"][q].elapsed_time(t["ev"][p]) for t in mp.timing) / len(mp.timing)
+           for p, q in zip(ph[1:], ph[:-1])}
+    mp.timing = None
     res = {"ms_per_call": dt * 1e3, "ms_per_iteration": dt * 1e3 / iters, "iterations_per_call": iters,
            "calls": calls, "graphs_cached": len(mp._graphs), "bundle_adjustment": ba,
-           "pixels": cfg["pixels"], "window": F}
+           "pixels": cfg["pixels"], "window": F,
+           "phase_host_ms": {k: round(v, 3) for k, v in host.items()},
+           "phase_gpu_ms": {k: round(v, 3) for k, v in gpu.items()},
+           "iterations_gpu_ms_per_iteration": gpu["iterations"] / iters}
     del mp, scene
     torch.cuda.empty_cache()
     return res
@@ -969,6 +983,43 @@ def engine_stage_ms(dev, cfg, reps=50):
     out = {}
     for stage in ("middle", "fine", "color"):
         out[stage], _ = graph_time(scene, lambda: scene.step(stage=stage), reps)
+    out["schedule_60"] = (25 * out["middle"] + 12 * out["fine"] + 23 * out["color"]) / 60.0
+    del scene
+    torch.cuda.empty_cache()
+    return {k: round(v, 4) for k, v in out.items()}
+
+
+def engine_ba_stage_ms(dev, cfg, reps=50):
+    """The bare engine with bundle adjustment per stage at a config's shape: engine.MappingEngine.iteration
+    over the 5-frame window with d/dpts formed by the backward, the batched camera gradient of the 4
+    non-oldest cameras (nslam_cam_grad_batch) and their Adam step, the poses re-derived from the cameras
+    each iteration (nslam_cam_pose_batch) — the GPU work of an optimize_map BA iteration, replayed in
+    hipGraph blocks, without the drop-in's per-call work."""
+    P = pkg()
+    scene = Room0Scene(dev, 0, cfg=dict(cfg), path="fused")
+    F = cfg["window"]
+    n = cfg["pixels"] // F
+    c2w = torch.eye(4, device=dev).repeat(F, 1, 1)
+    c2w[:, :3] = scene.c2w
+    frames = [(scene.depth[f], scene.color[f], c2w[f]) for f in range(F)]
+    cams = P.common.camera_tensors(c2w[1:]).contiguous()
+    cgrad = torch.zeros_like(cams)
+    ws = torch.zeros((F - 1) * P.ops.CAM_GRAD_WS_DOUBLES, dtype=torch.float64, device=dev)
+    tk = torch.zeros(F - 1, dtype=torch.int32, device=dev)
+    copt = P.ops.FusedAdam([{"params": [cams], "lr": 0.001}])
+    eng = scene.engine
+
+    def post_bwd(gps, ro, rd, z):
+        P.ops.cam_grad_batch(cams, c2w[1:], [(1 + k) * n for k in range(F - 1)], n, gps, z, rd, cgrad, ws, tk)
+        copt.step(grads={cams: cgrad})
+
+    def step(stage):
+        P.ops.cam_pose_batch(cams, c2w[1:])
+        eng.iteration(stage, frames, None, n, (cfg["H"], cfg["W"]), (cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"]),
+                      scene.opt, trainable_decoders=("color",), seed=1000, post_bwd=post_bwd)
+    out = {}
+    for stage in ("middle", "fine", "color"):
+        out[stage], _ = graph_time(scene, lambda: step(stage), reps)
     out["schedule_60"] = (25 * out["middle"] + 12 * out["fine"] + 23 * out["color"]) / 60.0
     del scene
     torch.cuda.empty_cache()
@@ -1053,17 +1104,21 @@ def leg_main(leg):
         res = apartment_iterations(dev)
     elif leg == "optimize_map":
         res = {"engine_ms_per_iteration": engine_stage_ms(dev, ROOM0),
+               "engine_ba_ms_per_iteration": engine_ba_stage_ms(dev, ROOM0),
                "optimize_map": optimize_map_leg(dev, ROOM0, ba=False),
                "optimize_map_ba": optimize_map_leg(dev, ROOM0, ba=True)}
-        for k in ("optimize_map", "optimize_map_ba"):
-            res[k]["vs_engine_schedule"] = res[k]["ms_per_iteration"] / res["engine_ms_per_iteration"]["schedule_60"]
+        for k, e in (("optimize_map", "engine_ms_per_iteration"), ("optimize_map_ba", "engine_ba_ms_per_iteration")):
+            res[k]["vs_engine_schedule"] = res[k]["ms_per_iteration"] / res[e]["schedule_60"]
+            res[k]["engine_baseline"] = e
         res["workload"] = ("Replica room0: Mapper.optimize_map(60 iterations, 1000 px over a 5-frame window) per call "
                            "vs the bare engine's iterations of the same stage mix (25 middle / 12 fine / 23 colour)")
     elif leg == "scene0000":
         res = {"engine_ms_per_iteration": engine_stage_ms(dev, SCENE0000),
+               "engine_ba_ms_per_iteration": engine_ba_stage_ms(dev, SCENE0000),
                "optimize_map_ba": optimize_map_leg(dev, SCENE0000, ba=True)}
         om = res["optimize_map_ba"]
-        om["vs_engine_schedule"] = om["ms_per_iteration"] / res["engine_ms_per_iteration"]["schedule_60"]
+        om["vs_engine_schedule"] = om["ms_per_iteration"] / res["engine_ba_ms_per_iteration"]["schedule_60"]
+        om["engine_baseline"] = "engine_ba_ms_per_iteration"
         om["ray_samples_per_s_upper"] = SCENE0000["pixels"] * 48 / (om["ms_per_iteration"] * 1e-3)
         res["workload"] = ("configs[2] ScanNet scene0000: 460x620, Mapper.optimize_map with BA over a 5-frame window "
                            "(4 cameras), 5000 px x 48 samples, 60 iterations per call")

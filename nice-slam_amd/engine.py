@@ -131,13 +131,6 @@ class MappingEngine:
         # where the merged Adam runs: after the mask-only launch on its side stream ("side") or on the
         # main stream after the join ("main", experiment)
         self.adam_on = _env_choice("NSLAM_ADAM_ON", "side", ("side", "main"))
-        # backward topology of a colour iteration with the merged Adam: "wgrad_main" (the weight gradients
-        # on the caller's stream, the mask-only launch + Adam on a side stream, joined before the next
-        # forward) or "lean_main" (the mask-only launch right after the loss on the caller's stream, the
-        # weight gradients on the side stream, Adam on the caller's stream once their event fires: the
-        # critical path loss -> mask-only -> Adam -> next forward has no cross-queue edge but that event)
-        self.topology = _env_choice("NSLAM_BWD_TOPOLOGY", "wgrad_main", ("wgrad_main", "lean_main"))
-        self._joined_side = False  # the last query_bwd already ordered the side stream before the caller's
         self._wg_ev = None
         for k, v in c.items():
             if not v.is_contiguous(memory_format=torch.channels_last_3d):
@@ -320,10 +313,6 @@ class MappingEngine:
         lean = [d for d in decs if self.merge and masks and (d not in wgt or (d == "color" and tape_color))]
         others = [d for d in decs if d not in lean]
         gp = {d: torch.empty(n, 3, dtype=torch.float64, device=z.device) for d in decs} if pts_grad else None
-        self._joined_side = False
-        if (self.topology == "lean_main" and on_branch is not None and concurrent and not ordered_branches
-                and self.adam_merge and n > 0 and "color" in wgt and tape_color and lean == decs and not others):
-            return self._bwd_lean_main(cfg, n, g_raw, ro, rd, z, lean, gp, on_branch, decs, pts_parts)
         # units: (kind, decoder names) in enqueue order
         units = []
         if "color" in lean and "color" in wgt and n > 0:
@@ -437,55 +426,6 @@ class MappingEngine:
             return None
         parts = [gp[d] for d in decs]
         if pts_parts:  # the per-decoder shares, for a consumer that sums them itself
-            return parts
-        out = parts[0]
-        for g in parts[1:]:
-            out += g
-        return out
-
-    def _bwd_lean_main(self, cfg, n, g_raw, ro, rd, z, lean, gp, on_branch, decs, pts_parts):
-        """query_bwd in the "lean_main" topology: the side stream forks after the loss and runs the colour
-        weight gradients (+ its slab reduction), recording an event; the caller's stream runs the mask-only
-        launch of every decoder, waits for that event and runs the merged Adam.  Everything the side stream
-        ran before the event (a ray prefetch enqueued there first, too) is then ordered before the caller's
-        next work: no join is needed (self._joined_side)."""
-        main = torch.cuda.current_stream(z.device)
-        if not self._side:
-            self._side.append(torch.cuda.Stream(z.device))
-        side = self._side[0]
-        if self._wg_ev is None:
-            self._wg_ev = torch.cuda.Event()
-        with ops._span("query_bwd"):
-            side.wait_stream(main)
-            for t in (ro, rd, z, g_raw, self._saved, self._tape):
-                if t is not None:
-                    t.record_stream(side)
-            with torch.cuda.stream(side):
-                wsb = lib().nslam_query_bwd_decoder_workspace_size(ctypes.byref(cfg), _lib.DEC_COLOR, n)
-                ws = torch.empty(wsb, dtype=torch.uint8, device=z.device)
-                with ops._span("query_bwd.color_wgrad"):
-                    rc = lib().nslam_color_wgrad(ctypes.byref(cfg), None, n, ptr(g_raw), ptr(ws), wsb, side.cuda_stream)
-                check(rc, "nslam_color_wgrad")
-                self._wg_ev.record(side)
-            lc = _lib.NslamQueryCfg.from_buffer_copy(cfg)
-            gps = (ctypes.c_void_p * 4)()
-            mask = 0
-            for name in lean:
-                d = ops._DEC_ID[name]
-                mask |= 1 << d
-                lc.dgrad[d] = _lib.NslamDecGrad()
-                if gp is not None:
-                    gps[d] = ptr(gp[name])
-            with ops._span("query_bwd." + "+".join(lean)):
-                rc = lib().nslam_query_bwd_decoders(ctypes.byref(lc), mask, None, n, ptr(g_raw), gps, main.cuda_stream)
-            check(rc, "nslam_query_bwd_decoders")
-            main.wait_event(self._wg_ev)
-            on_branch(lean, part="all")
-        self._joined_side = True
-        if gp is None:
-            return None
-        parts = [gp[d] for d in decs]
-        if pts_parts:
             return parts
         out = parts[0]
         for g in parts[1:]:
@@ -655,8 +595,8 @@ class MappingEngine:
             exchange(keys, dnames)
         elif allreduce is not None:  # the grid gradients as one flat buffer, plus the decoder gradients
             allreduce([self.gbuf] + [self.decs[n].grad for n in dnames])
-        if side is not None and not (self._joined_side and side is self._side[0]):
-            main.wait_stream(side)  # join: the next call reads the prefetched set
+        if side is not None:  # join: the next call reads the prefetched set
+            main.wait_stream(side)
         if post_bwd is not None:
             post_bwd(gps if isinstance(gps, list) else [gps], ro, rd, z)
         if on_branch is None:

@@ -55,6 +55,18 @@ def _remap_bilinear(img, u, v):
     return tap(x0, y0) * w00 + tap(x0 + 1, y0) * w01 + tap(x0, y0 + 1) * w10 + tap(x0 + 1, y0 + 1) * w11
 
 
+_KMAT = {}
+
+
+def _intrinsics(fx, fy, cx, cy, dev):
+    """The camera matrix as a float64 device tensor, made once per (intrinsics, device): a hipGraph
+    capturing its users must not copy it from the host."""
+    key = (float(fx), float(fy), float(cx), float(cy), str(dev))
+    if key not in _KMAT:
+        _KMAT[key] = torch.tensor([[fx, 0.0, cx], [0.0, fy, cy], [0.0, 0.0, 1.0]], dtype=torch.float64, device=dev)
+    return _KMAT[key]
+
+
 def frustum_mask(c2w, key, val_shape, depth, bound, H, W, fx, fy, cx, cy):
     """Mapper.get_mask_from_c2w (Mapper.py:93-164) on the device: bool mask [X, Y, Z] of the
     grid voxels inside the camera frustum up to the observed depth + 0.5 m, or within 0.5 m of
@@ -71,11 +83,11 @@ def frustum_mask(c2w, key, val_shape, depth, bound, H, W, fx, fy, cx, cy):
     c2w = c2w.to(dev).float()
     if c2w.shape[0] == 3:
         c2w = torch.cat([c2w, torch.tensor([[0, 0, 0, 1.0]], device=dev)], 0)
-    w2c = torch.linalg.inv(c2w)
+    w2c = torch.linalg.inv_ex(c2w)[0]  # (torch.linalg.inv without its error check: no host sync, capturable)
     cam = points @ w2c[:3, :3].T + w2c[:3, 3]
     cam = cam.double()
     cam[:, 0] *= -1
-    K = torch.tensor([[fx, 0.0, cx], [0.0, fy, cy], [0.0, 0.0, 1.0]], dtype=torch.float64, device=dev)
+    K = _intrinsics(fx, fy, cx, cy, dev)
     uvz = cam @ K.T
     z = uvz[:, 2] + 1e-5
     uv = (uvz[:, :2] / z[:, None]).float()
@@ -130,10 +142,12 @@ class Mapper(object):
         self._fopt = None
         self._cam = {}      # number of BA cameras -> (cams, grad, ws, tickets, FusedAdam)
         self._slots = None  # (depth [F,H,W], color [F,H,W,3], c2w [F,4,4]) of the window
+        self._setup = None  # persistent inputs of the captured per-call setup (_setup_inputs)
         self._graphs = {}
         # the device draws' stream key (from torch's CPU generator, so torch.manual_seed pins it)
         self._draw_seed = int(torch.randint(0, 2 ** 62, (1,)).item())
         self.calls = 0
+        self.timing = None  # set to [] to record per-call phase times (host clock + HIP events; bench legs)
 
     # ------------------------------------------------------------------------------------------
     def get_mask_from_c2w(self, c2w, key, val_shape, depth):
@@ -145,20 +159,29 @@ class Mapper(object):
         """Mapper.py:185-221: per keyframe, the fraction of the current frame's near-surface samples
         (100 pixels × 16 depths in [0.8·d, d + 0.5]) that project inside it (20-px margin, in front
         of the camera).  One host sync for all keyframes (the reference's loop is host numpy)."""
+        counts, n = self._overlap_counts(gt_color, gt_depth, c2w, [kf["est_c2w"] for kf in keyframe_dict], N_samples,
+                                         pixels)
+        if counts is None:
+            return []
+        # mask.sum() / uv.shape[0] as the reference divides: an integer count over the sample count
+        return [int(cnt) / n for cnt in counts.cpu()]
+
+    def _overlap_counts(self, gt_color, gt_depth, c2w, poses, N_samples=16, pixels=100):
+        """The device half of keyframe_overlap_scores: (counts [len(poses)] device int64 or None, samples)."""
         dev = self.device
         H, W, fx, fy, cx, cy = self.H, self.W, self.fx, self.fy, self.cx, self.cy
         rays_o, rays_d, gd, _ = get_samples(0, H, 0, W, pixels, H, W, fx, fy, cx, cy, c2w, gt_depth, gt_color, dev,
                                             generator=self.generator)
-        if not keyframe_dict:
-            return []
+        if not poses:
+            return None, 0
         gd = gd.reshape(-1, 1).repeat(1, N_samples)
         t = torch.linspace(0.0, 1.0, N_samples, device=dev)
         z = gd * 0.8 * (1.0 - t) + (gd + 0.5) * t
         verts = (rays_o[..., None, :] + rays_d[..., None, :] * z[..., :, None]).reshape(-1, 3)
-        K = torch.tensor([[fx, 0.0, cx], [0.0, fy, cy], [0.0, 0.0, 1.0]], dtype=torch.float64, device=dev)
+        K = _intrinsics(fx, fy, cx, cy, dev)
         counts = []
-        for kf in keyframe_dict:
-            w2c = torch.linalg.inv(kf["est_c2w"].to(dev).float())
+        for pose in poses:
+            w2c = torch.linalg.inv_ex(pose.to(dev).float())[0]
             cam = (verts @ w2c[:3, :3].T + w2c[:3, 3]).double()
             cam[:, 0] *= -1
             uvz = cam @ K.T
@@ -167,15 +190,18 @@ class Mapper(object):
             edge = 20
             m = (uv[:, 0] < W - edge) & (uv[:, 0] > edge) & (uv[:, 1] < H - edge) & (uv[:, 1] > edge) & (zz < 0)
             counts.append(m.sum())
-        n = verts.shape[0]
-        # mask.sum() / uv.shape[0] as the reference divides: an integer count over the sample count
-        return [int(cnt) / n for cnt in torch.stack(counts).cpu()]
+        return torch.stack(counts), verts.shape[0]
 
     def keyframe_selection_overlap(self, gt_color, gt_depth, c2w, keyframe_dict, k, N_samples=16, pixels=100):
         """Mapper.py:166-228: keyframes whose frustum sees the current frame's surface samples,
         ranked by overlap (stable sort, as `sorted`), then a random permutation (numpy RNG) of the
         ones with any overlap, truncated to k."""
         scores = self.keyframe_overlap_scores(gt_color, gt_depth, c2w, keyframe_dict, N_samples, pixels)
+        return self._rank_keyframes(scores, k)
+
+    @staticmethod
+    def _rank_keyframes(scores, k):
+        """The host half of keyframe_selection_overlap (Mapper.py:222-228)."""
         ranked = sorted(enumerate(scores), key=lambda s: s[1], reverse=True)
         sel = [kid for kid, s in ranked if s > 0.0]
         return list(np.random.permutation(np.array(sel))[:k])
@@ -280,29 +306,112 @@ class Mapper(object):
             self._graphs.clear()  # (captured against the old slots)
         return self._slots
 
+    def _call_masks(self, c2w, depth):
+        """This call's frustum masks (Mapper.py:314-333; None = every voxel): grids of one shape share one."""
+        masks, by_shape = {}, {}
+        for k in self._grid_keys():
+            shp = tuple(self.c[k].shape[2:])
+            if not self.frustum_feature_selection:
+                masks[k] = None
+            elif k == "grid_coarse":
+                masks[k] = self.get_mask_from_c2w(c2w, k, shp, depth)
+            else:
+                if shp not in by_shape:
+                    by_shape[shp] = self.get_mask_from_c2w(c2w, k, shp, depth)
+                masks[k] = by_shape[shp]
+        return masks
+
+    def _setup_inputs(self, K):
+        """Persistent inputs of the captured per-call setup: the current frame, its pose, the keyframe poses."""
+        st = self._setup
+        if st is None or st["poses"].shape[0] < K:
+            dev, H, W = self.device, self.H, self.W
+            st = self._setup = {"depth": torch.zeros(H, W, dtype=torch.float32, device=dev),
+                                "color": torch.zeros(H, W, 3, dtype=torch.float32, device=dev),
+                                "c2w": torch.eye(4, dtype=torch.float32, device=dev),
+                                "poses": torch.eye(4, dtype=torch.float32, device=dev).repeat(max(8, 2 * K), 1, 1)}
+            self._graphs = {k: v for k, v in self._graphs.items() if k[0] != "setup"}  # (bound to the old buffers)
+        return st
+
     def _optimize_map_fused(self, num_joint_iters, lr_factor, idx, cur_gt_color, cur_gt_depth, gt_cur_c2w,
                             keyframe_dict, keyframe_list, cur_c2w):
         """optimize_map on the fused engine (see the module docstring)."""
         dev = self.device
         H, W = self.H, self.W
+        tm = None
+        if self.timing is not None:
+            import time
+            tm = {"t0": time.perf_counter(), "clock": time.perf_counter, "ev": {}}
+
+        def mark(name):  # host time and a HIP event on the caller's stream at a phase boundary
+            if tm is not None:
+                tm[name] = tm["clock"]()
+                e = torch.cuda.Event(enable_timing=True)
+                e.record()
+                tm["ev"][name] = e
+
         cur_gt_depth = cur_gt_depth.to(dev).float()
         cur_gt_color = cur_gt_color.to(dev).float()
         cur_c2w = cur_c2w.to(dev).float()
         eng = self.engine()
         for d in eng.decs.values():  # parameters may have been assigned since the last call
             d.repack()
+        device_draws = _common.select_uv is _SELECT_UV and self.generator is None
+        use_graphs = self.graphs and device_draws
         # Everything that does not depend on the keyframe selection is enqueued first: the selection reads
         # its overlap scores back to the host (the reference's numpy ranking), and what is queued before
-        # that read overlaps the previous call's iterations still running on the device.
-        # The frustum selection of this call (Mapper.py:314-333), bound on the device:
-        keys = self._grid_keys()
-        masks = {k: (self.get_mask_from_c2w(cur_c2w, k, self.c[k].shape[2:], cur_gt_depth)
-                     if self.frustum_feature_selection else None) for k in keys}
-        eng.bind_masks(masks)
-        opt = self._optimizer(eng)
-        opt.reset_state()  # a fresh Adam for this call (Mapper.py:365-389): zero moments and step counts
-        optimize_frame, oldest_frame = self._select_window(keyframe_dict, keyframe_list, cur_gt_color, cur_gt_depth,
-                                                           cur_c2w)
+        # that read overlaps the previous call's iterations still running on the device: this call's
+        # frustum selection (Mapper.py:314-333) bound on the device, a fresh Adam (Mapper.py:365-389: zero
+        # moments and step counts) and, with graphs, the overlap counts — one captured graph per keyframe count.
+        overlap_here = (use_graphs and self.keyframe_selection_method == "overlap" and len(keyframe_dict) > 1
+                        and "keyframe_selection_overlap" not in self.__dict__)
+        if use_graphs:
+            kfs = keyframe_dict[:-1] if overlap_here else []
+            st = self._setup_inputs(len(kfs))
+            st["depth"].copy_(cur_gt_depth)
+            st["color"].copy_(cur_gt_color)
+            st["c2w"][:cur_c2w.shape[0]].copy_(cur_c2w)
+            if kfs:
+                st["poses"][:len(kfs)].copy_(torch.stack([kf["est_c2w"].to(dev).float()[:4] for kf in kfs]))
+
+            def setup():
+                eng.bind_masks(self._call_masks(st["c2w"], st["depth"]))
+                o = self._optimizer(eng)
+                o.init_state()
+                o.reset_state()
+                if kfs:
+                    cnt, n = self._overlap_counts(st["color"], st["depth"], st["c2w"],
+                                                  [st["poses"][i] for i in range(len(kfs))])
+                    return cnt, n
+                return None, 0
+
+            key = ("setup", len(kfs))
+            if key not in self._graphs:
+                setup()  # eager warm-up: first-time allocations (engine capacity buffers, Adam state, caches)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                    out = setup()
+                self._graphs[key] = (g, out)
+            g, (counts, n_samp) = self._graphs[key]
+            g.replay()
+            opt = self._optimizer(eng)
+        else:
+            eng.bind_masks(self._call_masks(cur_c2w, cur_gt_depth))
+            opt = self._optimizer(eng)
+            opt.reset_state()
+        mark("masks")
+        if overlap_here:  # the window from the captured overlap counts (one read-back; Mapper.py:256-272)
+            scores = [int(c) / n_samp for c in counts.cpu()]
+            optimize_frame = self._rank_keyframes(scores, self.mapping_window_size - 2)
+            oldest_frame = None
+            if len(keyframe_list) > 0:
+                optimize_frame = optimize_frame + [len(keyframe_list) - 1]
+                oldest_frame = min(optimize_frame)
+            optimize_frame += [-1]
+        else:
+            optimize_frame, oldest_frame = self._select_window(keyframe_dict, keyframe_list, cur_gt_color,
+                                                               cur_gt_depth, cur_c2w)
+        mark("selected")
         F = len(optimize_frame)
         n_per = self.mapping_pixels // F
         # window slots: the oldest frame (fixed under BA) first, then the others in optimize_frame order
@@ -311,6 +420,7 @@ class Mapper(object):
             order.remove(oldest_frame)
             order.insert(0, oldest_frame)
         depth_s, color_s, c2w_s = self._window_slots(F)
+        poses = []
         for s, fr in enumerate(order):
             if fr == -1:
                 d, c, m = cur_gt_depth, cur_gt_color, cur_c2w
@@ -319,25 +429,33 @@ class Mapper(object):
                 m = keyframe_dict[fr]["est_c2w"].to(dev).float()
             depth_s[s].copy_(d)
             color_s[s].copy_(c)
-            c2w_s[s, :m.shape[0]].copy_(m)
+            poses.append(m[:3])
+        poses = torch.stack(poses)
+        c2w_s[:F, :3].copy_(poses)
         frames = [(depth_s[s], color_s[s], c2w_s[s]) for s in range(F)]
         c0 = 1 if (self.BA and oldest_frame is not None) else 0
         ncam = (F - c0) if self.BA else 0
         cam = None
         if ncam:  # the 7-vectors of the optimised frames (Mapper.py:349-363)
             cams, cgrad, cws, ctk, copt = cam = self._cam_state(ncam)
-            cams0 = camera_tensors(c2w_s[c0:F])
-            cams.copy_(cams0)
+            copt.init_state()
+
+            def cams_init():  # (captured with the first stage's graph below)
+                cams.copy_(camera_tensors(c2w_s[c0:F]))
+                copt.reset_state()
 
         def post_bwd(gps, ro, rd, z):  # BA: camera gradients of every optimised frame, then their Adam step
             ops.cam_grad_batch(cams, c2w_s[c0:F], [(c0 + k) * n_per for k in range(ncam)], n_per, gps, z, rd, cgrad,
                                cws, ctk)
             copt.step(grads={cams: cgrad})
 
-        device_draws = _common.select_uv is _SELECT_UV and self.generator is None
         intr = (self.fx, self.fy, self.cx, self.cy)
         tdec = self._trainable()
         ar = torch.arange(H * W, device=dev) if not device_draws else None
+        # device draws without BA: the next iteration's gather + sampler run beside this one's render and
+        # backward (engine prefetch); every run of one stage starts with its own batch (eng._pre reset), so
+        # a captured run holds its whole prefetch chain.  BA rewrites the poses in place: no prefetch.
+        prefetch = device_draws and not ncam
 
         def iteration(stage, record=None):
             if ncam:
@@ -351,14 +469,14 @@ class Mapper(object):
                                                                        device=dev, generator=self.generator)[0]
             ray_loss, _ = eng.iteration(stage, frames, pix, n_per, (H, W), intr, opt, trainable_decoders=tdec,
                                         use_gt_in_sampler=not self.coarse_mapper, seed=self._draw_seed,
-                                        post_bwd=post_bwd if ncam else None)
+                                        post_bwd=post_bwd if ncam else None, prefetch=prefetch)
             if record is not None:
                 record(ray_loss)
 
         def set_lr(stage, zero=False):
-            st = self.cfg["mapping"]["stage"][stage]
+            st_ = self.cfg["mapping"]["stage"][stage]
             for gi, name in enumerate(_STAGE_GROUPS):
-                opt.param_groups[gi]["lr"] = 0.0 if zero else st[name + "_lr"] * lr_factor
+                opt.param_groups[gi]["lr"] = 0.0 if zero else st_[name + "_lr"] * lr_factor
             if cam is not None:
                 copt.param_groups[0]["lr"] = self.BA_cam_lr if (stage == "color" and not zero) else 0.0
 
@@ -371,7 +489,6 @@ class Mapper(object):
             else:
                 runs.append([stg, 1])
         hist = self.loss_history
-        use_graphs = self.graphs and device_draws
         plan = []
         warmed = False
         if use_graphs:
@@ -379,28 +496,34 @@ class Mapper(object):
             # draws the same pixels whether its graphs were cached or just captured (and as the eager path)
             ctr = eng.draws(self._draw_seed).counter
             ctr0 = ctr.clone()
-            for stg, n in runs:
-                key = (stg, n, F, n_per, c0, ncam, float(lr_factor), hist is not None, tdec)
+            for ri, (stg, n) in enumerate(runs):
+                first = ri == 0 and ncam > 0  # the first run's graph also sets the BA cameras up
+                key = ("stage", stg, n, F, n_per, c0, ncam, float(lr_factor), hist is not None, tdec, first)
                 if key not in self._graphs:
                     # one zero-lr eager iteration (the maps do not move; lazily made streams, events, tickets
                     # and draw counters exist before capture), then the capture itself (nothing runs)
+                    if ncam:
+                        cams_init()
                     set_lr(stg, zero=True)
+                    eng._pre = None
                     iteration(stg)
                     warmed = True
                     set_lr(stg)
                     losses = torch.zeros(n, dtype=torch.float64, device=dev) if hist is not None else None
                     g = torch.cuda.CUDAGraph()
+                    eng._pre = None
                     with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                        if first:
+                            cams_init()
                         for i in range(n):
                             iteration(stg, None if losses is None else (lambda rl, i=i: losses[i].copy_(rl.sum())))
                     self._graphs[key] = (g, losses)
                 plan.append((stg, n, self._graphs[key]))
             ctr.copy_(ctr0)
-        if warmed:  # (the warm-up steps moved the Adam state)
+        if warmed:  # (the warm-up steps moved the Adam state and rewrote the BA cameras' poses)
             opt.reset_state()
-        if cam is not None:
-            copt.reset_state()
-            cams.copy_(cams0)
+            c2w_s[:F, :3].copy_(poses)
+        mark("window")
         if use_graphs:
             for stg, n, (g, losses) in plan:
                 self.stage = stg
@@ -408,23 +531,29 @@ class Mapper(object):
                 if hist is not None:
                     hist.extend(losses.clone().unbind())
         else:
+            if ncam:
+                cams_init()
             for stg, n in runs:
                 self.stage = stg
                 set_lr(stg)
+                eng._pre = None
                 for _ in range(n):
                     iteration(stg, None if hist is None else (lambda rl: hist.append(rl.sum())))
+        mark("iterations")
+        if tm is not None:
+            self.timing.append(tm)
         if not ncam:
             return None
         # BA write-back (Mapper.py:521-540): the optimised poses of the keyframes and the current frame
-        bottom = torch.tensor([[0, 0, 0, 1.0]], dtype=torch.float32, device=dev)
-        out = ops.cam_pose_batch(cams.detach().clone(), torch.empty(ncam, 3, 4, dtype=torch.float32, device=dev))
+        out = torch.zeros(ncam, 4, 4, dtype=torch.float32, device=dev)
+        out[:, 3, 3] = 1.0
+        ops.cam_pose_batch(cams, out)
         for k in range(ncam):
             fr = order[c0 + k]
-            c2w = torch.cat([out[k], bottom], 0)
             if fr == -1:
-                cur_c2w = c2w
+                cur_c2w = out[k]
             else:
-                keyframe_dict[fr]["est_c2w"] = c2w.clone()
+                keyframe_dict[fr]["est_c2w"] = out[k]
         return cur_c2w
 
     def _optimize_map_autograd(self, num_joint_iters, lr_factor, idx, cur_gt_color, cur_gt_depth, gt_cur_c2w,

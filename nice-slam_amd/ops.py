@@ -910,6 +910,12 @@ class FusedAdam:
                                        stream_ptr(self.device))
         check(rc, "nslam_adam_step")
 
+    def init_state(self):
+        """Create every parameter's Adam state now (buffers a hipGraph captured later can hold by address)."""
+        for g in self.param_groups:
+            for p in g["params"]:
+                self._st(p, g.get("rows"))
+
     @torch.no_grad()
     def reset_state(self):
         """Zero every parameter's Adam state (moments and step count) in place: the optimiser then behaves

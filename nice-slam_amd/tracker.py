@@ -145,6 +145,10 @@ class Tracker(object):
         gt_depth, gt_color = gt_depth.to(device), gt_color.to(device)
         if idx == 0 or self.gt_camera:
             return gt_c2w.clone()
+        if (self.fused and self.graphs and not self.seperate_LR and self.generator is None
+                and _common.select_uv is _SELECT_UV):
+            return self._track_graph(gt_color, gt_depth, pre_c2w,
+                                     prev2_c2w if self.const_speed_assumption else None)
         if self.const_speed_assumption and prev2_c2w is not None:
             pre = pre_c2w.float().to(device)
             delta = pre @ torch.linalg.inv_ex(prev2_c2w.to(device).float())[0]  # (no error check: no sync)
@@ -184,8 +188,6 @@ class Tracker(object):
         from .ops import FusedAdam
         eng = self.engine()
         device = self.device
-        if self.graphs and self.generator is None and _common.select_uv is _SELECT_UV:
-            return self._track_graph(eng, camera_tensor, gt_color, gt_depth)
         cam = camera_tensor.detach().clone().requires_grad_(True)
         opt = FusedAdam([{"params": [cam], "lr": self.cam_lr}])
         best = cam.detach().clone()
@@ -201,51 +203,64 @@ class Tracker(object):
         bottom = torch.tensor([[0, 0, 0, 1.0]], dtype=torch.float32, device=device)
         return torch.cat([get_camera_from_tensor(best), bottom], 0)
 
-    def _track_graph(self, eng, camera_tensor, gt_color, gt_depth):
+    def _track_graph(self, gt_color, gt_depth, pre_c2w, prev2_c2w):
+        """track_frame's whole per-frame work as ONE captured hipGraph, replayed for every frame: the pose
+        guess (constant speed, Tracker.py:191-198), its camera 7-vector, a fresh Adam, the camera loop with
+        device pixel draws and the device-side best-pose selection (Tracker.py:225-250), and the result pose.
+        Per frame the host copies the frame and the previous poses into persistent buffers and replays."""
         from .ops import FusedAdam
+        eng = self.engine()
         dev = self.device
         st = self._fstate
         if st is None:
             cam = torch.zeros(7, dtype=torch.float32, device=dev).requires_grad_(True)
+            out = torch.eye(4, dtype=torch.float32, device=dev)
             st = self._fstate = {
                 "depth": torch.zeros(self.H, self.W, dtype=torch.float32, device=dev),
                 "color": torch.zeros(self.H, self.W, 3, dtype=torch.float32, device=dev),
+                "pre": torch.eye(4, dtype=torch.float32, device=dev), "prev2": torch.eye(4, dtype=torch.float32, device=dev),
                 "cam": cam, "opt": FusedAdam([{"params": [cam], "lr": self.cam_lr}]),
                 "best": torch.zeros(7, dtype=torch.float32, device=dev),
-                "best_loss": torch.zeros((), dtype=torch.float64, device=dev)}
+                "best_loss": torch.zeros((), dtype=torch.float64, device=dev), "out": out}
+            st["opt"].init_state()
         cam, opt, best, best_loss = st["cam"], st["opt"], st["best"], st["best_loss"]
         st["depth"].copy_(gt_depth)
         st["color"].copy_(gt_color)
+        st["pre"][:3].copy_(pre_c2w[:3])  # (the bottom row stays [0, 0, 0, 1])
+        speed = prev2_c2w is not None
+        if speed:
+            st["prev2"][:3].copy_(prev2_c2w[:3])
         n, iters = self.tracking_pixels, self.num_cam_iters
 
-        def loop():
-            for _ in range(iters):
+        def frame(zero_lr=False):
+            pre = st["pre"]
+            est = (pre @ torch.linalg.inv_ex(st["prev2"])[0]) @ pre if speed else pre
+            cam0 = camera_tensors(est[None])[0]
+            with torch.no_grad():
+                cam.copy_(cam0)
+                best.copy_(cam0)
+            best_loss.fill_(float("inf"))
+            opt.reset_state()
+            for _ in range(1 if zero_lr else iters):
                 loss = eng.iteration(cam, st["depth"], st["color"], None, opt, n=n, seed=self._draw_seed)
                 better = loss < best_loss
                 best_loss.copy_(torch.where(better, loss, best_loss))
                 best.copy_(torch.where(better, cam.detach(), best))
+            st["out"][:3].copy_(get_camera_from_tensor(best))
 
-        key = (iters, n)
+        key = (iters, n, speed)
         if key not in self._graphs:
-            # one zero-lr eager iteration (camera grad, Adam ticket, draw counter made before capture);
+            # one zero-lr eager iteration (camera grad, Adam ticket, draw counter, caches made before capture);
             # the draw stream is rewound, so the frame draws as it would have eagerly
             ctr = eng.eng.draws(self._draw_seed).counter
             ctr0 = ctr.clone()
-            with torch.no_grad():
-                cam.copy_(camera_tensor)
             opt.param_groups[0]["lr"] = 0.0
-            eng.iteration(cam, st["depth"], st["color"], None, opt, n=n, seed=self._draw_seed)
+            frame(zero_lr=True)
             opt.param_groups[0]["lr"] = self.cam_lr
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                loop()
+                frame()
             self._graphs[key] = g
             ctr.copy_(ctr0)
-        with torch.no_grad():
-            cam.copy_(camera_tensor)
-            best.copy_(camera_tensor)
-        best_loss.fill_(float("inf"))
-        opt.reset_state()
         self._graphs[key].replay()
-        bottom = torch.tensor([[0, 0, 0, 1.0]], dtype=torch.float32, device=dev)
-        return torch.cat([get_camera_from_tensor(best.clone()), bottom], 0)
+        return st["out"].clone()

@@ -449,3 +449,79 @@ def test_scene0000_bundle_adjustment_window5(monkeypatch, path):
     # measured on MI355X: poses <= 2.7e-5, grid deltas <= 7.8e-5, camera gradients <= 3.3e-6
     assert all(v < 1e-4 for k, v in report.items() if k.endswith("_grad")), report
     assert all(v < 1e-3 for v in report.values()), report
+
+
+# ------------------------------------------------------------------------------------------------
+# the bench's own room0 iteration (bench.py Room0Scene): pinned directly, not only transitively
+# ------------------------------------------------------------------------------------------------
+def _bench():
+    from conftest import REPO
+    if REPO not in sys.path:
+        sys.path.insert(0, REPO)
+    import bench
+    return bench
+
+
+def test_room0_bench_iteration_matches_oracle():
+    """configs[1]: the bench's room0 workload (bench.Room0Scene: room0 bound and grids, 5 keyframes x 200
+    pixels, 48 samples, frustum rows of frame 0) — one colour-stage engine iteration with given pixel draws
+    vs the oracle on the same rays: loss and every compact gradient the exchange would see."""
+    bench = _bench()
+    scene = bench.Room0Scene(DEV, 0, cfg=dict(bench.ROOM0), path="autograd")
+    cfg = scene.cfg
+    cam = {k: cfg[k] for k in ("H", "W", "fx", "fy", "cx", "cy")}
+    grids = {k: v.detach().requires_grad_(False) for k, v in scene.grids.items()}
+    sd = {k: v.detach().cpu() for k, v in scene.nice.state_dict().items()}
+    n_per = cfg["pixels"] // cfg["window"]
+    pix = torch.randint(cam["H"] * cam["W"], (cfg["window"] * n_per,), generator=torch.Generator().manual_seed(101))
+    frames = [(d.cpu(), c.cpu(), torch.cat([m.cpu(), torch.tensor([[0, 0, 0, 1.0]])])) for d, c, m in scene.frames]
+    fdev = [(d, c, m) for d, c, m in scene.frames]
+    rows = {k: scene.rows[k] for k in ("grid_middle", "grid_fine", "grid_color")}
+    eng, snap, ray_loss, keep = run_engine(scene.nice, grids, scene.bound, fdev, pix, n_per, cam, "color", rows, 32, 16,
+                                           ("color",))
+    ro, rd, gd, gc, k_ref = oracle_batch(frames, pix, n_per, cam, scene.bound)
+    assert torch.equal(keep.bool().cpu(), k_ref)
+    gcpu = {k: v.detach().cpu().contiguous() for k, v in grids.items()}
+    loss, g, dec, _ = oracle_step(sd, gcpu, ro, rd, gd, gc, "color", scene.bound, 32, 16, ("color",))
+    report = {"loss_rel": abs(float(ray_loss.sum()) - loss) / loss, "rays": int(ro.shape[0])}
+    ok = report["loss_rel"] < 1e-5
+    for k in ("grid_middle", "grid_fine", "grid_color"):
+        ok &= check(report, k, snap[k], compact(g[k], rows[k]), TOL[k])
+    ok &= check(report, "color_decoder", snap["dec.color"], decoder_flat(scene.nice, "color", dec), TOL["decoder"])
+    print(json.dumps(report, indent=1))
+    assert ok, report
+
+
+def test_room0_bench_graph_replay_matches_eager():
+    """The bench's timed path itself — device draws, the ray prefetch on the mask-only launch's stream, the
+    merged Adam, iterations replayed from captured hipGraphs (bench.StepGraphs) — against the same
+    iterations launched eagerly from an identical scene: after 4 iterations (2 eager warm-ups inside the
+    capture helper + 2 replays vs 4 eager) the map and colour-decoder UPDATES agree to float-atomic order
+    (which Adam's normalisation lifts to ~1e-5 relative: tolerance 1e-3, as the other loop tests)."""
+    bench = _bench()
+    out = []
+    g0 = d0 = None
+    for replay in (False, True):
+        torch.manual_seed(0)
+        scene = bench.Room0Scene(DEV, 0, cfg=dict(bench.ROOM0), path="fused")
+        if g0 is None:
+            g0 = {k: v.detach().clone() for k, v in scene.grids.items()}
+            d0 = scene.engine.decs["color"].param.detach().clone()
+        if replay:
+            g, mode = bench.capture_step_graphs(scene.step, block=2, sync=scene.flip_parity)
+            assert mode == "hipgraph"
+            g.run(2)
+            g.finish()
+        else:
+            for _ in range(4):
+                scene.step()
+        torch.cuda.synchronize()
+        out.append(({k: v.detach().clone() for k, v in scene.grids.items()},
+                    scene.engine.decs["color"].param.detach().clone(), int(scene.kept)))
+        del scene
+    (ga, da, ka), (gb, db, kb) = out
+    assert ka == kb > 0
+    report = {k: rel_l2(gb[k] - g0[k], ga[k] - g0[k]) for k in ga}
+    report["color_decoder"] = rel_l2(db - d0, da - d0)
+    print(report)
+    assert all(v < 1e-3 for v in report.values()), report

@@ -279,15 +279,12 @@ def test_engine_prefetch_matches_serial(tiny):
     out = {}
     # (prefetch, its stream, one merged Adam): serial; the round-5 default (the prefetch on the mask-only
     # launch's stream, one Adam after both branches); round 4's (its own stream, per-branch Adam)
-    # (+ round 6's lean_main topology: the prefetch ahead of the weight gradients on the side stream, whose
-    # event the caller's stream waits for before Adam — no join)
-    variants = ((False, "lean", True, "wgrad_main"), (True, "lean", True, "wgrad_main"), (True, "own", False, "wgrad_main"),
-                (True, "lean", True, "lean_main"))
+    variants = ((False, "lean", True), (True, "lean", True), (True, "own", False))
     for key in variants:
-        pre, pst, merge, topo = key
+        pre, pst, merge = key
         nice, c = _nice(sc)
         eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV)
-        eng.prefetch_stream, eng.adam_merge, eng.topology = pst, merge, topo
+        eng.prefetch_stream, eng.adam_merge = pst, merge
         opt = P.ops.FusedAdam([{"params": [eng.decs["color"].param], "lr": 0.005}] +
                               [{"params": [c[k]], "lr": 0.005} for k in ("grid_middle", "grid_fine", "grid_color")])
         kept = torch.zeros(1, dtype=torch.int64, device=DEV)
@@ -341,12 +338,11 @@ def test_engine_branch_order_and_concurrency_keep_the_map(tiny):
     the same map, decoder, packed copy and Adam steps (grid atomics order aside)."""
     sc, frames = _frames(tiny)
     out = {}
-    for variant in ("first", "second", "serial", "lean_main"):
+    for variant in ("first", "second", "serial"):
         nice, c = _nice(sc)
         eng = P.engine.MappingEngine(nice, c, sc.bound, 32, 16, device=DEV)
         eng.wgrad_first = variant != "second"
         eng.concurrent = variant != "serial"
-        eng.topology = "lean_main" if variant == "lean_main" else "wgrad_main"
         opt = P.ops.FusedAdam([{"params": [eng.decs["color"].param], "lr": 0.005}] +
                               [{"params": [c[k]], "lr": 0.005} for k in ("grid_middle", "grid_fine", "grid_color")])
         for it in range(3):
@@ -357,7 +353,7 @@ def test_engine_branch_order_and_concurrency_keep_the_map(tiny):
         out[variant] = ({k: v.detach().clone() for k, v in c.items()}, eng.decs["color"].param.detach().clone(),
                         eng.decs["color"].packed.clone(), sorted(float(st["step"]) for st in opt.state.values()))
     b = out["serial"]
-    for v in ("first", "second", "lean_main"):
+    for v in ("first", "second"):
         a = out[v]
         for k in a[0]:
             assert rel_l2(a[0][k], b[0][k]) < 1e-5, (v, k)
