@@ -177,6 +177,10 @@ struct AdamArgs {
 constexpr int kAdamThreads = 256;
 constexpr int kAdamItems = 4;  // float4 rows (or floats) per thread: 4 x 4 loads in flight
 
+// A segment with a device live count (ABI v19 n_live) gets at most kLiveBlocks workgroups, which stride
+// over the live rows: its launch does not scale with the capacity it is sized for.
+constexpr int64_t kLiveBlocks = 512;
+
 // the element update and its coefficients: adam_coef / adam_one (nslam_dev.h)
 __global__ __launch_bounds__(kAdamThreads) void k_adam(AdamArgs a) {
   const int64_t b = blockIdx.x;
@@ -184,9 +188,18 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam(AdamArgs a) {
   while (s + 1 < a.nseg && b >= a.blk0[s + 1]) ++s;
   const nslam_adam_seg& sg = a.seg[s];
   const float step = *sg.step;
-  adam_segment_block<kAdamItems>(
-      sg, [&] { return adam_coef(a.b1, a.b2, a.eps, sg.lr, step); }, b - a.blk0[s], a.zero_grad, (int)threadIdx.x,
-      kAdamThreads);
+  const auto coef = [&] { return adam_coef(a.b1, a.b2, a.eps, sg.lr, step); };
+  if (sg.n_live) {  // stride the live rows (the same per-row update as the one-pass path)
+    nslam_adam_seg live = sg;
+    live.n = *sg.n_live < sg.n ? *sg.n_live : sg.n;
+    live.n_live = nullptr;
+    const int64_t need = adam_segment_blocks<kAdamItems>(live, kAdamThreads);
+    const int64_t assigned = a.blk0[s + 1] - a.blk0[s];
+    for (int64_t lb = b - a.blk0[s]; lb < need; lb += assigned)
+      adam_segment_block<kAdamItems>(live, coef, lb, a.zero_grad, (int)threadIdx.x, kAdamThreads);
+  } else {
+    adam_segment_block<kAdamItems>(sg, coef, b - a.blk0[s], a.zero_grad, (int)threadIdx.x, kAdamThreads);
+  }
   if (a.ticket) {
     // Every workgroup read its segment's step count at its start (the value was consumed long
     // before this point), so once all of them have drawn a ticket no read is outstanding and the
@@ -338,7 +351,8 @@ extern "C" int nslam_adam_step(const nslam_adam_seg* segs, int32_t n_segs, float
       const uintptr_t al = (uintptr_t)g.param | (uintptr_t)g.grad | (uintptr_t)g.exp_avg | (uintptr_t)g.exp_avg_sq;
       if (al & 15) return NSLAM_EINVAL;
     }
-    blocks += adam_segment_blocks<kAdamItems>(g, kAdamThreads);
+    const int64_t nb = adam_segment_blocks<kAdamItems>(g, kAdamThreads);
+    blocks += g.n_live ? (nb < kLiveBlocks ? nb : kLiveBlocks) : nb;
   }
   a.blk0[n_segs] = blocks;
   a.nseg = n_segs;

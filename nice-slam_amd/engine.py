@@ -280,7 +280,7 @@ class MappingEngine:
         return raw
 
     def query_bwd(self, stage, ro, rd, z, g_raw, grid_grads, dec_grads, concurrent=None, pts_grad=False,
-                  on_branch=None, pts_parts=False, ordered_branches=False):
+                  on_branch=None, pts_parts=False, ordered_branches=False, on_pts=None):
         """Backward into the engine's gradient buffers, as independent launches ("branches") that write
         disjoint buffers:
           lean     every decoder's grid gradient (and d/dpts) from the forward's ReLU masks, ONE launch
@@ -300,7 +300,11 @@ class MappingEngine:
         grid and parameters — the per-branch Adam of the mapping iteration.
         ordered_branches: the weight-gradient branch's on_branch starts only after the lean branch's
         on_branch work (not just the lean launch) — for collectives issued there on two communicators,
-        which every rank must then run in the same order (distributed.ShardedAdamExchange)."""
+        which every rank must then run in the same order (distributed.ShardedAdamExchange).
+        on_pts(parts): with pts_grad, called once every decoder's d/dpts share is written — on the lean
+        launch's stream right after it when that launch forms all of them (bundle adjustment's camera
+        gradient then runs beside the weight gradients, not after the join), else on the caller's stream
+        after the join."""
         n = z.numel()
         self._clean = False
         concurrent = self.concurrent if concurrent is None else concurrent
@@ -371,6 +375,11 @@ class MappingEngine:
                             rc = lib().nslam_query_bwd_decoders(ctypes.byref(lc), mask, None, n, ptr(g_raw), gps,
                                                                 st.cuda_stream)
                         check(rc, "nslam_query_bwd_decoders")
+                        if on_pts is not None and pts_grad and set(names) == set(decs):
+                            for name in names:  # (allocated on the caller's stream)
+                                gp[name].record_stream(st)
+                            on_pts([gp[d] for d in decs])
+                            on_pts = None
                         if has_wgrad and self._lean_ev is None:  # one persistent event (never destroyed mid-capture)
                             self._lean_ev = torch.cuda.Event()
                         if has_wgrad and not ordered_branches:
@@ -417,6 +426,8 @@ class MappingEngine:
                     on_branch(["color"], part="all")
             for st in used:
                 main.wait_stream(st)
+            if on_pts is not None and pts_grad:
+                on_pts([gp[d] for d in decs])
             if merged_names is not None:
                 # NSLAM_ADAM_ON=main: the merged update on the main stream after the join (the weight
                 # gradients ran on it; the join covers the lean launch), so the next iteration's forward
@@ -480,10 +491,12 @@ class MappingEngine:
         and draws its own batch.  With prefetch the returned `keep` is a persistent buffer, valid
         until the next iteration() call (which overwrites it): clone it to keep it longer.
         post_bwd(g_pts parts, rays_o, rays_d, z): the backward also forms d loss / d pts (every decoder's
-        share, a list of [N*S, 3] float64) and this runs on the main stream once the whole backward is
-        done, before the main-stream Adam — bundle adjustment's camera gradients and camera step
-        (Mapper.py:346-363, 503-504).  Camera poses that change in place make prefetch invalid: pass
-        prefetch=False with it.
+        share, a list of [N*S, 3] float64) and this runs as soon as they are written (on the mask-only
+        launch's stream, beside the weight gradients; query_bwd on_pts) — bundle adjustment's camera
+        gradients and camera step (Mapper.py:346-363, 503-504).  Its work must be ordered before the
+        next iteration by the join (it is: it runs on a stream the join covers).  Camera poses that a step changes in place make a prefetched batch
+        stale (the version check cannot see a kernel's writes): the caller passes prefetch=False whenever
+        its camera step can move them (Mapper: the colour stage, where their lr is not 0).
         """
         H, W = hw
         fx, fy, cx, cy = intrinsics
@@ -507,7 +520,7 @@ class MappingEngine:
                              out=None if out is None else out[5])
             return [ro, rd, gd, gc, keep, z]
 
-        prefetch = prefetch and pix is None and post_bwd is None
+        prefetch = prefetch and pix is None
         side = None
         if prefetch:
             # A prefetched batch is only valid for the very frames (images and poses, unmodified) it was
@@ -587,8 +600,9 @@ class MappingEngine:
                 if sub:
                     optimizer.step(grads=sub, zero_grad=clean)
 
-        gps = self.query_bwd(stage, ro, rd, z, g_raw, keys, dnames, on_branch=on_branch, ordered_branches=sharded,
-                             pts_grad=post_bwd is not None, pts_parts=True)
+        on_pts = (lambda parts: post_bwd(parts, ro, rd, z)) if post_bwd is not None else None
+        self.query_bwd(stage, ro, rd, z, g_raw, keys, dnames, on_branch=on_branch, ordered_branches=sharded,
+                       pts_grad=post_bwd is not None, pts_parts=True, on_pts=on_pts)
         if sharded:
             pass
         elif exchange is not None:  # frustum-compacted all-reduce (distributed.SparseGradExchange)
@@ -597,8 +611,6 @@ class MappingEngine:
             allreduce([self.gbuf] + [self.decs[n].grad for n in dnames])
         if side is not None:  # join: the next call reads the prefetched set
             main.wait_stream(side)
-        if post_bwd is not None:
-            post_bwd(gps if isinstance(gps, list) else [gps], ro, rd, z)
         if on_branch is None:
             optimizer.step(grads=grads, zero_grad=clean)
         self._clean = clean and (not sharded or exchange.leaves_clean)

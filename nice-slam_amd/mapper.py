@@ -452,10 +452,13 @@ class Mapper(object):
         intr = (self.fx, self.fy, self.cx, self.cy)
         tdec = self._trainable()
         ar = torch.arange(H * W, device=dev) if not device_draws else None
-        # device draws without BA: the next iteration's gather + sampler run beside this one's render and
-        # backward (engine prefetch); every run of one stage starts with its own batch (eng._pre reset), so
-        # a captured run holds its whole prefetch chain.  BA rewrites the poses in place: no prefetch.
-        prefetch = device_draws and not ncam
+        # device draws: the next iteration's gather + sampler run beside this one's render and backward
+        # (engine prefetch); every run of one stage starts with its own batch (eng._pre reset), so a
+        # captured run holds its whole prefetch chain.  With BA the poses the rays come from move only in
+        # the colour stage (the cameras' lr is 0 before it, Mapper.py:420-421: their Adam state advances,
+        # the 7-vectors do not), so only colour-stage BA iterations draw their rays serially.
+        def prefetch_for(stage):
+            return device_draws and (not ncam or stage != "color")
 
         def iteration(stage, record=None):
             if ncam:
@@ -469,7 +472,7 @@ class Mapper(object):
                                                                        device=dev, generator=self.generator)[0]
             ray_loss, _ = eng.iteration(stage, frames, pix, n_per, (H, W), intr, opt, trainable_decoders=tdec,
                                         use_gt_in_sampler=not self.coarse_mapper, seed=self._draw_seed,
-                                        post_bwd=post_bwd if ncam else None, prefetch=prefetch)
+                                        post_bwd=post_bwd if ncam else None, prefetch=prefetch_for(stage))
             if record is not None:
                 record(ray_loss)
 

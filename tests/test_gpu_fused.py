@@ -188,6 +188,35 @@ def test_fused_adam_matches_torch():
     assert float(opt.state[b_f]["step"]) == 3.0 and float(opt.state[w_f]["step"]) == 6.0
 
 
+@pytest.mark.parametrize("n_vox", [210, 30000])
+def test_fused_adam_live_count_matches_exact_rows(n_vox):
+    """ABI v19 n_live: a row-masked segment sized for a capacity (row list and Adam state for every voxel,
+    compact gradient [capacity][32]) whose live count is a device word updates exactly what a segment of
+    the live rows alone does — bit for bit — and nothing else; with a capacity far above the live count
+    (30000 voxels: the launch is capped at 512 workgroups that stride the live rows) too."""
+    g = torch.Generator(device=DEV).manual_seed(1)
+    Z = n_vox // 42
+    grid = torch.randn(1, 32, Z, 6, 7, device=DEV, generator=g).contiguous(memory_format=torch.channels_last_3d)
+    nv = grid.shape[2] * 42
+    live = torch.randperm(nv, device=DEV, generator=g)[: nv // 3].sort().values.to(torch.int32)
+    k = live.numel()
+    cap_rows = torch.full((nv,), 7, dtype=torch.int32, device=DEV)   # (entries past k: never read)
+    cap_rows[:k] = live
+    n_live = torch.tensor([k], dtype=torch.int64, device=DEV)
+    ga, gb = grid.clone(), grid.clone()
+    opt_a = P.ops.FusedAdam([{"params": [ga], "lr": 0.05, "rows": live}])
+    opt_b = P.ops.FusedAdam([{"params": [gb], "lr": 0.05, "rows": cap_rows, "n_live": n_live}])
+    for _ in range(4):
+        comp = torch.randn(k, 32, device=DEV, generator=g)
+        cap = torch.randn(nv, 32, device=DEV, generator=g)   # garbage past the live rows
+        cap[:k] = comp
+        opt_a.step(grads={ga: comp.clone()})
+        opt_b.step(grads={gb: cap})
+    assert torch.equal(ga, gb)
+    assert torch.equal(opt_a.state[ga]["exp_avg"], opt_b.state[gb]["exp_avg"][: k * 32])
+    assert float(opt_b.state[gb]["exp_avg"][k * 32:].abs().max()) == 0.0   # state past the live rows untouched
+
+
 def test_engine_iteration_matches_autograd_path(tiny):
     sc, frames = _frames(tiny)
     nice, c = _nice(sc)
