@@ -372,6 +372,27 @@ int nslam_cam_grad_batch(const float* cams, const float* c2w, int64_t c2w_stride
 /* ABI v19: nslam_cam_pose for n cameras in one launch: c2w + k * c2w_stride = get_camera_from_tensor(cams[k]). */
 int nslam_cam_pose_batch(const float* cams, float* c2w, int64_t c2w_stride, int32_t n, void* stream);
 
+/* ABI v20.  The frustum voxel selection of Mapper.get_mask_from_c2w (Mapper.py:93-164) after its two
+ * projection GEMMs, compacted into a capacity-bound row list (what MappingEngine.bind_masks builds with
+ * torch ops, in one pass of four launches).  Inputs in the reference's point order
+ * i = (ix*ny + iy)*nz + iz of its meshgrid: uvz [N][3] float64 = (points @ w2c[:3,:3]ᵀ + w2c[:3,3])
+ * .double() * (-1, 1, 1) @ Kᵀ and near [N] (uint8 bool) = |points - t|² < 0.25, both formed by the
+ * caller; depth [H][W] float32 (the current frame).  Computes uv = (uvz[:2] / (uvz[2] + 1e-5)) as
+ * float, cv2.remap's bilinear depth at uv (1/32-pixel fixed-point positions, zero border), zero depths
+ * replaced by the maximum over all N points, and mask = (0 < u < W, 0 < v < H, 0 <= -z <= depth + 0.5)
+ * | near; then, over voxels v = (iz*ny + iy)*nx + ix (channels-last order): slot[v] = the rank of v among
+ * the selected voxels or -1, rows[rank] = v (ascending), *n_live = their count.  mask_ref: optional [N]
+ * uint8 mask in the reference order.  ws: nslam_frustum_rows_workspace_size(N) bytes. */
+int nslam_frustum_rows(const double* uvz, const uint8_t* near, const float* depth, int32_t H, int32_t W, int32_t nx,
+                       int32_t ny, int32_t nz, int32_t* slot, int32_t* rows, int64_t* n_live, uint8_t* mask_ref,
+                       void* ws, size_t ws_bytes, void* stream);
+size_t nslam_frustum_rows_workspace_size(int64_t n_vox);
+
+/* ABI v20.  The tracker's best-pose bookkeeping of one camera iteration (Tracker.py:245-247: if loss <
+ * best_loss: best_loss = loss, candidate = camera_tensor), on the device: if *loss < *best_loss (float64),
+ * *best_loss = *loss and best[0..n) = cam[0..n) (n <= 64, float32).  One single-wave launch. */
+int nslam_track_best(const double* loss, double* best_loss, const float* cam, float* best, int32_t n, void* stream);
+
 /* ABI v9.  c2w [3,4] f32 = get_camera_from_tensor(cam [7]) (common.py:137-176, quad2rotation's
  * products and differences, no FMA contraction), one thread.  |q|² is summed ((w²+x²)+y²)+z²;
  * the order of torch's (quad*quad).sum(-1) reduction is not pinned, so the pose matches the

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NSLAM_LIB") or os.path.join(_HERE, "libnslam.so")  # NSLAM_LIB: instrumented builds
 
 NSLAM_OK = 0
-ABI_VERSION = 19
+ABI_VERSION = 20
 STAGES = {"coarse": 0, "middle": 1, "fine": 2, "color": 3}
 DEC_COARSE, DEC_MIDDLE, DEC_FINE, DEC_COLOR = 0, 1, 2, 3
 
@@ -117,7 +117,7 @@ EXPORTS = (
     "nslam_render_loss_workspace_size", "nslam_adam_step", "nslam_rows_pack", "nslam_rows_unpack",
     "nslam_query_fwd_ws", "nslam_query_fwd_workspace_size", "nslam_cam_grad", "nslam_cam_pose",
     "nslam_query_tape_size", "nslam_color_wgrad", "nslam_cam_grad_parts", "nslam_cam_grad_batch",
-    "nslam_cam_pose_batch",
+    "nslam_cam_pose_batch", "nslam_frustum_rows", "nslam_frustum_rows_workspace_size", "nslam_track_best",
 )
 
 _lib = None
@@ -182,6 +182,10 @@ def lib():
         L.nslam_cam_grad_batch.argtypes = [vp, vp, i64, i32, ctypes.POINTER(i64), i64, ctypes.POINTER(vp), i32, vp, vp,
                                            i64, i32, vp, vp, vp, vp]
         L.nslam_cam_pose_batch.argtypes = [vp, vp, i64, i32, vp]
+        L.nslam_frustum_rows.argtypes = [vp, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, sz, vp]
+        L.nslam_frustum_rows_workspace_size.argtypes = [i64]
+        L.nslam_frustum_rows_workspace_size.restype = sz
+        L.nslam_track_best.argtypes = [vp, vp, vp, vp, i32, vp]
         if L.nslam_abi_version() != ABI_VERSION:
             raise RuntimeError(f"libnslam.so ABI {L.nslam_abi_version()} != {ABI_VERSION}: rebuild it")
         _lib = L

@@ -719,6 +719,29 @@ extern "C" int nslam_cam_pose(const float* cam, float* c2w, void* stream) {
   return e == hipSuccess ? NSLAM_OK : NSLAM_EHIP - (int)e;
 }
 
+namespace {
+
+// One wave: lanes read the loss and the best loss before lane 0 stores (one instruction stream), so no lane
+// sees a half-updated best.
+__global__ __launch_bounds__(64) void k_track_best(const double* __restrict__ loss, double* __restrict__ best_loss,
+                                                   const float* __restrict__ cam, float* __restrict__ best, int n) {
+  const double l = *loss, b = *best_loss;
+  if (!(l < b)) return;  // (NaN: not better, as torch's comparison)
+  if ((int)threadIdx.x < n) best[threadIdx.x] = cam[threadIdx.x];
+  if (threadIdx.x == 0) *best_loss = l;
+}
+
+}  // namespace
+
+extern "C" int nslam_track_best(const double* loss, double* best_loss, const float* cam, float* best, int32_t n,
+                                void* stream) {
+  if (!loss || !best_loss || !cam || !best || n < 1 || n > 64) return NSLAM_EINVAL;
+  hipLaunchKernelGGL(k_track_best, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), loss, best_loss, cam,
+                     best, (int)n);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? NSLAM_OK : NSLAM_EHIP - (int)e;
+}
+
 extern "C" int nslam_cam_pose_batch(const float* cams, float* c2w, int64_t c2w_stride, int32_t n, void* stream) {
   if (!cams || !c2w || n < 1 || n > 64 || c2w_stride < 12) return NSLAM_EINVAL;
   hipLaunchKernelGGL(k_cam_pose_batch, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), cams, c2w,

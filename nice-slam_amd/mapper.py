@@ -67,6 +67,49 @@ def _intrinsics(fx, fy, cx, cy, dev):
     return _KMAT[key]
 
 
+_POINTS = {}
+
+
+def _grid_points(bound, val_shape, dev):
+    """The grid's voxel positions in get_mask_from_c2w's meshgrid order [X*Y*Z, 3] (cached per shape)."""
+    b = bound
+    key = (tuple(float(v) for v in torch.as_tensor(b).reshape(-1)), tuple(int(v) for v in val_shape), str(dev))
+    if key not in _POINTS:
+        nz, ny, nx = (int(v) for v in val_shape)
+        X, Y, Z = torch.meshgrid(torch.linspace(float(b[0][0]), float(b[0][1]), nx, device=dev),
+                                 torch.linspace(float(b[1][0]), float(b[1][1]), ny, device=dev),
+                                 torch.linspace(float(b[2][0]), float(b[2][1]), nz, device=dev), indexing="ij")
+        _POINTS[key] = torch.stack([X, Y, Z], dim=-1).reshape(-1, 3)
+    return _POINTS[key]
+
+
+def frustum_rows_device(c2w, val_shape, depth, bound, H, W, fx, fy, cx, cy, slot, rows, n_live, mask_ref=None):
+    """frustum_mask fused with its compaction (ABI v20 nslam_frustum_rows): slot [Z*Y*X] int32, rows (>= the
+    voxel count) int32 and n_live int64 [1] are written in place, as MappingEngine.bind_masks would from the
+    mask.  The two projection GEMMs and the near-camera test run here with frustum_mask's own torch ops (the
+    same values bit for bit); the remap, the depth tests and the compaction run in one kernel sequence.
+    mask_ref: optional uint8 [X*Y*Z] receiving the mask in frustum_mask's order."""
+    from ._lib import check, lib, ptr, stream_ptr
+    dev = depth.device
+    points = _grid_points(bound, val_shape, dev)
+    c2w = c2w.to(dev).float()
+    w2c = torch.linalg.inv_ex(c2w)[0]
+    cam = points @ w2c[:3, :3].T + w2c[:3, 3]
+    cam = cam.double()
+    cam[:, 0] *= -1
+    uvz = cam @ _intrinsics(fx, fy, cx, cy, dev).T
+    d = points - c2w[:3, 3]
+    near = ((d * d).sum(1) < 0.5 * 0.5).to(torch.uint8)
+    nz, ny, nx = (int(v) for v in val_shape)
+    n = nx * ny * nz
+    wsb = lib().nslam_frustum_rows_workspace_size(n)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    dep = depth.float().contiguous()
+    rc = lib().nslam_frustum_rows(ptr(uvz.contiguous()), ptr(near), ptr(dep), H, W, nx, ny, nz, ptr(slot), ptr(rows),
+                                  ptr(n_live), ptr(mask_ref), ptr(ws), wsb, stream_ptr(dev))
+    check(rc, "nslam_frustum_rows")
+
+
 def frustum_mask(c2w, key, val_shape, depth, bound, H, W, fx, fy, cx, cy):
     """Mapper.get_mask_from_c2w (Mapper.py:93-164) on the device: bool mask [X, Y, Z] of the
     grid voxels inside the camera frustum up to the observed depth + 0.5 m, or within 0.5 m of
@@ -306,6 +349,33 @@ class Mapper(object):
             self._graphs.clear()  # (captured against the old slots)
         return self._slots
 
+    def _bind_frustum(self, eng, c2w, depth):
+        """This call's frustum selection bound into the engine's capacity buffers (Mapper.py:314-333): the
+        fused kernel (nslam_frustum_rows) per grid shape, the other grids of that shape copying its rows;
+        the coarse grid (an all-true mask, Mapper.py:113-115) and frustum_feature_selection=False through
+        bind_masks.  get_mask_from_c2w replaced on the instance (a test hook) also goes through bind_masks."""
+        keys = self._grid_keys()
+        if (not self.frustum_feature_selection or self.coarse_mapper
+                or "get_mask_from_c2w" in self.__dict__):
+            eng.bind_masks(self._call_masks(c2w, depth))
+            return
+        if getattr(eng, "_cap_keys", None) != tuple(sorted(keys)):
+            eng.bind_masks({k: None for k in keys})  # (first call: the capacity buffers)
+        done = {}
+        for k in keys:
+            shp = tuple(self.c[k].shape[2:])
+            rows, n_live = eng.live_rows(k)
+            slot = eng.slot[k]
+            if shp in done:
+                s0, r0, n0 = done[shp]
+                slot.copy_(s0)
+                rows.copy_(r0)
+                n_live.copy_(n0)
+            else:
+                frustum_rows_device(c2w, shp, depth, self.bound, self.H, self.W, self.fx, self.fy, self.cx, self.cy,
+                                    slot, rows, n_live)
+                done[shp] = (slot, rows, n_live)
+
     def _call_masks(self, c2w, depth):
         """This call's frustum masks (Mapper.py:314-333; None = every voxel): grids of one shape share one."""
         masks, by_shape = {}, {}
@@ -375,7 +445,7 @@ class Mapper(object):
                 st["poses"][:len(kfs)].copy_(torch.stack([kf["est_c2w"].to(dev).float()[:4] for kf in kfs]))
 
             def setup():
-                eng.bind_masks(self._call_masks(st["c2w"], st["depth"]))
+                self._bind_frustum(eng, st["c2w"], st["depth"])
                 o = self._optimizer(eng)
                 o.init_state()
                 o.reset_state()
@@ -396,7 +466,7 @@ class Mapper(object):
             g.replay()
             opt = self._optimizer(eng)
         else:
-            eng.bind_masks(self._call_masks(cur_c2w, cur_gt_depth))
+            self._bind_frustum(eng, cur_c2w, cur_gt_depth)
             opt = self._optimizer(eng)
             opt.reset_state()
         mark("masks")

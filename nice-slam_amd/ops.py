@@ -692,6 +692,15 @@ def cam_pose_batch(cams, c2w):
     return c2w
 
 
+def track_best(loss, best_loss, cam, best):
+    """nslam_track_best (ABI v20): if loss < best_loss (float64 device scalars): best_loss = loss, best = cam."""
+    if loss.dtype != torch.float64 or best_loss.dtype != torch.float64 or cam.dtype != torch.float32 \
+            or best.shape != cam.shape or not (cam.is_contiguous() and best.is_contiguous()):
+        raise ValueError("track_best: float64 scalars and two contiguous float32 vectors of one shape")
+    check(lib().nslam_track_best(ptr(loss), ptr(best_loss), ptr(cam), ptr(best), cam.numel(), stream_ptr(cam.device)),
+          "nslam_track_best")
+
+
 def cam_grad_batch(cams, c2w, ray_begin, n_per, g_pts, z, rd, out, ws, tickets):
     """nslam_cam_grad_batch (ABI v19): out [n, 7] = d loss / d cams [n, 7] of the bundle-adjustment cameras,
     camera k's rays being [ray_begin[k], ray_begin[k] + n_per) of the batch (z [N, S] f64, rd [N, 3] f32,

@@ -208,7 +208,7 @@ class Tracker(object):
         guess (constant speed, Tracker.py:191-198), its camera 7-vector, a fresh Adam, the camera loop with
         device pixel draws and the device-side best-pose selection (Tracker.py:225-250), and the result pose.
         Per frame the host copies the frame and the previous poses into persistent buffers and replays."""
-        from .ops import FusedAdam
+        from .ops import FusedAdam, track_best
         eng = self.engine()
         dev = self.device
         st = self._fstate
@@ -243,9 +243,7 @@ class Tracker(object):
             opt.reset_state()
             for _ in range(1 if zero_lr else iters):
                 loss = eng.iteration(cam, st["depth"], st["color"], None, opt, n=n, seed=self._draw_seed)
-                better = loss < best_loss
-                best_loss.copy_(torch.where(better, loss, best_loss))
-                best.copy_(torch.where(better, cam.detach(), best))
+                track_best(loss, best_loss, cam.detach(), best)  # (Tracker.py:245-247, one launch)
             st["out"][:3].copy_(get_camera_from_tensor(best))
 
         key = (iters, n, speed)

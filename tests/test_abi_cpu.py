@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_strerror(pkg):
     L = pkg._lib.lib()
-    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 19
+    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 20
     assert L.nslam_strerror(0) == b"ok"
     assert b"invalid" in L.nslam_strerror(-1)
 
@@ -245,3 +245,20 @@ def test_v19_cam_batch_validates_without_gpu(pkg):
     assert L.nslam_cam_pose_batch(None, 64, 16, 2, None) == -1
     assert L.nslam_cam_pose_batch(64, 64, 16, 0, None) == -1
     assert L.nslam_cam_pose_batch(64, 64, 8, 2, None) == -1
+
+
+def test_v20_frustum_rows_validates_without_gpu(pkg):
+    L = pkg._lib.lib()
+    need = L.nslam_frustum_rows_workspace_size(10 * 12 * 20)
+    assert need > 2400 * 5 and L.nslam_frustum_rows_workspace_size(0) == 0
+    args = [64, 64, 64, 680, 1200, 20, 12, 10, 64, 64, 64, None, 64, need, None]
+    for i in (0, 1, 2, 8, 9, 10):  # a missing input / output buffer
+        a = list(args)
+        a[i] = None
+        assert L.nslam_frustum_rows(*a) == -1, i
+    a = list(args)
+    a[5] = 0                            # an empty grid axis
+    assert L.nslam_frustum_rows(*a) == -1
+    a = list(args)
+    a[13] = need - 1                    # short workspace
+    assert L.nslam_frustum_rows(*a) == -3

@@ -249,3 +249,47 @@ def test_keyframe_overlap_device_matches_reference(loop, monkeypatch):
     np.random.seed(int(loop["overlap.np_seed"]))
     sel = mp.keyframe_selection_overlap(color, depth, torch.from_numpy(cur).to(DEV), kf, int(loop["overlap.k"]))
     assert [int(s) for s in sel] == [int(s) for s in loop["overlap.selected"]]
+
+
+def test_frustum_rows_kernel_matches_mask(loop):
+    """ABI v20 nslam_frustum_rows (the remap, depth tests and compaction in one kernel sequence) at room0
+    shapes: its mask equals the reference's get_mask_from_c2w fixture and mapper.frustum_mask (torch) bit
+    for bit, on the fixture's pose and on 6 more (random look directions, a zero-depth patch); rows are the
+    ascending channels-last nonzeros of that mask, slot their inverse, n_live their count."""
+    b, poses, cur = scenes.room0_window()
+    cam = scenes.ROOM0_CAM
+    bound = torch.from_numpy(b)
+    depth0 = torch.from_numpy(scenes.box_depth(cur, cam, b, seed=int(loop["frustum.depth_seed"]))).to(DEV)
+    cases = [(torch.from_numpy(cur), depth0, "fixture")]
+    g = np.random.default_rng(3)
+    ctr = b.mean(1)
+    for k in range(6):
+        c2w = scenes.look_pose(ctr, float(g.uniform(0, 6.28)), float(g.uniform(-0.4, 0.4)),
+                               tuple(float(v) for v in g.uniform(-0.6, 0.6, 3)))
+        d = torch.from_numpy(scenes.box_depth(c2w, cam, b, seed=40 + k)).to(DEV)
+        if k % 2:
+            d[100:200, 300:500] = 0  # zero depths take the maximum over all grid points
+        cases.append((torch.from_numpy(c2w), d, f"pose{k}"))
+    for key in ("grid_middle", "grid_fine"):
+        shp = tuple(int(v) for v in loop["frustum.shape." + key])
+        nz, ny, nx = shp
+        n = nx * ny * nz
+        for c2w, d, name in cases:
+            slot = torch.full((n,), -7, dtype=torch.int32, device=DEV)
+            rows = torch.full((n + 1,), -7, dtype=torch.int32, device=DEV)
+            n_live = torch.zeros(1, dtype=torch.int64, device=DEV)
+            mref = torch.zeros(n, dtype=torch.uint8, device=DEV)
+            P.mapper.frustum_rows_device(c2w.to(DEV), shp, d, bound, cam["H"], cam["W"], cam["fx"], cam["fy"],
+                                         cam["cx"], cam["cy"], slot, rows, n_live, mask_ref=mref)
+            m = P.mapper.frustum_mask(c2w.to(DEV), key, shp, d, bound, cam["H"], cam["W"], cam["fx"], cam["fy"],
+                                      cam["cx"], cam["cy"])
+            assert torch.equal(mref.bool().reshape(nx, ny, nz), m), (key, name)
+            if name == "fixture":
+                assert np.array_equal(mref.bool().reshape(nx, ny, nz).cpu().numpy(), loop["frustum.mask." + key])
+            want = P.engine.frustum_rows(m)
+            k = int(n_live)
+            assert k == want.numel() > 0, (key, name)
+            assert torch.equal(rows[:k], want), (key, name)
+            inv = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+            inv[want.long()] = torch.arange(k, dtype=torch.int32, device=DEV)
+            assert torch.equal(slot, inv), (key, name)
