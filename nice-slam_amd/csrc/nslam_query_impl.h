@@ -988,15 +988,14 @@ __device__ __forceinline__ void noxyz_backward(const float* __restrict__ pk, con
 // TR: dc is formed transposed (lane (c, h) register r = channel c of point F(r, h); gemm_acc_t), the
 // layout the lean scatter walk consumes without an LDS transpose (only without EMBG: coord_grad
 // reads the C layout)
-// stash, img (EMBG; the d/dpts mask-only kernels): this wave's LDS scratch — mask_3(dh_3), which the
-// Fourier backward reads after the rest of the chain, waits in stash (1024 floats) and dc, complete
-// before the Fourier backward, goes to the caller's scatter image img (tstore layout) then, so neither
-// holds 16 registers through it (the caller reads dc back from img: tload)
+// img (EMBG; the d/dpts mask-only kernels): the caller's scatter image — dc, complete before the Fourier
+// backward, is stored there (tstore layout) and does not hold 16 registers through it (the caller's
+// scatter reads it there; its coordinate gradient reads it back: tload)
 template <int NC, int NOUT, int GOFS, bool EMBG, bool TR = false>
 __device__ __forceinline__ void xyz_backward_saved(const float* __restrict__ pk, const uint32_t m[5],
                                                    const float x[3], const float (&gall)[4], int lane, f32x16& dc,
                                                    float gx[3], const float* gh4 = nullptr,
-                                                   float* __restrict__ stash = nullptr, float* __restrict__ img = nullptr) {
+                                                   float* __restrict__ img = nullptr) {
   static_assert(!(TR && EMBG), "d/dpts needs dc in the C layout");
   const XyzPack L{NC};
   const int h = lane >> 5;
@@ -1014,14 +1013,9 @@ __device__ __forceinline__ void xyz_backward_saved(const float* __restrict__ pk,
   dh = zero16();
   gemm_acc(dh, pk + L.L4T() * NSLAM_FRAG, da, lane);
   gemm_acc_tr<TR>(dc, pk + L.FCT(3) * NSLAM_FRAG, dh, lane);
-  f32x16 da3 = apply_mask(dh, m[3]);
+  const f32x16 da3 = apply_mask(dh, m[3]);
   dh = zero16();
   gemm_acc(dh, pk + (L.L3T() + 3) * NSLAM_FRAG, da3, lane);
-  if (EMBG && stash) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) stash[r * 64 + lane] = da3[r];
-    asm volatile("" ::: "memory");  // (read back below, not forwarded: the registers are free meanwhile)
-  }
   gemm_acc_tr<TR>(dc, pk + L.FCT(2) * NSLAM_FRAG, dh, lane);
   da = apply_mask(dh, m[2]);
   dh = zero16();
@@ -1036,12 +1030,7 @@ __device__ __forceinline__ void xyz_backward_saved(const float* __restrict__ pk,
     da = apply_mask(dh, m[0]);
     if (img) {
       tstore(img, dc, lane);
-      asm volatile("" ::: "memory");
-    }
-    if (stash) {
-      asm volatile("" ::: "memory");
-#pragma unroll
-      for (int r = 0; r < 16; ++r) da3[r] = stash[r * 64 + lane];
+      asm volatile("" ::: "memory");  // (read back after the scatter, not kept in registers meanwhile)
     }
     const float* FB = pk + L.FB();
 #pragma unroll
@@ -1928,15 +1917,9 @@ constexpr int kMaxSlabs = 4096;  // WG == 2 above this many tiles
 // lean mapping tile (saved masks, no weight or point gradients): dc transposed, walk without LDS image
 constexpr bool lean_tr(int WG, bool PG, bool SAVED) { return SAVED && WG == 0 && !PG; }
 // per-wave LDS floats of a backward kernel variant
-// d/dpts mask-only tile (saved masks, point gradients): dc and mask_3(dh_3) wait in LDS through the
-// Fourier backward (xyz_backward_saved's img / stash)
-constexpr bool pg_stash(int WG, bool PG, bool SAVED) { return SAVED && WG == 0 && PG; }
-constexpr int kStashFloats = 1024;
 // per-wave LDS floats of a backward kernel variant
 constexpr int bwd_scratch_floats(int WG, bool PG, bool SAVED) {
-  return WG ? kScratchFloats
-            : lean_tr(WG, PG, SAVED) ? kWalkFloats
-                                     : TILE_FLOATS + kWalkFloats + (pg_stash(WG, PG, SAVED) ? kStashFloats : 0);
+  return WG ? kScratchFloats : lean_tr(WG, PG, SAVED) ? kWalkFloats : TILE_FLOATS + kWalkFloats;
 }
 
 template <int DEC, int WG, bool PG, bool FIRST, bool SAVED>
@@ -1988,11 +1971,10 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
   // the lean mapping chain forms dc transposed for the register-only scatter walk (lean_tr)
   constexpr bool TR = lean_tr(WG, PG, SAVED);
   float* const tab = TR ? S.sA : S.sA + TILE_FLOATS;  // the walk table (after the transpose image if any)
-  // d/dpts mask-only tiles (not the coarse decoder's: its chain keeps dc in registers): dc in the scatter
-  // image and mask_3(dh_3) in the stash after the walk table while the Fourier backward runs
-  constexpr bool STASH = pg_stash(WG, PG, SAVED) && DEC != NSLAM_DEC_COARSE;
-  float* const stash = STASH ? S.sA + TILE_FLOATS + kWalkFloats : nullptr;
-  float* const img = STASH ? S.sA : nullptr;
+  // d/dpts mask-only tiles (not the coarse decoder's: its chain keeps dc in registers): dc waits in the
+  // scatter image while the Fourier backward runs
+  constexpr bool IMGDC = SAVED && WG == 0 && PG && DEC != NSLAM_DEC_COARSE;
+  float* const img = IMGDC ? S.sA : nullptr;
   if (SAVED) {  // masks from the forward: no recompute (the mask-only chain)
     uint32_t m[5];
     load_masks(a, DEC, tile, m, lane);
@@ -2002,11 +1984,11 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
     if (DEC == NSLAM_DEC_COARSE) {
       noxyz_backward_saved<TR>(pk, m, g[3], lane, dc);
     } else if (DEC == NSLAM_DEC_FINE) {
-      xyz_backward_saved<2, 1, 3, PG, TR>(pk, m, q.x, g, lane, dc, gx, nullptr, stash, img);
+      xyz_backward_saved<2, 1, 3, PG, TR>(pk, m, q.x, g, lane, dc, gx, nullptr, img);
     } else if (DEC == NSLAM_DEC_COLOR) {
-      xyz_backward_saved<1, 3, 0, PG, TR>(pk, m, q.x, g, lane, dc, gx, gh4, stash, img);
+      xyz_backward_saved<1, 3, 0, PG, TR>(pk, m, q.x, g, lane, dc, gx, gh4, img);
     } else {
-      xyz_backward_saved<1, 1, 3, PG, TR>(pk, m, q.x, g, lane, dc, gx, nullptr, stash, img);
+      xyz_backward_saved<1, 1, 3, PG, TR>(pk, m, q.x, g, lane, dc, gx, nullptr, img);
     }
   } else if (DEC == NSLAM_DEC_COARSE) {
     const f32x16 c = gather_tile(gr.data, cr, lane);
@@ -2030,7 +2012,7 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
     if (WG) {
       scatter_grid_grad_halves(gr.grad, gr.slot, cr, dc, q.valid, S, lane);
     } else {  // walk table: the lean kernels' slot after the transpose image
-      scatter_grid_grad_uniform<SAVED, TR, STASH>(gr.grad, scn, cr.cell, dc, S.sA, tab, lane);
+      scatter_grid_grad_uniform<SAVED, TR, IMGDC>(gr.grad, scn, cr.cell, dc, S.sA, tab, lane);
     }
   }
   PHASE(DEC, 13);
@@ -2044,7 +2026,7 @@ __device__ __forceinline__ void dec_bwd_tile(const QueryKArgs& a, int64_t tile, 
       for (int k = 0; k < 3; ++k) asm volatile("" : "+v"(q2.p[k]));
       grid_corners(cr, gr, q2);
     }
-    if (STASH) {
+    if (IMGDC) {
       lds_sync();  // (the scatter read the image; the reads below are this wave's own stores)
       dc = tload(S.sA, lane);
     }
@@ -2132,8 +2114,8 @@ struct MultiDecArgs {
 #define NSLAM_MULTI_LB 4
 #endif
 #ifndef NSLAM_MULTI_PG_LB
-#define NSLAM_MULTI_PG_LB 3  // the d/dpts (tracking, bundle adjustment) variant: 163 VGPRs with dc and
-                             // mask_3(dh_3) in LDS through the Fourier backward (218 before: 2 waves/SIMD)
+#define NSLAM_MULTI_PG_LB 3  // the d/dpts (tracking, bundle adjustment) variant: 163 VGPRs with dc in the
+                             // scatter image through the Fourier backward (218 before: 2 waves/SIMD)
 #endif
 template <bool PG>
 __global__ __launch_bounds__(64 * kWavesBwd, PG ? NSLAM_MULTI_PG_LB : NSLAM_MULTI_LB) void k_dec_bwd_multi(QueryKArgs a, MultiDecArgs m) {
