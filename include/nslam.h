@@ -392,6 +392,13 @@ size_t nslam_frustum_rows_workspace_size(int64_t n_vox);
  * best_loss: best_loss = loss, candidate = camera_tensor), on the device: if *loss < *best_loss (float64),
  * *best_loss = *loss and best[0..n) = cam[0..n) (n <= 64, float32).  One single-wave launch. */
 int nslam_track_best(const double* loss, double* best_loss, const float* cam, float* best, int32_t n, void* stream);
+/* ABI v21.  The camera iteration's loss and its best-pose bookkeeping in one launch: *loss_out = the sum of
+ * ray_loss[0..n_rays) (float64; a fixed-order tree over one workgroup: the same value every call), then,
+ * when best_loss is not NULL, nslam_track_best's update with that sum (cam, best: n <= 64 float32).
+ * Replaces optimize_cam_in_batch's loss.sum() (Tracker.py:110-123) and the comparison of Tracker.py:245-247,
+ * so the tracker's camera loop needs no reduction launch of its own. */
+int nslam_loss_sum_best(const double* ray_loss, int64_t n_rays, double* loss_out, double* best_loss, const float* cam,
+                        float* best, int32_t n, void* stream);
 
 /* ABI v9.  c2w [3,4] f32 = get_camera_from_tensor(cam [7]) (common.py:137-176, quad2rotation's
  * products and differences, no FMA contraction), one thread.  |q|² is summed ((w²+x²)+y²)+z²;

@@ -533,6 +533,16 @@ __device__ __forceinline__ void cam_grad_parts_body(const CamPartsArgs& a, unsig
     for (int k = 0; k < 12; ++k) red[k][wave] = acc[k];
   }
   __syncthreads();
+  if (nwg == 1) {  // one workgroup: no partials to publish, no hand-over
+    if (threadIdx.x < 12) {
+      double t = 0.0;
+      for (int w = 0; w < kCamThreads / 64; ++w) t += red[threadIdx.x][w];
+      red[threadIdx.x][0] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) cam_grad_epilogue(a.cam, a.c2w, red, a.g_cam);
+    return;
+  }
   if (threadIdx.x < 12) {  // fixed-order sum over the waves, published as this workgroup's partial
     double t = 0.0;
     for (int w = 0; w < kCamThreads / 64; ++w) t += red[threadIdx.x][w];
@@ -732,6 +742,42 @@ __global__ __launch_bounds__(64) void k_track_best(const double* __restrict__ lo
 }
 
 }  // namespace
+
+namespace {
+// the loss of a camera iteration (fixed-order sum over one workgroup) and, optionally, the best-pose update
+constexpr int kSumThreads = 256;
+__global__ __launch_bounds__(kSumThreads) void k_loss_sum_best(const double* __restrict__ rl, int64_t n,
+                                                              double* __restrict__ out, double* __restrict__ best_loss,
+                                                              const float* __restrict__ cam, float* __restrict__ best,
+                                                              int nc) {
+  __shared__ double s[kSumThreads];
+  double t = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += kSumThreads) t += rl[i];
+  s[threadIdx.x] = t;
+  __syncthreads();
+  for (int w = kSumThreads / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
+    __syncthreads();
+  }
+  const double l = s[0];
+  if (threadIdx.x == 0) *out = l;
+  if (!best_loss) return;
+  if (!(l < *best_loss)) return;  // (NaN: not better, as torch's comparison)
+  __syncthreads();                // (every thread has read *best_loss before it is replaced)
+  if ((int)threadIdx.x < nc) best[threadIdx.x] = cam[threadIdx.x];
+  if (threadIdx.x == 0) *best_loss = l;
+}
+}  // namespace
+
+extern "C" int nslam_loss_sum_best(const double* ray_loss, int64_t n_rays, double* loss_out, double* best_loss,
+                                   const float* cam, float* best, int32_t n, void* stream) {
+  if (!loss_out || n_rays < 0 || (n_rays > 0 && !ray_loss)) return NSLAM_EINVAL;
+  if (best_loss && (!cam || !best || n < 1 || n > 64)) return NSLAM_EINVAL;
+  hipLaunchKernelGGL(k_loss_sum_best, dim3(1), dim3(kSumThreads), 0, reinterpret_cast<hipStream_t>(stream), ray_loss,
+                     n_rays, loss_out, best_loss, cam, best, (int)n);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? NSLAM_OK : NSLAM_EHIP - (int)e;
+}
 
 extern "C" int nslam_track_best(const double* loss, double* best_loss, const float* cam, float* best, int32_t n,
                                 void* stream) {

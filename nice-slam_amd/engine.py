@@ -676,17 +676,20 @@ class TrackingEngine:
         # multi-workgroup camera-gradient kernel (no torch adds, no single-workgroup reduction)
         self.cam_parts = True
         self._cam_ws = self._cam_ticket = None
+        self._loss = None  # the last iteration's loss (device f64 scalar, overwritten by the next one)
 
     def n_window(self):
         h0, h1, w0, w1 = self.window
         return (h1 - h0) * (w1 - w0)
 
-    def iteration(self, cam, depth, color, pix, optimizer, n=None, seed=0):
+    def iteration(self, cam, depth, color, pix, optimizer, n=None, seed=0, best=None):
         """One camera iteration on frame (depth [H,W], color [H,W,3]) with pixel draws `pix`
         (int64 [n], select_uv indices into the edge-cropped window), or pix=None: n pixels drawn inside
         the gather kernel (uniform over the window, stream `seed`; capturable in a hipGraph).  cam: [7]
         leaf tensor whose .grad the optimizer reads.  Returns the loss (device f64 scalar) of the pose
-        BEFORE the step."""
+        BEFORE the step: the kept rays' losses summed in a fixed order (nslam_loss_sum_best; a buffer the
+        next call overwrites), which with best = (best_loss, best_cam) also keeps the best pose
+        (Tracker.py:245-247) in the same launch."""
         fx, fy, cx, cy = self.intr
         n = pix.numel() if pix is not None else int(n)
         draw = self.eng.draws(seed) if pix is None else None
@@ -716,7 +719,16 @@ class TrackingEngine:
             # the whole pts → rays → c2w → 7-vector chain in one launch
             ops.cam_grad(cam.detach(), c2w, g_pts, z, rd, cam.grad)
         optimizer.step()
-        return ray_loss.sum()
+        # the loss of the pose before the step (its rays' losses) and, with `best`, the best-pose update in
+        # one launch: the candidate is the 7-vector right after that step, as the reference keeps it
+        # (optimize_cam_in_batch steps before Tracker.py:245-247 compares)
+        if self._loss is None:
+            self._loss = torch.empty((), dtype=torch.float64, device=cam.device)
+        if best is None:
+            ops.loss_sum_best(ray_loss, self._loss)
+        else:
+            ops.loss_sum_best(ray_loss, self._loss, best[0], cam.detach(), best[1])
+        return self._loss
 
 
 def frustum_rows(mask_xyz: torch.Tensor) -> torch.Tensor:

@@ -701,6 +701,24 @@ def track_best(loss, best_loss, cam, best):
           "nslam_track_best")
 
 
+def loss_sum_best(ray_loss, out, best_loss=None, cam=None, best=None):
+    """nslam_loss_sum_best (ABI v21): out (float64 device scalar) = ray_loss.sum() in a fixed order (one
+    workgroup: the same value on every call); with best_loss: if out < best_loss, best_loss = out and
+    best = cam (nslam_track_best's update, Tracker.py:245-247).  Returns out."""
+    if ray_loss.dtype != torch.float64 or out.dtype != torch.float64 or not ray_loss.is_contiguous():
+        raise ValueError("loss_sum_best: a contiguous float64 ray_loss and a float64 scalar out")
+    if best_loss is not None and (best_loss.dtype != torch.float64 or cam.dtype != torch.float32
+                                  or best.shape != cam.shape or not (cam.is_contiguous() and best.is_contiguous())):
+        raise ValueError("loss_sum_best: a float64 best_loss and two contiguous float32 vectors of one shape")
+    check(lib().nslam_loss_sum_best(ptr(ray_loss), ray_loss.numel(), ptr(out),
+                                    ptr(best_loss) if best_loss is not None else None,
+                                    ptr(cam) if best_loss is not None else None,
+                                    ptr(best) if best_loss is not None else None,
+                                    cam.numel() if best_loss is not None else 0, stream_ptr(ray_loss.device)),
+          "nslam_loss_sum_best")
+    return out
+
+
 def cam_grad_batch(cams, c2w, ray_begin, n_per, g_pts, z, rd, out, ws, tickets):
     """nslam_cam_grad_batch (ABI v19): out [n, 7] = d loss / d cams [n, 7] of the bundle-adjustment cameras,
     camera k's rays being [ray_begin[k], ray_begin[k] + n_per) of the batch (z [N, S] f64, rd [N, 3] f32,

@@ -196,10 +196,7 @@ class Tracker(object):
         color = gt_color.float().contiguous()
         for _ in range(self.num_cam_iters):
             pix = torch.randint(eng.n_window(), (self.tracking_pixels,), device=device, generator=self.generator)
-            loss = eng.iteration(cam, depth, color, pix, opt)
-            better = loss < best_loss
-            best_loss = torch.where(better, loss, best_loss)
-            best = torch.where(better, cam.detach(), best)
+            eng.iteration(cam, depth, color, pix, opt, best=(best_loss, best))  # (+ Tracker.py:245-247)
         bottom = torch.tensor([[0, 0, 0, 1.0]], dtype=torch.float32, device=device)
         return torch.cat([get_camera_from_tensor(best), bottom], 0)
 
@@ -208,7 +205,7 @@ class Tracker(object):
         guess (constant speed, Tracker.py:191-198), its camera 7-vector, a fresh Adam, the camera loop with
         device pixel draws and the device-side best-pose selection (Tracker.py:225-250), and the result pose.
         Per frame the host copies the frame and the previous poses into persistent buffers and replays."""
-        from .ops import FusedAdam, track_best
+        from .ops import FusedAdam
         eng = self.engine()
         dev = self.device
         st = self._fstate
@@ -242,8 +239,9 @@ class Tracker(object):
             best_loss.fill_(float("inf"))
             opt.reset_state()
             for _ in range(1 if zero_lr else iters):
-                loss = eng.iteration(cam, st["depth"], st["color"], None, opt, n=n, seed=self._draw_seed)
-                track_best(loss, best_loss, cam.detach(), best)  # (Tracker.py:245-247, one launch)
+                # (the iteration's loss launch also keeps the best pose, Tracker.py:245-247)
+                eng.iteration(cam, st["depth"], st["color"], None, opt, n=n, seed=self._draw_seed,
+                              best=(best_loss, best))
             st["out"][:3].copy_(get_camera_from_tensor(best))
 
         key = (iters, n, speed)

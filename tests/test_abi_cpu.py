@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_strerror(pkg):
     L = pkg._lib.lib()
-    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 20
+    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 21
     assert L.nslam_strerror(0) == b"ok"
     assert b"invalid" in L.nslam_strerror(-1)
 
@@ -262,3 +262,14 @@ def test_v20_frustum_rows_validates_without_gpu(pkg):
     a = list(args)
     a[13] = need - 1                    # short workspace
     assert L.nslam_frustum_rows(*a) == -3
+
+
+def test_v21_loss_sum_best_validates_without_gpu(pkg):
+    """nslam_loss_sum_best needs an output scalar (and a loss vector when there are rays); with a
+    best_loss it needs the two camera vectors and 1 <= n <= 64 — all before any launch."""
+    L = pkg._lib.lib()
+    assert L.nslam_loss_sum_best(4096, 10, None, None, None, None, 0, None) == -1      # no output
+    assert L.nslam_loss_sum_best(None, 10, 4096, None, None, None, 0, None) == -1      # no losses
+    assert L.nslam_loss_sum_best(4096, -1, 4096, None, None, None, 0, None) == -1      # negative count
+    assert L.nslam_loss_sum_best(4096, 10, 4096, 4096, None, 4096, 7, None) == -1     # best without cam
+    assert L.nslam_loss_sum_best(4096, 10, 4096, 4096, 4096, 4096, 65, None) == -1    # n > 64

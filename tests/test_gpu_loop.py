@@ -293,3 +293,37 @@ def test_frustum_rows_kernel_matches_mask(loop):
             inv = torch.full((n,), -1, dtype=torch.int32, device=DEV)
             inv[want.long()] = torch.arange(k, dtype=torch.int32, device=DEV)
             assert torch.equal(slot, inv), (key, name)
+
+
+@pytest.mark.parametrize("n", [0, 1, 200, 1000, 5000])
+def test_loss_sum_best_matches_torch_and_keeps_the_best_pose(n):
+    """ABI v21 nslam_loss_sum_best (the tracker's per-iteration loss and Tracker.py:245-247's best-pose
+    bookkeeping in one launch): the sum equals torch's float64 sum to rounding and is the same value on
+    every call (fixed order); a lower loss replaces best_loss and the best pose, an equal, higher or NaN
+    loss leaves both as they were (torch's comparison)."""
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(5 + n)
+    rl = torch.rand(n, dtype=torch.float64, device=dev, generator=g) * 3.0
+    out = torch.empty((), dtype=torch.float64, device=dev)
+    s1 = float(P.ops.loss_sum_best(rl, out))
+    s2 = float(P.ops.loss_sum_best(rl, out))
+    ref = float(rl.sum())
+    assert s1 == s2
+    assert abs(s1 - ref) <= 1e-12 * max(1.0, abs(ref))
+    cam = torch.arange(7, dtype=torch.float32, device=dev)
+    for best_before, expect_update in ((s1 + 1.0, True), (s1, False), (s1 - 1.0, False), (float("inf"), True)):
+        best_loss = torch.full((), best_before, dtype=torch.float64, device=dev)
+        best = torch.full((7,), -1.0, dtype=torch.float32, device=dev)
+        P.ops.loss_sum_best(rl, out, best_loss, cam, best)
+        torch.cuda.synchronize()
+        if expect_update:
+            assert float(best_loss) == s1 and torch.equal(best, cam)
+        else:
+            assert float(best_loss) == best_before and bool((best == -1.0).all())
+    if n:  # a NaN loss is never better
+        rl[0] = float("nan")
+        best_loss = torch.full((), float("inf"), dtype=torch.float64, device=dev)
+        best = torch.full((7,), -1.0, dtype=torch.float32, device=dev)
+        P.ops.loss_sum_best(rl, out, best_loss, cam, best)
+        torch.cuda.synchronize()
+        assert float(best_loss) == float("inf") and bool((best == -1.0).all())
