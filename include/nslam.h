@@ -217,7 +217,12 @@ int nslam_grid_sample_bwd(const float* grid, const int32_t* dims, const float* c
 typedef struct nslam_frame {
   const float* depth; /* [H][W] float32                              */
   const float* color; /* [H][W][3] float32                           */
-  const float* c2w;   /* [3 or 4][4] float32 row-major camera-to-world */
+  const float* c2w;   /* [3 or 4][4] float32 row-major camera-to-world (may be NULL when cam is set) */
+  /* ABI v21: the pose given by its camera 7-vector instead (get_camera_from_tensor, common.py:137-176, the
+   * arithmetic of nslam_cam_pose): the gather forms it itself and, when c2w_out is not NULL, also writes
+   * it there ([3][4] row-major) for later launches — the tracker's camera iteration needs no pose launch */
+  const float* cam;   /* [7] float32 (q, t) or NULL                   */
+  float* c2w_out;     /* [3][4] float32 or NULL                        */
 } nslam_frame;
 
 /* In-kernel pixel draws (ABI v7): with pix == NULL and draw != NULL the select_uv indices are drawn

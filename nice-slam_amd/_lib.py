@@ -74,7 +74,8 @@ LOSS_MAPPER, LOSS_TRACKER = 0, 1
 
 
 class NslamFrame(ctypes.Structure):
-    _fields_ = [("depth", ctypes.c_void_p), ("color", ctypes.c_void_p), ("c2w", ctypes.c_void_p)]
+    _fields_ = [("depth", ctypes.c_void_p), ("color", ctypes.c_void_p), ("c2w", ctypes.c_void_p),
+                ("cam", ctypes.c_void_p), ("c2w_out", ctypes.c_void_p)]
 
 
 class NslamLossCfg(ctypes.Structure):

@@ -21,6 +21,7 @@ int hip_status() {
 // ------------------------------------------------------------------------------------------
 struct GatherArgs {
   nslam_frame fr[NSLAM_MAX_FRAMES];
+  int32_t nf;
   int64_t n_per, n;
   const int64_t* pix;
   int32_t W, h0, w0, ww;
@@ -45,6 +46,20 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
 __device__ __forceinline__ double nanmax(double a, double b) { return (a > b || a != a) ? a : b; }
 __device__ __forceinline__ double nanmin(double a, double b) { return (a < b || a != a) ? a : b; }
 
+// get_camera_from_tensor (common.py:137-176): c2w [3][4] from the 7-vector (quad2rotation's products and
+// differences, no FMA contraction); the one arithmetic of k_cam_pose, k_cam_pose_batch and the gather
+__device__ __forceinline__ void cam_pose_one(const float* __restrict__ cam, float* __restrict__ c2w) {
+  const float qr = cam[0], qi = cam[1], qj = cam[2], qk = cam[3];
+  const float two_s = 2.0f / (((qr * qr + qi * qi) + qj * qj) + qk * qk);
+  const float R[9] = {1.0f - two_s * (qj * qj + qk * qk), two_s * (qi * qj - qk * qr), two_s * (qi * qk + qj * qr),
+                      two_s * (qi * qj + qk * qr), 1.0f - two_s * (qi * qi + qk * qk), two_s * (qj * qk - qi * qr),
+                      two_s * (qi * qk - qj * qr), two_s * (qj * qk + qi * qr), 1.0f - two_s * (qi * qi + qj * qj)};
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) c2w[4 * i + j] = R[3 * i + j];
+    c2w[4 * i + 3] = cam[4 + i];
+  }
+}
+
 // One pixel of frame f at window index k: rays_o/rays_d (common.py:74-89), gt depth (0 when the
 // inside mask drops the ray), the pixel offset and the mask.
 struct RayAt {
@@ -55,6 +70,15 @@ struct RayAt {
 
 __device__ __forceinline__ RayAt ray_at(const GatherArgs& a, int f, int64_t k) {
   const nslam_frame& fr = a.fr[f];
+  // ABI v21: a frame given by its camera 7-vector has its pose formed here (the same values as nslam_cam_pose);
+  // either way the 12 entries sit in registers (no pointer that could be private or global memory)
+  float P[12];
+  if (fr.cam) {
+    cam_pose_one(fr.cam, P);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 12; ++e) P[e] = fr.c2w[e];
+  }
   RayAt r;
   // window index -> (row, col); torch.linspace(W0, W1-1, W1-W0) holds exact integers
   const int64_t row = k / a.ww, col = k - row * a.ww;
@@ -68,7 +92,7 @@ __device__ __forceinline__ RayAt ray_at(const GatherArgs& a, int f, int64_t k) {
   const float d2 = -1.f;
 #pragma unroll
   for (int m = 0; m < 3; ++m) {
-    const float* c2w = fr.c2w + 4 * m;
+    const float* c2w = &P[4 * m];
     // torch's 3-element sum reduces as (p0 + p2) + p1 on this device (tools/probes/rays_order.py)
     r.d[m] = (d0 * c2w[0] + d2 * c2w[2]) + d1 * c2w[1];
     r.o[m] = c2w[3];
@@ -98,6 +122,10 @@ __device__ __forceinline__ int64_t draw_k(const GatherArgs& a, uint64_t ctr, uin
 
 __global__ __launch_bounds__(256) void k_gather_rays(GatherArgs a) {
   const int64_t ray = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x < NSLAM_MAX_FRAMES) {  // the poses formed from 7-vectors, for later launches
+    const nslam_frame& fr = a.fr[threadIdx.x];
+    if ((int)threadIdx.x < a.nf && fr.cam && fr.c2w_out) cam_pose_one(fr.cam, fr.c2w_out);
+  }
   __shared__ uint64_t ctr;
   __shared__ uint32_t wred[2][4];
   const bool drawn = a.pix == nullptr;
@@ -299,9 +327,10 @@ extern "C" int nslam_gather_rays(const nslam_frame* frames, int32_t n_frames, in
   if (!pix && draw->gt_max && !draw->gt_max_key) return NSLAM_EINVAL;
   GatherArgs a{};
   for (int f = 0; f < n_frames; ++f) {
-    if (!frames[f].depth || !frames[f].color || !frames[f].c2w) return NSLAM_EINVAL;
+    if (!frames[f].depth || !frames[f].color || (!frames[f].c2w && !frames[f].cam)) return NSLAM_EINVAL;
     a.fr[f] = frames[f];
   }
+  a.nf = n_frames;
   a.n_per = n_per;
   a.n = n;
   a.pix = pix;
@@ -699,17 +728,6 @@ extern "C" int nslam_cam_grad_batch(const float* cams, const float* c2w, int64_t
 
 namespace {
 
-__device__ __forceinline__ void cam_pose_one(const float* __restrict__ cam, float* __restrict__ c2w) {
-  const float qr = cam[0], qi = cam[1], qj = cam[2], qk = cam[3];
-  const float two_s = 2.0f / (((qr * qr + qi * qi) + qj * qj) + qk * qk);
-  const float R[9] = {1.0f - two_s * (qj * qj + qk * qk), two_s * (qi * qj - qk * qr), two_s * (qi * qk + qj * qr),
-                      two_s * (qi * qj + qk * qr), 1.0f - two_s * (qi * qi + qk * qk), two_s * (qj * qk - qi * qr),
-                      two_s * (qi * qk - qj * qr), two_s * (qj * qk + qi * qr), 1.0f - two_s * (qi * qi + qj * qj)};
-  for (int i = 0; i < 3; ++i) {
-    for (int j = 0; j < 3; ++j) c2w[4 * i + j] = R[3 * i + j];
-    c2w[4 * i + 3] = cam[4 + i];
-  }
-}
 
 __global__ __launch_bounds__(64) void k_cam_pose(const float* __restrict__ cam, float* __restrict__ c2w) {
   if (threadIdx.x == 0) cam_pose_one(cam, c2w);

@@ -695,9 +695,11 @@ class TrackingEngine:
         draw = self.eng.draws(seed) if pix is None else None
         if self._c2w is None:
             self._c2w = torch.empty(3, 4, dtype=torch.float32, device=cam.device)
-        c2w = ops.cam_pose(cam.detach(), self._c2w)  # get_camera_from_tensor in one launch
-        ro, rd, gd, gc, keep = ops.gather_rays([(depth, color, c2w)], pix, n, self.H, self.W, self.window,
-                                               fx, fy, cx, cy, self.bound, draw=draw)
+        # get_camera_from_tensor inside the gather (ABI v21), which also leaves the pose in self._c2w for
+        # the camera gradient
+        c2w = self._c2w
+        ro, rd, gd, gc, keep = ops.gather_rays([(depth, color, c2w, cam.detach())], pix, n, self.H, self.W,
+                                               self.window, fx, fy, cx, cy, self.bound, draw=draw)
         z = ops.sample_z(ro, rd, gd, self.bound, self.n_strat, self.n_surf)
         # the fine + middle occupancy sum is formed by the loss kernel as it reads raw (no combine pass)
         raw = self.eng.query_fwd("color", ro, rd, z, defer_occ=True)

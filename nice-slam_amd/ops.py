@@ -552,7 +552,9 @@ def gather_rays(frames, pix, n_per, H, W, window, fx, fy, cx, cy, bound=None, dr
     """get_samples (src/common.py:92-134) for every frame of a window in one launch, plus the
     inside-mask prefilter (Mapper.py:469-481) when `bound` is given.
 
-    frames: list of (depth [H,W] f32, color [H,W,3] f32, c2w [3|4,4] f32) device tensors;
+    frames: list of (depth [H,W] f32, color [H,W,3] f32, c2w [3|4,4] f32) device tensors, or of
+    (depth, color, c2w_out [3|4,4] f32, cam [7] f32): the pose formed in the kernel from the camera
+    7-vector (nslam_cam_pose's values) and written to c2w_out's first three rows (ABI v21);
     pix: int64 [len(frames)*n_per] select_uv randint indices into each frame's window
     (h0, h1, w0, w1).  Returns rays_o, rays_d [N,3] f32, gt_depth [N] f32 (0 for dropped rays),
     gt_color [N,3] f32, keep [N] uint8.
@@ -568,14 +570,24 @@ def gather_rays(frames, pix, n_per, H, W, window, fx, fy, cx, cy, bound=None, dr
     dev = pix.device if pix is not None else draw.counter.device
     arr = (_lib.NslamFrame * nf)()
     keepalive = []
-    for f, (d, c, m) in enumerate(frames):
+    for f, fr in enumerate(frames):
+        d, c, m = fr[:3]
+        cam = fr[3] if len(fr) > 3 else None
         d = d.detach().float().contiguous()
         c = c.detach().float().contiguous()
-        m = m.detach().float().contiguous()
+        if cam is None:
+            m = m.detach().float().contiguous()
+        elif m.dtype != torch.float32 or not m.is_contiguous() or cam.dtype != torch.float32 \
+                or not cam.is_contiguous() or cam.numel() != 7:
+            raise ValueError("a frame given by its camera: c2w_out contiguous f32 [3|4,4], cam contiguous f32 [7]")
         if tuple(d.shape) != (H, W) or tuple(c.shape) != (H, W, 3) or m.shape[-1] != 4 or m.shape[0] < 3:
             raise ValueError("frame tensors must be depth [H,W], color [H,W,3], c2w [3|4,4]")
         keepalive += [d, c, m]
-        arr[f].depth, arr[f].color, arr[f].c2w = ptr(d), ptr(c), ptr(m)
+        arr[f].depth, arr[f].color = ptr(d), ptr(c)
+        if cam is None:
+            arr[f].c2w = ptr(m)
+        else:
+            arr[f].cam, arr[f].c2w_out = ptr(cam.detach()), ptr(m)
     if pix is not None:
         pix = pix.to(torch.int64).contiguous()
     n = nf * n_per

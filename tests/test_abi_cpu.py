@@ -273,3 +273,13 @@ def test_v21_loss_sum_best_validates_without_gpu(pkg):
     assert L.nslam_loss_sum_best(4096, -1, 4096, None, None, None, 0, None) == -1      # negative count
     assert L.nslam_loss_sum_best(4096, 10, 4096, 4096, None, 4096, 7, None) == -1     # best without cam
     assert L.nslam_loss_sum_best(4096, 10, 4096, 4096, 4096, 4096, 65, None) == -1    # n > 64
+
+
+def test_v21_gather_frame_needs_a_pose_or_a_camera(pkg):
+    """A frame with neither c2w nor cam (ABI v21) is rejected before any launch."""
+    L = pkg._lib.lib()
+    fr = (pkg._lib.NslamFrame * 1)()
+    fr[0].depth, fr[0].color = 4096, 4096
+    args = [fr, 1, 10, 4096, 96, 128, 0, 96, 0, 128, 500.0, 500.0, 64.0, 48.0, None, None, 4096, 4096, 4096, 4096,
+            None, None, None, None]
+    assert L.nslam_gather_rays(*args) == -1

@@ -693,6 +693,31 @@ def test_gather_rays_device_draws(tiny, window):
     assert np.all(np.abs(q - 0.25) < 0.03), q
 
 
+def test_gather_rays_from_camera_vectors(tiny):
+    """ABI v21 nslam_frame.cam: frames given by their camera 7-vectors — the gather forms each pose itself
+    (nslam_cam_pose's arithmetic) and writes it to c2w_out: the pose equals nslam_cam_pose's bit for bit
+    and the rays equal a gather of frames given by that pose; frames of both kinds mix in one call."""
+    sc, frames = _frames(tiny)
+    H, W = 96, 128
+    g = torch.Generator().manual_seed(3)
+    cams = []
+    for f in range(len(frames)):
+        q = torch.randn(4, generator=g)
+        cams.append(torch.cat([q / q.norm(), torch.randn(3, generator=g) * 0.3]).float().to(DEV))
+    poses = [P.ops.cam_pose(c, torch.empty(3, 4, dtype=torch.float32, device=DEV)) for c in cams]
+    outs = [torch.full((3, 4), -7.0, dtype=torch.float32, device=DEV) for _ in cams]
+    mixed = [(d, c, outs[f], cams[f]) if f != 1 else (d, c, poses[f]) for f, (d, c, _) in enumerate(frames)]
+    ref_frames = [(d, c, poses[f]) for f, (d, c, _) in enumerate(frames)]
+    pix = torch.randint(H * W, (len(frames) * 300,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(4))
+    got = P.ops.gather_rays(mixed, pix, 300, H, W, (0, H, 0, W), sc.fx, sc.fy, sc.cx, sc.cy, sc.bound)
+    ref = P.ops.gather_rays(ref_frames, pix, 300, H, W, (0, H, 0, W), sc.fx, sc.fy, sc.cx, sc.cy, sc.bound)
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
+    for f in (0, 2):
+        assert torch.equal(outs[f], poses[f])
+    assert bool((outs[1] == -7.0).all())  # a frame given by its pose: nothing written
+
+
 def test_adam_mirror_keeps_packed_copy_current(tiny):
     """FusedAdam.set_mirror: the engine's packed decoder copy after Adam equals a fresh repack."""
     sc, frames = _frames(tiny)
