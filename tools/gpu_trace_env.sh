@@ -1,5 +1,5 @@
 # Round 6: a kernel trace of the captured room0 iteration under the given environment settings.
-# usage: bash tools/gpu_r6_trace_env.sh TAG "VAR=a VAR2=b" ["VAR=c" ...]
+# usage: bash tools/gpu_trace_env.sh TAG "VAR=a VAR2=b" ["VAR=c" ...]
 set -o pipefail
 OUT=gpurun_out/${1:?tag}; shift; mkdir -p $OUT; export TMPDIR=/tmp
 i=0
