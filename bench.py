@@ -993,7 +993,7 @@ def engine_ba_stage_ms(dev, cfg, reps=50):
     """The bare engine with bundle adjustment per stage at a config's shape: engine.MappingEngine.iteration
     over the 5-frame window with d/dpts formed by the backward, the batched camera gradient of the 4
     non-oldest cameras (nslam_cam_grad_batch) and their Adam step, the poses re-derived from the cameras
-    each iteration (nslam_cam_pose_batch) — the GPU work of an optimize_map BA iteration, replayed in
+    each iteration by the gather (nslam_frame.cam, ABI v21) — the GPU work of an optimize_map BA iteration, replayed in
     hipGraph blocks, without the drop-in's per-call work."""
     P = pkg()
     scene = Room0Scene(dev, 0, cfg=dict(cfg), path="fused")
@@ -1001,8 +1001,9 @@ def engine_ba_stage_ms(dev, cfg, reps=50):
     n = cfg["pixels"] // F
     c2w = torch.eye(4, device=dev).repeat(F, 1, 1)
     c2w[:, :3] = scene.c2w
-    frames = [(scene.depth[f], scene.color[f], c2w[f]) for f in range(F)]
     cams = P.common.camera_tensors(c2w[1:]).contiguous()
+    frames = [(scene.depth[0], scene.color[0], c2w[0])]
+    frames += [(scene.depth[f], scene.color[f], c2w[f], cams[f - 1]) for f in range(1, F)]
     cgrad = torch.zeros_like(cams)
     ws = torch.zeros((F - 1) * P.ops.CAM_GRAD_WS_DOUBLES, dtype=torch.float64, device=dev)
     tk = torch.zeros(F - 1, dtype=torch.int32, device=dev)
@@ -1014,7 +1015,6 @@ def engine_ba_stage_ms(dev, cfg, reps=50):
         copt.step(grads={cams: cgrad})
 
     def step(stage):
-        P.ops.cam_pose_batch(cams, c2w[1:])
         eng.iteration(stage, frames, None, n, (cfg["H"], cfg["W"]), (cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"]),
                       scene.opt, trainable_decoders=("color",), seed=1000, post_bwd=post_bwd)
     out = {}

@@ -405,6 +405,15 @@ int nslam_track_best(const double* loss, double* best_loss, const float* cam, fl
 int nslam_loss_sum_best(const double* ray_loss, int64_t n_rays, double* loss_out, double* best_loss, const float* cam,
                         float* best, int32_t n, void* stream);
 
+/* ABI v22.  The inverse map for n poses in one launch: cams[k] (7 float32) = get_tensor_from_camera(c2w +
+ * k * c2w_stride) (common.py:179-201, as common.camera_tensors restates it on the device: quaternion
+ * (w,x,y,z) by the trace / largest-diagonal branch rule in float64, normalised, w >= 0, then T, rounded to
+ * float32 once); cams_copy (optional) receives the same 7-vectors.  Replaces the tracker's per-frame
+ * camera_tensor and best-pose initialisation (Tracker.py:199-200, 225) and bundle adjustment's camera
+ * set-up (Mapper.py:349-363), each ~70 torch launches.  n <= 64, c2w_stride >= 12 floats. */
+int nslam_cam_vector_batch(const float* c2w, int64_t c2w_stride, int32_t n, float* cams, float* cams_copy,
+                           void* stream);
+
 /* ABI v9.  c2w [3,4] f32 = get_camera_from_tensor(cam [7]) (common.py:137-176, quad2rotation's
  * products and differences, no FMA contraction), one thread.  |q|² is summed ((w²+x²)+y²)+z²;
  * the order of torch's (quad*quad).sum(-1) reduction is not pinned, so the pose matches the

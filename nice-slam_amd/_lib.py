@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NSLAM_LIB") or os.path.join(_HERE, "libnslam.so")  # NSLAM_LIB: instrumented builds
 
 NSLAM_OK = 0
-ABI_VERSION = 21
+ABI_VERSION = 22
 STAGES = {"coarse": 0, "middle": 1, "fine": 2, "color": 3}
 DEC_COARSE, DEC_MIDDLE, DEC_FINE, DEC_COLOR = 0, 1, 2, 3
 
@@ -119,7 +119,7 @@ EXPORTS = (
     "nslam_query_fwd_ws", "nslam_query_fwd_workspace_size", "nslam_cam_grad", "nslam_cam_pose",
     "nslam_query_tape_size", "nslam_color_wgrad", "nslam_cam_grad_parts", "nslam_cam_grad_batch",
     "nslam_cam_pose_batch", "nslam_frustum_rows", "nslam_frustum_rows_workspace_size", "nslam_track_best",
-    "nslam_loss_sum_best",
+    "nslam_loss_sum_best", "nslam_cam_vector_batch",
 )
 
 _lib = None
@@ -189,6 +189,7 @@ def lib():
         L.nslam_frustum_rows_workspace_size.restype = sz
         L.nslam_track_best.argtypes = [vp, vp, vp, vp, i32, vp]
         L.nslam_loss_sum_best.argtypes = [vp, i64, vp, vp, vp, vp, i32, vp]
+        L.nslam_cam_vector_batch.argtypes = [vp, i64, i32, vp, vp, vp]
         if L.nslam_abi_version() != ABI_VERSION:
             raise RuntimeError(f"libnslam.so ABI {L.nslam_abi_version()} != {ABI_VERSION}: rebuild it")
         _lib = L

@@ -806,6 +806,59 @@ extern "C" int nslam_track_best(const double* loss, double* best_loss, const flo
   return e == hipSuccess ? NSLAM_OK : NSLAM_EHIP - (int)e;
 }
 
+namespace {
+
+// get_tensor_from_camera (common.py:179-201) as common.camera_tensors restates it on the device: rotation →
+// quaternion (w,x,y,z) by the trace / largest-diagonal branch rule in float64, normalised, w >= 0, then T;
+// rounded to float32 once.  NaN compares false (the last branch, as torch.where's) and survives the clamp.
+__device__ __forceinline__ void cam_vector_one(const float* __restrict__ M, float* __restrict__ out,
+                                               float* __restrict__ out2) {
+  const double r00 = M[0], r01 = M[1], r02 = M[2], r10 = M[4], r11 = M[5], r12 = M[6];
+  const double r20 = M[8], r21 = M[9], r22 = M[10];
+  const double tr = (r00 + r11) + r22;
+  auto root = [](double x) { return 2.0 * sqrt(x < 0.0 ? 0.0 : x); };
+  double q[4];
+  if (tr > 0.0) {
+    const double s = root(tr + 1.0);
+    q[0] = 0.25 * s; q[1] = (r21 - r12) / s; q[2] = (r02 - r20) / s; q[3] = (r10 - r01) / s;
+  } else if (r00 > r11 && r00 > r22) {
+    const double s = root(((1.0 + r00) - r11) - r22);
+    q[0] = (r21 - r12) / s; q[1] = 0.25 * s; q[2] = (r01 + r10) / s; q[3] = (r02 + r20) / s;
+  } else if (r11 > r22) {
+    const double s = root(((1.0 + r11) - r00) - r22);
+    q[0] = (r02 - r20) / s; q[1] = (r01 + r10) / s; q[2] = 0.25 * s; q[3] = (r12 + r21) / s;
+  } else {
+    const double s = root(((1.0 + r22) - r00) - r11);
+    q[0] = (r10 - r01) / s; q[1] = (r02 + r20) / s; q[2] = (r12 + r21) / s; q[3] = 0.25 * s;
+  }
+  const double nrm = sqrt(((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3]);
+  for (int i = 0; i < 4; ++i) q[i] = q[i] / nrm;
+  const bool flip = q[0] < 0.0;
+  float v[7];
+  for (int i = 0; i < 4; ++i) v[i] = (float)(flip ? -q[i] : q[i]);
+  v[4] = M[3]; v[5] = M[7]; v[6] = M[11];
+  for (int i = 0; i < 7; ++i) out[i] = v[i];
+  if (out2)
+    for (int i = 0; i < 7; ++i) out2[i] = v[i];
+}
+
+__global__ __launch_bounds__(64) void k_cam_vector_batch(const float* __restrict__ c2w, int64_t stride, int n,
+                                                         float* __restrict__ cams, float* __restrict__ cams2) {
+  const int k = threadIdx.x;
+  if (k < n) cam_vector_one(c2w + stride * k, cams + 7 * k, cams2 ? cams2 + 7 * k : nullptr);
+}
+
+}  // namespace
+
+extern "C" int nslam_cam_vector_batch(const float* c2w, int64_t c2w_stride, int32_t n, float* cams, float* cams_copy,
+                                      void* stream) {
+  if (!c2w || !cams || n < 1 || n > 64 || c2w_stride < 12) return NSLAM_EINVAL;
+  hipLaunchKernelGGL(k_cam_vector_batch, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), c2w, c2w_stride,
+                     (int)n, cams, cams_copy);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? NSLAM_OK : NSLAM_EHIP - (int)e;
+}
+
 extern "C" int nslam_cam_pose_batch(const float* cams, float* c2w, int64_t c2w_stride, int32_t n, void* stream) {
   if (!cams || !c2w || n < 1 || n > 64 || c2w_stride < 12) return NSLAM_EINVAL;
   hipLaunchKernelGGL(k_cam_pose_batch, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), cams, c2w,

@@ -31,7 +31,7 @@ import torch
 
 from . import common as _common
 from . import ops
-from .common import camera_tensors, get_camera_from_tensor, get_samples, get_tensor_from_camera, random_select
+from .common import get_camera_from_tensor, get_samples, get_tensor_from_camera, random_select
 
 _SELECT_UV = _common.select_uv  # the product's own pixel selection (a replacement one forces eager draws)
 _STAGE_GROUPS = ("decoders", "coarse", "middle", "fine", "color")
@@ -511,8 +511,12 @@ class Mapper(object):
             copt.init_state()
 
             def cams_init():  # (captured with the first stage's graph below)
-                cams.copy_(camera_tensors(c2w_s[c0:F]))
+                ops.cam_vector_batch(c2w_s[c0:F], cams)  # get_tensor_from_camera of each, one launch
                 copt.reset_state()
+
+            # the optimised frames are gathered from their 7-vectors: the gather forms each pose
+            # (get_camera_from_tensor) and writes it to the frame's slot for the camera gradient (ABI v21)
+            frames[c0:] = [(depth_s[s], color_s[s], c2w_s[s], cams[s - c0]) for s in range(c0, F)]
 
         def post_bwd(gps, ro, rd, z):  # BA: camera gradients of every optimised frame, then their Adam step
             ops.cam_grad_batch(cams, c2w_s[c0:F], [(c0 + k) * n_per for k in range(ncam)], n_per, gps, z, rd, cgrad,
@@ -531,8 +535,6 @@ class Mapper(object):
             return device_draws and (not ncam or stage != "color")
 
         def iteration(stage, record=None):
-            if ncam:
-                ops.cam_pose_batch(cams, c2w_s[c0:F])  # get_camera_from_tensor of every BA camera
             pix = None
             if not device_draws:  # select_uv per frame, in optimize_frame order (Mapper.py:437-467)
                 pix = torch.empty(F * n_per, dtype=torch.int64, device=dev)

@@ -689,6 +689,22 @@ def cam_grad_parts(cam, c2w, g_pts, z, rd, out, ws, ticket):
 CAM_GRAD_WS_DOUBLES = 32 * 12  # NSLAM_CAM_GRAD_WS_DOUBLES
 
 
+def cam_vector_batch(c2w, out, copy=None):
+    """nslam_cam_vector_batch (ABI v22): out[k] = get_tensor_from_camera(c2w[k]) for c2w [n, 3|4, 4] f32
+    (common.camera_tensors' arithmetic, one launch); copy: optional second [n, 7] f32 receiving the same."""
+    n = c2w.shape[0]
+    if c2w.dtype != torch.float32 or c2w.dim() != 3 or c2w.shape[1] not in (3, 4) or c2w.shape[2] != 4 \
+            or not c2w.is_contiguous() or not 1 <= n <= 64:
+        raise ValueError("cam_vector_batch: c2w must be a contiguous float32 [n, 3|4, 4], 1 <= n <= 64")
+    for t in (out,) if copy is None else (out, copy):
+        if t.dtype != torch.float32 or tuple(t.shape) != (n, 7) or not t.is_contiguous():
+            raise ValueError("cam_vector_batch: out / copy must be contiguous float32 [n, 7]")
+    rc = lib().nslam_cam_vector_batch(ptr(c2w), c2w.shape[1] * 4, n, ptr(out), None if copy is None else ptr(copy),
+                                      stream_ptr(c2w.device))
+    check(rc, "nslam_cam_vector_batch")
+    return out
+
+
 def cam_pose_batch(cams, c2w):
     """nslam_cam_pose_batch (ABI v19): c2w[k, :3, :4] = get_camera_from_tensor(cams[k]) for cams [n, 7] f32
     and c2w [n, 3 or 4, 4] f32 (both contiguous), one launch."""

@@ -205,6 +205,7 @@ class Tracker(object):
         guess (constant speed, Tracker.py:191-198), its camera 7-vector, a fresh Adam, the camera loop with
         device pixel draws and the device-side best-pose selection (Tracker.py:225-250), and the result pose.
         Per frame the host copies the frame and the previous poses into persistent buffers and replays."""
+        from . import ops
         from .ops import FusedAdam
         eng = self.engine()
         dev = self.device
@@ -232,17 +233,15 @@ class Tracker(object):
         def frame(zero_lr=False):
             pre = st["pre"]
             est = (pre @ torch.linalg.inv_ex(st["prev2"])[0]) @ pre if speed else pre
-            cam0 = camera_tensors(est[None])[0]
-            with torch.no_grad():
-                cam.copy_(cam0)
-                best.copy_(cam0)
+            # the guess's 7-vector into the camera and the best pose in one launch (ABI v22)
+            ops.cam_vector_batch(est[None], cam.detach().view(1, 7), best.view(1, 7))
             best_loss.fill_(float("inf"))
             opt.reset_state()
             for _ in range(1 if zero_lr else iters):
                 # (the iteration's loss launch also keeps the best pose, Tracker.py:245-247)
                 eng.iteration(cam, st["depth"], st["color"], None, opt, n=n, seed=self._draw_seed,
                               best=(best_loss, best))
-            st["out"][:3].copy_(get_camera_from_tensor(best))
+            ops.cam_pose(best, st["out"][:3])  # get_camera_from_tensor(best), one launch
 
         key = (iters, n, speed)
         if key not in self._graphs:

@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_strerror(pkg):
     L = pkg._lib.lib()
-    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 21
+    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 22
     assert L.nslam_strerror(0) == b"ok"
     assert b"invalid" in L.nslam_strerror(-1)
 
@@ -273,6 +273,17 @@ def test_v21_loss_sum_best_validates_without_gpu(pkg):
     assert L.nslam_loss_sum_best(4096, -1, 4096, None, None, None, 0, None) == -1      # negative count
     assert L.nslam_loss_sum_best(4096, 10, 4096, 4096, None, 4096, 7, None) == -1     # best without cam
     assert L.nslam_loss_sum_best(4096, 10, 4096, 4096, 4096, 4096, 65, None) == -1    # n > 64
+
+
+def test_v22_cam_vector_batch_validates_without_gpu(pkg):
+    """nslam_cam_vector_batch needs poses and outputs, 1 <= n <= 64 and a pose stride of at least 12 floats
+    — all checked before any launch (the copy is optional)."""
+    L = pkg._lib.lib()
+    assert L.nslam_cam_vector_batch(None, 16, 1, 4096, None, None) == -1     # no poses
+    assert L.nslam_cam_vector_batch(4096, 16, 1, None, 4096, None) == -1     # no output
+    assert L.nslam_cam_vector_batch(4096, 16, 0, 4096, None, None) == -1     # no cameras
+    assert L.nslam_cam_vector_batch(4096, 16, 65, 4096, None, None) == -1    # n > 64
+    assert L.nslam_cam_vector_batch(4096, 8, 2, 4096, None, None) == -1      # stride < 12
 
 
 def test_v21_gather_frame_needs_a_pose_or_a_camera(pkg):

@@ -327,3 +327,53 @@ def test_loss_sum_best_matches_torch_and_keeps_the_best_pose(n):
         P.ops.loss_sum_best(rl, out, best_loss, cam, best)
         torch.cuda.synchronize()
         assert float(best_loss) == float("inf") and bool((best == -1.0).all())
+
+
+def _rotations(n, gen):
+    """Random rotations, a quarter of them rotated by pi about x / y / z so every branch of the
+    trace / largest-diagonal rule is taken (trace <= 0 with r00, r11 or r22 the largest)."""
+    q = torch.randn(n, 4, generator=gen, dtype=torch.float64)
+    q = q / q.norm(dim=1, keepdim=True)
+    R = P.common.quad2rotation(q)
+    flips = [torch.diag(torch.tensor(d, dtype=torch.float64)) for d in ((1, -1, -1), (-1, 1, -1), (-1, -1, 1))]
+    small = P.common.quad2rotation(q * torch.tensor([1.0, 0.05, 0.05, 0.05], dtype=torch.float64))
+    for k in range(n):
+        if k % 4:
+            R[k] = flips[k % 4 - 1] @ small[k]
+    return R
+
+
+@pytest.mark.parametrize("rows", [3, 4])
+def test_cam_vector_batch_matches_camera_tensors(rows):
+    """nslam_cam_vector_batch (ABI v22) == common.camera_tensors (the device restatement of the reference's
+    get_tensor_from_camera, common.py:179-201) on poses taking every branch, for [n,3,4] and [n,4,4] slots;
+    the optional copy equals the output; and cam_pose(cam_vector(c2w)) gives c2w back.  Tolerance: 1 float32
+    ulp per entry (|q|² is summed in a fixed order, torch's reduction order is not pinned)."""
+    gen = torch.Generator().manual_seed(5)
+    n = 64
+    R = _rotations(n, gen)
+    c2w = torch.zeros(n, rows, 4, dtype=torch.float64)
+    c2w[:, :3, :3] = R
+    c2w[:, :3, 3] = torch.randn(n, 3, generator=gen, dtype=torch.float64)
+    if rows == 4:
+        c2w[:, 3, 3] = 1.0
+    c2w = c2w.float().to(DEV)
+    tr = c2w[:, 0, 0] + c2w[:, 1, 1] + c2w[:, 2, 2]
+    assert bool((tr > 0).any()) and bool((tr <= 0).any())
+    out = torch.full((n, 7), -9.0, device=DEV)
+    cp = torch.full((n, 7), -9.0, device=DEV)
+    P.ops.cam_vector_batch(c2w, out, cp)
+    ref = P.common.camera_tensors(c2w)
+    assert torch.equal(out, cp)
+    exact = int((out == ref).all(dim=1).sum())
+    print(f"cam_vector_batch: {exact}/{n} bit-identical to camera_tensors")
+    assert float((out - ref).abs().max()) <= 2 ** -23
+    assert bool((out[:, 0] >= 0).all())
+    back = torch.empty(3, 4, device=DEV)
+    for k in range(n):
+        P.ops.cam_pose(out[k].contiguous(), back)
+        assert float((back - c2w[k, :3]).abs().max()) < 1e-5
+    # one camera, no copy
+    one = torch.empty(1, 7, device=DEV)
+    P.ops.cam_vector_batch(c2w[:1].contiguous(), one)
+    assert torch.equal(one[0], out[0])

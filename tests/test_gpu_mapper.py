@@ -135,7 +135,9 @@ def test_tracker_graph_matches_eager_device_draws(tiny):
     eng = tr2.engine()
     ref = []
     for pre in pres:
-        cam = P.common.camera_tensors(pre[None])[0].clone().requires_grad_(True)
+        # (the graph forms the guess's 7-vector and the result pose with nslam_cam_vector_batch / nslam_cam_pose)
+        cam = P.ops.cam_vector_batch(pre[None].contiguous(), torch.empty(1, 7, device="cuda"))[0]
+        cam = cam.clone().requires_grad_(True)
         opt = P.ops.FusedAdam([{"params": [cam], "lr": cfg["tracking"]["lr"]}])
         best, best_loss = cam.detach().clone(), torch.full((), float("inf"), dtype=torch.float64, device="cuda")
         for _ in range(cfg["tracking"]["iters"]):
@@ -143,7 +145,9 @@ def test_tracker_graph_matches_eager_device_draws(tiny):
             better = loss < best_loss
             best_loss = torch.where(better, loss, best_loss)
             best = torch.where(better, cam.detach(), best)
-        ref.append(torch.cat([P.common.get_camera_from_tensor(best), torch.tensor([[0, 0, 0, 1.0]], device="cuda")]))
+        pose = torch.eye(4, device="cuda")
+        P.ops.cam_pose(best.contiguous(), pose[:3])
+        ref.append(pose)
     for a, b in zip(got, ref):
         assert torch.equal(a, b), (a - b).abs().max()
     assert not torch.equal(got[0], pres[0])  # the loop moved the pose
