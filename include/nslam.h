@@ -374,6 +374,28 @@ int nslam_cam_grad_batch(const float* cams, const float* c2w, int64_t c2w_stride
                          const int64_t* ray_begin, int64_t n_rays_per, const double* const* g_pts, int32_t n_parts,
                          const double* z_vals, const float* rays_d, int64_t n_rays, int32_t n_samples, float* g_cam,
                          double* ws, uint32_t* tickets, void* stream);
+/* ABI v23.  A tracking iteration's camera tail fused into nslam_cam_grad_parts' last workgroup: after g_cam
+ * is formed, Adam on the camera 7-vector in place (torch.optim.Adam, Tracker.py:126: nslam_adam_step's
+ * element update and bias corrections with the step count *step, then *step += 1), *loss_out = the sum of
+ * ray_loss[0..n_rays) (nslam_loss_sum_best's fixed-order tree: the same value), and, when best_loss is not
+ * NULL, the best-pose update (Tracker.py:245-247) with the stepped camera.  Bit-identical to
+ * nslam_cam_grad_parts + nslam_adam_step + nslam_loss_sum_best in that order, in one launch. */
+typedef struct nslam_cam_tail {
+  float* cam;        /* [7], read by the gradient and stepped in place */
+  float* exp_avg;    /* [7] Adam state */
+  float* exp_avg_sq; /* [7] */
+  float* step;       /* [1] step count */
+  float lr, beta1, beta2, eps;
+  const double* ray_loss; /* [n_rays] the iteration's per-ray losses */
+  int64_t n_rays;
+  double* loss_out;  /* [1] */
+  double* best_loss; /* [1] or NULL */
+  float* best;       /* [7] (with best_loss) */
+} nslam_cam_tail;
+int nslam_cam_grad_step(const nslam_cam_tail* tail, const float* c2w, const double* const* g_pts, int32_t n_parts,
+                        const double* z_vals, const float* rays_d, int64_t n_rays, int32_t n_samples, float* g_cam,
+                        double* ws, uint32_t* ticket, void* stream);
+
 /* ABI v19: nslam_cam_pose for n cameras in one launch: c2w + k * c2w_stride = get_camera_from_tensor(cams[k]). */
 int nslam_cam_pose_batch(const float* cams, float* c2w, int64_t c2w_stride, int32_t n, void* stream);
 

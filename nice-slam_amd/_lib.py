@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NSLAM_LIB") or os.path.join(_HERE, "libnslam.so")  # NSLAM_LIB: instrumented builds
 
 NSLAM_OK = 0
-ABI_VERSION = 22
+ABI_VERSION = 23
 STAGES = {"coarse": 0, "middle": 1, "fine": 2, "color": 3}
 DEC_COARSE, DEC_MIDDLE, DEC_FINE, DEC_COLOR = 0, 1, 2, 3
 
@@ -89,6 +89,15 @@ class NslamDraw(ctypes.Structure):  # ABI v7 in-kernel pixel draws
                 ("gt_max_key", ctypes.c_void_p)]
 
 
+class NslamCamTail(ctypes.Structure):
+    """nslam_cam_tail (ABI v23): the camera's Adam step, the iteration's loss and the best pose."""
+    _fields_ = [("cam", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p), ("exp_avg_sq", ctypes.c_void_p),
+                ("step", ctypes.c_void_p), ("lr", ctypes.c_float), ("beta1", ctypes.c_float),
+                ("beta2", ctypes.c_float), ("eps", ctypes.c_float), ("ray_loss", ctypes.c_void_p),
+                ("n_rays", ctypes.c_int64), ("loss_out", ctypes.c_void_p), ("best_loss", ctypes.c_void_p),
+                ("best", ctypes.c_void_p)]
+
+
 class NslamAdamSeg(ctypes.Structure):
     _fields_ = [
         ("param", ctypes.c_void_p),
@@ -119,7 +128,7 @@ EXPORTS = (
     "nslam_query_fwd_ws", "nslam_query_fwd_workspace_size", "nslam_cam_grad", "nslam_cam_pose",
     "nslam_query_tape_size", "nslam_color_wgrad", "nslam_cam_grad_parts", "nslam_cam_grad_batch",
     "nslam_cam_pose_batch", "nslam_frustum_rows", "nslam_frustum_rows_workspace_size", "nslam_track_best",
-    "nslam_loss_sum_best", "nslam_cam_vector_batch",
+    "nslam_loss_sum_best", "nslam_cam_vector_batch", "nslam_cam_grad_step",
 )
 
 _lib = None
@@ -190,6 +199,8 @@ def lib():
         L.nslam_track_best.argtypes = [vp, vp, vp, vp, i32, vp]
         L.nslam_loss_sum_best.argtypes = [vp, i64, vp, vp, vp, vp, i32, vp]
         L.nslam_cam_vector_batch.argtypes = [vp, i64, i32, vp, vp, vp]
+        L.nslam_cam_grad_step.argtypes = [ctypes.POINTER(NslamCamTail), vp, ctypes.POINTER(vp), i32, vp, vp, i64, i32,
+                                          vp, vp, vp, vp]
         if L.nslam_abi_version() != ABI_VERSION:
             raise RuntimeError(f"libnslam.so ABI {L.nslam_abi_version()} != {ABI_VERSION}: rebuild it")
         _lib = L

@@ -523,7 +523,49 @@ struct CamPartsArgs {
   float* g_cam;
   double* ws;  // [kCamParts][12]
   uint32_t* ticket;
+  nslam_cam_tail tail;  // ABI v23 (nslam_cam_grad_step): the camera's Adam step, loss and best pose
+  int32_t has_tail;
 };
+
+// ABI v23: what follows a tracking iteration's camera gradient, in the workgroup that formed it (all its
+// threads): the loss sum (k_loss_sum_best's fixed-order tree over its first kTailSum threads: the same
+// value), Adam on the 7-vector (adam_coef / adam_one: k_adam's element update, bit for bit), the step
+// count, and the best-pose update with the stepped camera.  Thread 0 wrote g_cam (the epilogue) and
+// alone reads it back, and it alone writes the camera after the epilogue read it.
+constexpr int kTailSum = 256;
+__device__ void cam_tail(const CamPartsArgs& a) {
+  const nslam_cam_tail& t = a.tail;
+  __shared__ double s[kTailSum];
+  if (threadIdx.x < kTailSum) {
+    double acc = 0.0;
+    for (int64_t i = threadIdx.x; i < t.n_rays; i += kTailSum) acc += t.ray_loss[i];
+    s[threadIdx.x] = acc;
+  }
+  __syncthreads();
+  for (int w = kTailSum / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  const double l = s[0];
+  float* cam = t.cam;
+  const AdamCoef c = adam_coef(t.beta1, t.beta2, t.eps, t.lr, *t.step);
+  float p[7];
+  for (int k = 0; k < 7; ++k) {
+    float pk = cam[k], m = t.exp_avg[k], v = t.exp_avg_sq[k];
+    adam_one(pk, a.g_cam[k], m, v, c);
+    p[k] = pk;
+    cam[k] = pk;
+    t.exp_avg[k] = m;
+    t.exp_avg_sq[k] = v;
+  }
+  *t.step += 1.f;
+  *t.loss_out = l;
+  if (t.best_loss && l < *t.best_loss) {  // (NaN: not better, as torch's comparison)
+    for (int k = 0; k < 7; ++k) t.best[k] = p[k];
+    *t.best_loss = l;
+  }
+}
 
 // workgroup wg of nwg of one camera's gradient (k_cam_grad_parts: the whole grid; k_cam_grad_batch: the
 // x extent of the grid row of camera blockIdx.y)
@@ -570,6 +612,7 @@ __device__ __forceinline__ void cam_grad_parts_body(const CamPartsArgs& a, unsig
     }
     __syncthreads();
     if (threadIdx.x == 0) cam_grad_epilogue(a.cam, a.c2w, red, a.g_cam);
+    if (a.has_tail) cam_tail(a);
     return;
   }
   if (threadIdx.x < 12) {  // fixed-order sum over the waves, published as this workgroup's partial
@@ -599,8 +642,8 @@ __device__ __forceinline__ void cam_grad_parts_body(const CamPartsArgs& a, unsig
   __syncthreads();
   if (threadIdx.x < 12) red[threadIdx.x][0] = t;
   __syncthreads();
-  if (threadIdx.x != 0) return;
-  cam_grad_epilogue(a.cam, a.c2w, red, a.g_cam);
+  if (threadIdx.x == 0) cam_grad_epilogue(a.cam, a.c2w, red, a.g_cam);
+  if (a.has_tail) cam_tail(a);
 }
 
 __global__ __launch_bounds__(kCamThreads) void k_cam_grad_parts(CamPartsArgs a) { cam_grad_parts_body(a, blockIdx.x, gridDim.x); }
@@ -659,9 +702,10 @@ extern "C" int nslam_cam_grad(const float* cam, const float* c2w, const double* 
   return e == hipSuccess ? NSLAM_OK : NSLAM_EHIP - (int)e;
 }
 
-extern "C" int nslam_cam_grad_parts(const float* cam, const float* c2w, const double* const* g_pts, int32_t n_parts,
-                                    const double* z_vals, const float* rays_d, int64_t n_rays, int32_t n_samples,
-                                    float* g_cam, double* ws, uint32_t* ticket, void* stream) {
+namespace {
+int cam_grad_parts_launch(const float* cam, const float* c2w, const double* const* g_pts, int32_t n_parts,
+                          const double* z_vals, const float* rays_d, int64_t n_rays, int32_t n_samples, float* g_cam,
+                          double* ws, uint32_t* ticket, const nslam_cam_tail* tail, void* stream) {
   if (!cam || !c2w || !g_cam || !ticket || !ws || n_rays < 0 || n_samples <= 0) return NSLAM_EINVAL;
   if (n_parts < 1 || n_parts > 4 || !g_pts) return NSLAM_EINVAL;
   if (n_rays > 0 && (!z_vals || !rays_d)) return NSLAM_EINVAL;
@@ -680,12 +724,33 @@ extern "C" int nslam_cam_grad_parts(const float* cam, const float* c2w, const do
   a.g_cam = g_cam;
   a.ws = ws;
   a.ticket = ticket;
+  if (tail) {
+    a.tail = *tail;
+    a.has_tail = 1;
+  }
   const int64_t np = n_rays * (int64_t)n_samples;
   int64_t wg = (np + kCamThreads - 1) / kCamThreads;
   wg = wg < 1 ? 1 : (wg > kCamParts ? kCamParts : wg);
   hipLaunchKernelGGL(k_cam_grad_parts, dim3((unsigned)wg), dim3(kCamThreads), 0, reinterpret_cast<hipStream_t>(stream), a);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? NSLAM_OK : NSLAM_EHIP - (int)e;
+}
+}  // namespace
+
+extern "C" int nslam_cam_grad_parts(const float* cam, const float* c2w, const double* const* g_pts, int32_t n_parts,
+                                    const double* z_vals, const float* rays_d, int64_t n_rays, int32_t n_samples,
+                                    float* g_cam, double* ws, uint32_t* ticket, void* stream) {
+  return cam_grad_parts_launch(cam, c2w, g_pts, n_parts, z_vals, rays_d, n_rays, n_samples, g_cam, ws, ticket, nullptr,
+                               stream);
+}
+
+extern "C" int nslam_cam_grad_step(const nslam_cam_tail* tail, const float* c2w, const double* const* g_pts,
+                                   int32_t n_parts, const double* z_vals, const float* rays_d, int64_t n_rays,
+                                   int32_t n_samples, float* g_cam, double* ws, uint32_t* ticket, void* stream) {
+  if (!tail || !tail->cam || !tail->exp_avg || !tail->exp_avg_sq || !tail->step || !tail->loss_out) return NSLAM_EINVAL;
+  if (tail->n_rays < 0 || (tail->n_rays > 0 && !tail->ray_loss) || (tail->best_loss && !tail->best)) return NSLAM_EINVAL;
+  return cam_grad_parts_launch(tail->cam, c2w, g_pts, n_parts, z_vals, rays_d, n_rays, n_samples, g_cam, ws, ticket,
+                               tail, stream);
 }
 
 extern "C" int nslam_cam_grad_batch(const float* cams, const float* c2w, int64_t c2w_stride, int32_t n_cams,

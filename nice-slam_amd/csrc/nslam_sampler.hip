@@ -262,4 +262,4 @@ extern "C" const char* nslam_strerror(int code) {
 }
 
 // v9: nslam_cam_grad / nslam_cam_pose exports (they first shipped under v8 without a bump)
-extern "C" int nslam_abi_version(void) { return 22; }
+extern "C" int nslam_abi_version(void) { return 23; }

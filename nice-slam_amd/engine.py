@@ -653,8 +653,9 @@ class TrackingEngine:
         sampler, decoders (ray form, ReLU masks saved) nslam_sample_rays, nslam_query_fwd_ws
         compositing + tracker loss + their backward    nslam_render_loss (mode TRACKER, median)
         d loss / d pts, frozen decoders                nslam_query_bwd_decoder (mask-only, 3 branches)
-        pts → rays → c2w → cam                         nslam_cam_grad (closed form, include/nslam.h)
-        Adam on the camera                             ops.FusedAdam (device step count)
+        pts → rays → c2w → cam                         nslam_cam_grad_step (closed form, include/nslam.h),
+        Adam on the camera, loss sum, best pose          whose last workgroup also steps the camera (FusedAdam's
+                                                       update, device step count) and keeps the best pose
 
     so `iters` iterations can be captured in one hipGraph.  Grids and decoders are constants
     (Tracker.py:138-141): no grid or weight gradients are formed.  As in the reference, dropped
@@ -675,12 +676,24 @@ class TrackingEngine:
         # ABI v15 nslam_cam_grad_parts: the frozen decoders' d/dpts buffers summed inside a
         # multi-workgroup camera-gradient kernel (no torch adds, no single-workgroup reduction)
         self.cam_parts = True
+        # ABI v23 nslam_cam_grad_step: with a FusedAdam over the camera alone, its step, the loss sum and the
+        # best pose run in the camera-gradient launch's last workgroup (two launches fewer per iteration)
+        self.cam_tail = True
         self._cam_ws = self._cam_ticket = None
         self._loss = None  # the last iteration's loss (device f64 scalar, overwritten by the next one)
 
     def n_window(self):
         h0, h1, w0, w1 = self.window
         return (h1 - h0) * (w1 - w0)
+
+    @staticmethod
+    def _tail_ok(optimizer, cam):
+        """The fused camera tail applies to a FusedAdam stepping exactly this dense camera tensor."""
+        if not isinstance(optimizer, ops.FusedAdam):
+            return False
+        ps = [p for g in optimizer.param_groups for p in g["params"]]
+        return (len(ps) == 1 and ps[0] is cam and optimizer.param_groups[0].get("rows") is None
+                and cam not in optimizer.mirrors and cam.is_contiguous() and cam.numel() == 7)
 
     def iteration(self, cam, depth, color, pix, optimizer, n=None, seed=0, best=None):
         """One camera iteration on frame (depth [H,W], color [H,W,3]) with pixel draws `pix`
@@ -715,6 +728,15 @@ class TrackingEngine:
             gps = self.eng.query_bwd("color", ro, rd, z, g_raw, (), (), pts_grad=True, pts_parts=True)
             if torch.is_tensor(gps):
                 gps = [gps]
+            if self._loss is None:
+                self._loss = torch.empty((), dtype=torch.float64, device=cam.device)
+            if self.cam_tail and self._tail_ok(optimizer, cam):
+                ex, ex2, stp = optimizer.state_of(cam)
+                adam = (ex, ex2, stp, optimizer.group_of(cam)["lr"], *optimizer.betas, optimizer.eps)
+                bl, bc = (None, None) if best is None else (best[0], best[1])
+                ops.cam_grad_step(cam.detach(), c2w, gps, z, rd, cam.grad, self._cam_ws, self._cam_ticket, adam,
+                                  ray_loss, self._loss, bl, bc)
+                return self._loss
             ops.cam_grad_parts(cam.detach(), c2w, gps, z, rd, cam.grad, self._cam_ws, self._cam_ticket)
         else:
             g_pts = self.eng.query_bwd("color", ro, rd, z, g_raw, (), (), pts_grad=True)

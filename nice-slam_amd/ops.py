@@ -686,6 +686,33 @@ def cam_grad_parts(cam, c2w, g_pts, z, rd, out, ws, ticket):
     return out
 
 
+def cam_grad_step(cam, c2w, g_pts, z, rd, g_cam, ws, ticket, adam, ray_loss, loss_out, best_loss=None, best=None):
+    """nslam_cam_grad_step (ABI v23): cam_grad_parts, then in its last workgroup the camera's Adam step in
+    place (adam = (exp_avg [7], exp_avg_sq [7], step [1], lr, beta1, beta2, eps)), loss_out = the fixed-order
+    sum of ray_loss and, with best_loss / best, the best-pose update — bit-identical to cam_grad_parts +
+    FusedAdam.step + loss_sum_best, in one launch."""
+    n, S = z.shape
+    ex, ex2, stp, lr, b1, b2, eps = adam
+    checks = ((cam, torch.float32, (7,)), (c2w, torch.float32, (3, 4)), (z, torch.float64, (n, S)),
+              (rd, torch.float32, (n, 3)), (g_cam, torch.float32, (7,)), (ws, torch.float64, (384,)),
+              (ticket, torch.int32, (1,)), (ex, torch.float32, (7,)), (ex2, torch.float32, (7,)),
+              (stp, torch.float32, (1,)), (ray_loss, torch.float64, (ray_loss.numel(),)),
+              (loss_out, torch.float64, ()))
+    if best_loss is not None:
+        checks += ((best_loss, torch.float64, ()), (best, torch.float32, (7,)))
+    for t, dt, shp in checks + tuple((g, torch.float64, (n * S, 3)) for g in g_pts):
+        if t.dtype != dt or tuple(t.shape) != shp or not t.is_contiguous():
+            raise ValueError(f"cam_grad_step: expected contiguous {dt} {shp}, got {t.dtype} {tuple(t.shape)}")
+    tail = _lib.NslamCamTail(ptr(cam), ptr(ex), ptr(ex2), ptr(stp), float(lr), float(b1), float(b2), float(eps),
+                             ptr(ray_loss), ray_loss.numel(), ptr(loss_out), ptr(best_loss), ptr(best))
+    bufs = (ctypes.c_void_p * len(g_pts))(*[ptr(g) for g in g_pts])
+    with _span("cam_grad"):
+        rc = lib().nslam_cam_grad_step(ctypes.byref(tail), ptr(c2w), bufs, len(g_pts), ptr(z), ptr(rd), n, S,
+                                       ptr(g_cam), ptr(ws), ptr(ticket), stream_ptr(cam.device))
+    check(rc, "nslam_cam_grad_step")
+    return loss_out
+
+
 CAM_GRAD_WS_DOUBLES = 32 * 12  # NSLAM_CAM_GRAD_WS_DOUBLES
 
 

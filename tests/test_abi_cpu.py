@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol(pkg):
 
 def test_abi_version_and_strerror(pkg):
     L = pkg._lib.lib()
-    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 22
+    assert L.nslam_abi_version() == pkg._lib.ABI_VERSION == 23
     assert L.nslam_strerror(0) == b"ok"
     assert b"invalid" in L.nslam_strerror(-1)
 
@@ -284,6 +284,35 @@ def test_v22_cam_vector_batch_validates_without_gpu(pkg):
     assert L.nslam_cam_vector_batch(4096, 16, 0, 4096, None, None) == -1     # no cameras
     assert L.nslam_cam_vector_batch(4096, 16, 65, 4096, None, None) == -1    # n > 64
     assert L.nslam_cam_vector_batch(4096, 8, 2, 4096, None, None) == -1      # stride < 12
+
+
+def test_v23_cam_grad_step_validates_without_gpu(pkg):
+    """nslam_cam_grad_step needs its tail (camera, Adam state, step count, loss output; a loss vector when there
+    are rays; the best pose with a best loss) before the gradient's own checks — all before any launch."""
+    import ctypes
+    L = pkg._lib.lib()
+    T = pkg._lib.NslamCamTail
+    bufs = (ctypes.c_void_p * 1)(4096)
+
+    def call(tail):
+        return L.nslam_cam_grad_step(None if tail is None else ctypes.byref(tail), 4096, bufs, 1, 4096, 4096, 10, 4,
+                                     4096, 4096, 4096, None)
+
+    def tail(**kw):
+        f = dict(cam=4096, exp_avg=4096, exp_avg_sq=4096, step=4096, lr=0.001, beta1=0.9, beta2=0.999, eps=1e-8,
+                 ray_loss=4096, n_rays=10, loss_out=4096, best_loss=None, best=None)
+        f.update(kw)
+        return T(**f)
+
+    assert call(None) == -1
+    assert call(tail(cam=None)) == -1
+    assert call(tail(step=None)) == -1
+    assert call(tail(loss_out=None)) == -1
+    assert call(tail(ray_loss=None)) == -1
+    assert call(tail(n_rays=-1)) == -1
+    assert call(tail(best_loss=4096)) == -1            # best loss without the best pose
+    assert L.nslam_cam_grad_step(ctypes.byref(tail()), None, bufs, 1, 4096, 4096, 10, 4, 4096, 4096, 4096,
+                                 None) == -1           # the gradient's own checks (no pose)
 
 
 def test_v21_gather_frame_needs_a_pose_or_a_camera(pkg):

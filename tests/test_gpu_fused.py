@@ -874,3 +874,38 @@ def test_engine_prefetch_discards_batch_of_other_frames(tiny):
     eng.iteration("color", moved, *args, seed=11, prefetch=True)
     ro = eng._pre[2][0][0].view(len(moved), 150, 3)
     assert torch.equal(ro[0], moved[0][2][:3, 3].expand(150, 3))
+
+
+@pytest.mark.parametrize("with_best", [False, True])
+def test_cam_grad_step_matches_separate_launches(tiny, with_best):
+    """nslam_cam_grad_step (ABI v23): the tracking iteration with the camera's Adam step, the loss sum and the
+    best-pose update fused into the camera-gradient launch == cam_grad_parts + FusedAdam.step + loss_sum_best,
+    bit for bit over 6 iterations (camera, gradient, Adam moments and step count, loss, best pose and loss)."""
+    import copy
+    scn = Scene(tiny)
+    slam = scn.slam(base_cfg())
+    cam0 = P.common.get_tensor_from_camera(scn.c2w).cuda()
+    cam0[4:] += torch.tensor([0.02, -0.01, 0.015], device=DEV)
+    gen = torch.Generator().manual_seed(9)
+    pixs = [torch.randint(400, (200,), generator=gen) for _ in range(6)]
+    runs = {}
+    for tail in (False, True):
+        te = P.engine.TrackingEngine(copy.deepcopy(slam.shared_decoders), slam.shared_c, scn.bound, 32, 16,
+                                     (scn.H, scn.W), (scn.fx, scn.fy, scn.cx, scn.cy), ignore_edge=(20, 20),
+                                     w_color=0.5, handle_dynamic=True, use_color=True, device=DEV)
+        te.cam_tail = tail
+        cam = cam0.clone().requires_grad_(True)
+        opt = P.ops.FusedAdam([{"params": [cam], "lr": 0.003}])
+        best = (torch.full((), float("inf"), dtype=torch.float64, device=DEV), cam0.clone()) if with_best else None
+        trace = []
+        for pix in pixs:
+            loss = te.iteration(cam, scn.depth.cuda(), scn.color.cuda(), (pix % te.n_window()).cuda(), opt, best=best)
+            trace.append(torch.cat([cam.detach(), cam.grad.detach(), *opt.state_of(cam)]).clone())
+            trace.append(loss.detach().clone().view(1))
+        if best is not None:
+            trace += [best[0].clone().view(1), best[1].clone()]
+        runs[tail] = trace
+    assert float(runs[False][1].abs().sum()) > 0
+    assert not torch.equal(runs[False][0][:7], cam0)  # the camera moved
+    for a, b in zip(runs[True], runs[False]):
+        assert torch.equal(a, b), (a - b).abs().max()
