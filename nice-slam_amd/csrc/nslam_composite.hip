@@ -256,7 +256,81 @@ struct LossArgs {
   float* g_raw;
   double* resid;      // tracker: r per ray (ws)
   const double* thr;  // tracker: 10 * median (ws), read by the backward pass
+  int32_t inline_median;  // pass 2 forms the threshold itself (n <= kInlineMedian)
 };
+
+// Tracker handle_dynamic: thr = 10 * median(r over kept rays) (torch.median: lower median), by every thread
+// of one workgroup: kept residuals into LDS (sv: a power of two >= n doubles); up to one per thread
+// (tracking: 200 rays) the median is selected by rank, else (or with a NaN) padded with +inf to a power of
+// two and bitonic-sorted.  Either way the same value for any workgroup size.
+constexpr int kMedianMax = 16384;
+
+__device__ double median_thr_block(const double* __restrict__ r, const uint8_t* __restrict__ keep, int n,
+                                   double* sv) {
+  __shared__ int cnt, nan_seen;
+  __shared__ double thr;
+  if (threadIdx.x == 0) cnt = nan_seen = 0;
+  __syncthreads();
+  int np2 = 1;
+  while (np2 < n) np2 <<= 1;
+  for (int i = threadIdx.x; i < np2; i += blockDim.x) sv[i] = INFINITY;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const double v = r[i];  // (loaded beside the mask, not after it: one memory round trip, not two)
+    if (!keep || keep[i]) {
+      if (v != v) nan_seen = 1;
+      sv[atomicAdd(&cnt, 1)] = v;
+    }
+  }
+  __syncthreads();
+  const int c = cnt;
+  if (c <= (int)blockDim.x && !nan_seen) {
+    // selection by rank (one value per thread, ties broken by slot): the value of rank (c-1)/2 is
+    // the lower median — the element the sort below would put there, without its log^2 passes
+    const int i = threadIdx.x;
+    if (i < c) {
+      const double x = sv[i];
+      int rank = 0;
+#pragma unroll 16
+      for (int j = 0; j < c; ++j) {  // (unrolled: 16 broadcast LDS reads in flight, not one at a time)
+        const double y = sv[j];
+        rank += (y < x) || (y == x && j < i);
+      }
+      if (rank == (c - 1) / 2) thr = 10.0 * x;
+    }
+    if (c == 0 && i == 0) thr = INFINITY;
+    __syncthreads();
+    return thr;
+  }
+  for (int k = 2; k <= np2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < np2; i += blockDim.x) {
+        const int l = i ^ j;
+        if (l > i) {
+          const double x = sv[i], y = sv[l];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) {
+            sv[i] = y;
+            sv[l] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  return cnt > 0 ? 10.0 * sv[(cnt - 1) / 2] : INFINITY;
+}
+
+__global__ __launch_bounds__(1024) void k_median_thr(const double* __restrict__ r, const uint8_t* __restrict__ keep,
+                                                     int n, double* __restrict__ thr) {
+  extern __shared__ double sv[];
+  const double t = median_thr_block(r, keep, n, sv);
+  if (threadIdx.x == 0) *thr = t;
+}
+
+// up to this many rays the tracker's loss pass 2 forms the threshold itself, in every workgroup (one
+// residual per thread: the rank selection), instead of a k_median_thr launch between the passes
+constexpr int kInlineMedian = 256;
 
 // PASS 0: mapper, fwd + loss + bwd in one pass.
 // PASS 1: tracker fwd (outputs + residual r).  PASS 2: tracker loss + bwd (after the median).
@@ -264,6 +338,17 @@ template <int PASS>
 __global__ __launch_bounds__(256) void k_render_loss(LossArgs a) {
   const int lane = threadIdx.x & 63;
   const int64_t ray = (int64_t)blockIdx.x * 4 + wave_id();
+  double thr = 0.0;
+  if constexpr (PASS == 2) {
+    if (a.cfg.handle_dynamic) {
+      if (a.inline_median) {  // (the whole workgroup, before any wave leaves)
+        __shared__ double sv[kInlineMedian];
+        thr = median_thr_block(a.resid, a.keep, (int)a.n, sv);
+      } else {
+        thr = *a.thr;
+      }
+    }
+  }
   if (ray >= a.n) return;
   const int S = a.S;
   const float* rr = a.raw + ray * (int64_t)S * 4;
@@ -295,7 +380,7 @@ __global__ __launch_bounds__(256) void k_render_loss(LossArgs a) {
       if (lane == 0) a.resid[ray] = r;
       return;
     }
-    const bool m = kp && gt > 0.f && (!a.cfg.handle_dynamic || r < *a.thr);
+    const bool m = kp && gt > 0.f && (!a.cfg.handle_dynamic || r < thr);
     gd = m ? -(sgnd(x) * (1.0 / sq)) : 0.0;
     lossd = m ? r : 0.0;
     mcol = m && a.cfg.use_color;
@@ -311,65 +396,6 @@ __global__ __launch_bounds__(256) void k_render_loss(LossArgs a) {
   }
   if (a.ray_loss && lane == 0) a.ray_loss[ray] = lossd;
   if (a.g_raw) ray_bwd(sm, nch, S, o.d, gd, 0.0, gc0, gc1, gc2, a.g_raw + ray * (int64_t)S * 4, lane);
-}
-
-// Tracker handle_dynamic: thr = 10 * median(r over kept rays) (torch.median: lower median).
-// One workgroup: kept residuals into LDS; up to one per thread (tracking: 200 rays) the median is
-// selected by rank, else (or with a NaN) padded with +inf to a power of two and bitonic-sorted.
-constexpr int kMedianMax = 16384;
-
-__global__ __launch_bounds__(1024) void k_median_thr(const double* __restrict__ r, const uint8_t* __restrict__ keep,
-                                                     int n, double* __restrict__ thr) {
-  extern __shared__ double sv[];
-  __shared__ int cnt, nan_seen;
-  if (threadIdx.x == 0) cnt = nan_seen = 0;
-  __syncthreads();
-  int np2 = 1;
-  while (np2 < n) np2 <<= 1;
-  for (int i = threadIdx.x; i < np2; i += blockDim.x) sv[i] = INFINITY;
-  __syncthreads();
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    if (!keep || keep[i]) {
-      const double v = r[i];
-      if (v != v) nan_seen = 1;
-      sv[atomicAdd(&cnt, 1)] = v;
-    }
-  }
-  __syncthreads();
-  const int c = cnt;
-  if (c <= (int)blockDim.x && !nan_seen) {
-    // selection by rank (one value per thread, ties broken by slot): the value of rank (c-1)/2 is
-    // the lower median — the element the sort below would put there, without its log^2 passes
-    const int i = threadIdx.x;
-    if (i < c) {
-      const double x = sv[i];
-      int rank = 0;
-      for (int j = 0; j < c; ++j) {
-        const double y = sv[j];
-        rank += (y < x) || (y == x && j < i);
-      }
-      if (rank == (c - 1) / 2) *thr = 10.0 * x;
-    }
-    if (c == 0 && i == 0) *thr = INFINITY;
-    return;
-  }
-  for (int k = 2; k <= np2; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < np2; i += blockDim.x) {
-        const int l = i ^ j;
-        if (l > i) {
-          const double x = sv[i], y = sv[l];
-          const bool up = (i & k) == 0;
-          if ((x > y) == up) {
-            sv[i] = y;
-            sv[l] = x;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
-  if (threadIdx.x == 0) *thr = cnt > 0 ? 10.0 * sv[(cnt - 1) / 2] : INFINITY;
 }
 
 int hip_status() {
@@ -452,7 +478,8 @@ extern "C" int nslam_render_loss(const nslam_loss_cfg* cfg, const float* raw, co
   a.resid = w;
   a.thr = w + n_rays;
   hipLaunchKernelGGL(k_render_loss<1>, grid, block, 0, s, a);  // outputs + residuals
-  if (cfg->handle_dynamic) {
+  a.inline_median = n_rays <= kInlineMedian && !getenv("NSLAM_MEDIAN_LAUNCH");
+  if (cfg->handle_dynamic && !a.inline_median) {
     int np2 = 1;
     while (np2 < n_rays) np2 <<= 1;
     const size_t lds = (size_t)np2 * sizeof(double);

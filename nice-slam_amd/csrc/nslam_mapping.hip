@@ -419,7 +419,7 @@ struct CamArgs {
 // The epilogue both camera-gradient kernels share (one thread): g_R = A·R, the quaternion VJP of
 // quad2rotation, and the translation part.  red[k][0], k < 12: Σ g (k < 3) and A (k = 3..11).
 __device__ void cam_grad_epilogue(const float* __restrict__ cam, const float* __restrict__ c2w, const double (*red)[kCamThreads / 64],
-                                  float* __restrict__ g_cam) {
+                                  float* __restrict__ g_cam, float* __restrict__ g_lds = nullptr) {
   struct Ax {
     const float* cam;
     const float* c2w;
@@ -457,8 +457,12 @@ __device__ void cam_grad_epilogue(const float* __restrict__ cam, const float* __
     Hq[i] = h;
     qHq += q[i] * h;
   }
-  for (int i = 0; i < 4; ++i) a.g_cam[i] = (float)(s * Hq[i] - 0.5 * s * s * qHq * q[i]);
-  for (int k = 0; k < 3; ++k) a.g_cam[4 + k] = (float)red[k][0];
+  float gc[7];
+  for (int i = 0; i < 4; ++i) gc[i] = (float)(s * Hq[i] - 0.5 * s * s * qHq * q[i]);
+  for (int k = 0; k < 3; ++k) gc[4 + k] = (float)red[k][0];
+  for (int k = 0; k < 7; ++k) a.g_cam[k] = gc[k];
+  if (g_lds)
+    for (int k = 0; k < 7; ++k) g_lds[k] = gc[k];
 }
 
 __global__ __launch_bounds__(kCamThreads) void k_cam_grad(CamArgs a) {
@@ -529,41 +533,48 @@ struct CamPartsArgs {
 
 // ABI v23: what follows a tracking iteration's camera gradient, in the workgroup that formed it (all its
 // threads): the loss sum (k_loss_sum_best's fixed-order tree over its first kTailSum threads: the same
-// value), Adam on the 7-vector (adam_coef / adam_one: k_adam's element update, bit for bit), the step
-// count, and the best-pose update with the stepped camera.  Thread 0 wrote g_cam (the epilogue) and
-// alone reads it back, and it alone writes the camera after the epilogue read it.
+// value), Adam on the 7-vector (adam_coef / adam_one, one element per thread: k_adam's element update, bit
+// for bit), the step count, and the best-pose update with the stepped camera.  The camera, its Adam state,
+// the step count and the best loss are loaded before the tree (their latency hides behind it); thread 0's
+// epilogue left g_cam in g_lds, published by the tree's barriers.  Every read of *step / *best_loss is
+// issued before those barriers, so thread 0 may replace them after.
 constexpr int kTailSum = 256;
-__device__ void cam_tail(const CamPartsArgs& a) {
+__device__ void cam_tail(const CamPartsArgs& a, const float* g_lds) {
   const nslam_cam_tail& t = a.tail;
   __shared__ double s[kTailSum];
-  if (threadIdx.x < kTailSum) {
+  const int k = threadIdx.x;
+  float p = 0.f, m = 0.f, v = 0.f, stp = 0.f;
+  double bl = 0.0;
+  if (k < 7) {
+    p = t.cam[k];
+    m = t.exp_avg[k];
+    v = t.exp_avg_sq[k];
+    stp = *t.step;
+    if (t.best_loss) bl = *t.best_loss;
+  }
+  if (k < kTailSum) {
     double acc = 0.0;
-    for (int64_t i = threadIdx.x; i < t.n_rays; i += kTailSum) acc += t.ray_loss[i];
-    s[threadIdx.x] = acc;
+    for (int64_t i = k; i < t.n_rays; i += kTailSum) acc += t.ray_loss[i];
+    s[k] = acc;
   }
   __syncthreads();
   for (int w = kTailSum / 2; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
+    if (k < w) s[k] += s[k + w];
     __syncthreads();
   }
-  if (threadIdx.x != 0) return;
+  if (k >= 7) return;
   const double l = s[0];
-  float* cam = t.cam;
-  const AdamCoef c = adam_coef(t.beta1, t.beta2, t.eps, t.lr, *t.step);
-  float p[7];
-  for (int k = 0; k < 7; ++k) {
-    float pk = cam[k], m = t.exp_avg[k], v = t.exp_avg_sq[k];
-    adam_one(pk, a.g_cam[k], m, v, c);
-    p[k] = pk;
-    cam[k] = pk;
-    t.exp_avg[k] = m;
-    t.exp_avg_sq[k] = v;
-  }
-  *t.step += 1.f;
-  *t.loss_out = l;
-  if (t.best_loss && l < *t.best_loss) {  // (NaN: not better, as torch's comparison)
-    for (int k = 0; k < 7; ++k) t.best[k] = p[k];
-    *t.best_loss = l;
+  const bool better = t.best_loss && l < bl;  // (NaN: not better, as torch's comparison)
+  const AdamCoef c = adam_coef(t.beta1, t.beta2, t.eps, t.lr, stp);
+  adam_one(p, g_lds[k], m, v, c);
+  t.cam[k] = p;
+  t.exp_avg[k] = m;
+  t.exp_avg_sq[k] = v;
+  if (better) t.best[k] = p;
+  if (k == 0) {
+    *t.step = stp + 1.f;
+    *t.loss_out = l;
+    if (better) *t.best_loss = l;
   }
 }
 
@@ -598,6 +609,8 @@ __device__ __forceinline__ void cam_grad_parts_body(const CamPartsArgs& a, unsig
   for (int k = 0; k < 12; ++k)
     for (int off = 32; off > 0; off >>= 1) acc[k] += __shfl_xor(acc[k], off, 64);
   __shared__ double red[12][kCamThreads / 64];
+  __shared__ float g_tail[7];
+  float* const g_lds = a.has_tail ? g_tail : nullptr;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (lane == 0) {
 #pragma unroll
@@ -611,8 +624,8 @@ __device__ __forceinline__ void cam_grad_parts_body(const CamPartsArgs& a, unsig
       red[threadIdx.x][0] = t;
     }
     __syncthreads();
-    if (threadIdx.x == 0) cam_grad_epilogue(a.cam, a.c2w, red, a.g_cam);
-    if (a.has_tail) cam_tail(a);
+    if (threadIdx.x == 0) cam_grad_epilogue(a.cam, a.c2w, red, a.g_cam, g_lds);
+    if (a.has_tail) cam_tail(a, g_lds);
     return;
   }
   if (threadIdx.x < 12) {  // fixed-order sum over the waves, published as this workgroup's partial
@@ -642,8 +655,8 @@ __device__ __forceinline__ void cam_grad_parts_body(const CamPartsArgs& a, unsig
   __syncthreads();
   if (threadIdx.x < 12) red[threadIdx.x][0] = t;
   __syncthreads();
-  if (threadIdx.x == 0) cam_grad_epilogue(a.cam, a.c2w, red, a.g_cam);
-  if (a.has_tail) cam_tail(a);
+  if (threadIdx.x == 0) cam_grad_epilogue(a.cam, a.c2w, red, a.g_cam, g_lds);
+  if (a.has_tail) cam_tail(a, g_lds);
 }
 
 __global__ __launch_bounds__(kCamThreads) void k_cam_grad_parts(CamPartsArgs a) { cam_grad_parts_body(a, blockIdx.x, gridDim.x); }

@@ -129,10 +129,12 @@ def _autograd_loss(raw, z, gd, gc, keep, mode, use_color, handle_dynamic, w):
     return depth, var, color, loss.detach(), raw.grad
 
 
-# n_per 100 (300 rays): the median by rank selection; 400 (1200 rays > 1024 threads): the bitonic sort
+# n_per 100 (300 rays): the median by rank selection; 400 (1200 rays > 1024 threads): the bitonic sort;
+# 60 (180 rays <= 256): the threshold formed inside loss pass 2 (no median launch)
 @pytest.mark.parametrize("mode,use_color,hd,n_per", [("mapper", True, False, 100), ("mapper", False, False, 100),
                                                      ("tracker", True, True, 100), ("tracker", False, True, 100),
-                                                     ("tracker", True, False, 100), ("tracker", True, True, 400)])
+                                                     ("tracker", True, False, 100), ("tracker", True, True, 400),
+                                                     ("tracker", True, True, 60)])
 def test_render_loss_matches_autograd(tiny, mode, use_color, hd, n_per):
     sc, frames = _frames(tiny)
     nice, c = _nice(sc)
@@ -909,3 +911,31 @@ def test_cam_grad_step_matches_separate_launches(tiny, with_best):
     assert not torch.equal(runs[False][0][:7], cam0)  # the camera moved
     for a, b in zip(runs[True], runs[False]):
         assert torch.equal(a, b), (a - b).abs().max()
+
+
+@pytest.mark.parametrize("n_per,nan", [(60, False), (60, True), (85, False), (2, False)])
+def test_tracker_median_in_pass2_matches_median_launch(tiny, monkeypatch, n_per, nan):
+    """Up to 256 rays the tracker loss's handle_dynamic threshold is formed inside loss pass 2 by every
+    workgroup (rank selection; the bitonic sort with a NaN residual) instead of the k_median_thr launch:
+    the same outputs bit for bit (NaN where NaN) — NSLAM_MEDIAN_LAUNCH=1 forces the launch."""
+    sc, frames = _frames(tiny)
+    nice, c = _nice(sc)
+    pix = torch.randint(96 * 128, (3 * n_per,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(8))
+    ro, rd, gd, gc, keep = P.ops.gather_rays(frames, pix, n_per, 96, 128, (0, 96, 0, 128), sc.fx, sc.fy, sc.cx,
+                                             sc.cy, sc.bound)
+    z = P.ops.sample_z(ro, rd, gd, sc.bound, 32, 16)
+    pts = ro[:, None, :] + rd[:, None, :] * z[:, :, None]
+    with torch.no_grad():
+        raw = nice(pts.reshape(-1, 3), c, stage="color", oob_bound=sc.bound).reshape(z.shape[0], z.shape[1], 4)
+    if nan:
+        k = int(torch.nonzero(keep)[0])
+        raw[k, :, 3] = float("nan")
+    outs = {}
+    for launch in (False, True):
+        if launch:
+            monkeypatch.setenv("NSLAM_MEDIAN_LAUNCH", "1")
+        outs[launch] = P.ops.render_loss(raw, z, gd, gc, keep, mode="tracker", use_color=True, handle_dynamic=True,
+                                         w_color=0.5)
+    for a, b in zip(outs[False], outs[True]):
+        torch.testing.assert_close(a, b, rtol=0, atol=0, equal_nan=True)
+    assert float(outs[False][3].nan_to_num().abs().sum()) > 0
