@@ -7,6 +7,9 @@
 // One wave per ray, one lane per sample; the transmittance is a wave prefix product and the sums
 // are wave shuffle reductions.  Rays with more than 64 samples are processed in 64-sample chunks
 // with a carried transmittance.
+#include <cstdlib>
+#include <cstring>
+
 #include "nslam_dev.h"
 
 namespace {
@@ -454,6 +457,8 @@ extern "C" int nslam_render_loss(const nslam_loss_cfg* cfg, const float* raw, co
   const bool trk = cfg->mode == NSLAM_LOSS_TRACKER;
   if (trk && cfg->handle_dynamic && n_rays > kMedianMax) return NSLAM_EUNSUPPORTED;
   if (ws_bytes < loss_ws(cfg, n_rays) || (loss_ws(cfg, n_rays) && !ws)) return NSLAM_EWORKSPACE;
+  const char* ml = getenv("NSLAM_MEDIAN_LAUNCH");  // "1": the separate median launch (A/B and tests)
+  if (ml && strcmp(ml, "0") != 0 && strcmp(ml, "1") != 0) return NSLAM_EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   LossArgs a{};
   a.cfg = *cfg;
@@ -478,7 +483,7 @@ extern "C" int nslam_render_loss(const nslam_loss_cfg* cfg, const float* raw, co
   a.resid = w;
   a.thr = w + n_rays;
   hipLaunchKernelGGL(k_render_loss<1>, grid, block, 0, s, a);  // outputs + residuals
-  a.inline_median = n_rays <= kInlineMedian && !getenv("NSLAM_MEDIAN_LAUNCH");
+  a.inline_median = n_rays <= kInlineMedian && !(ml && ml[0] == '1');
   if (cfg->handle_dynamic && !a.inline_median) {
     int np2 = 1;
     while (np2 < n_rays) np2 <<= 1;

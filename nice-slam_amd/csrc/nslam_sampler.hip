@@ -182,8 +182,9 @@ __global__ __launch_bounds__(256) void k_sample_wave(SamplerArgs a) {
     return;
   }
   int rank = 0;
-  for (int j = 0; j < S; ++j) {
-    const double vj = __shfl(v, j, 64);
+  const int v_lo = __double2loint(v), v_hi = __double2hiint(v);
+  for (int j = 0; j < S; ++j) {  // lane j's value by v_readlane (j is uniform): no LDS round trip per step
+    const double vj = __hiloint2double(__builtin_amdgcn_readlane(v_hi, j), __builtin_amdgcn_readlane(v_lo, j));
     rank += (vj < v || (vj == v && j < lane)) ? 1 : 0;
   }
   if (lane < S) out[rank] = v;

@@ -315,6 +315,16 @@ def test_v23_cam_grad_step_validates_without_gpu(pkg):
                                  None) == -1           # the gradient's own checks (no pose)
 
 
+def test_median_launch_knob_rejects_unknown_values(pkg, monkeypatch):
+    """NSLAM_MEDIAN_LAUNCH accepts "0" and "1" only: any other value is NSLAM_EINVAL before any launch."""
+    import ctypes
+    L = pkg._lib.lib()
+    cfg = pkg._lib.NslamLossCfg(pkg._lib.LOSS_TRACKER, 1, 1, 0.5)
+    monkeypatch.setenv("NSLAM_MEDIAN_LAUNCH", "yes")
+    assert L.nslam_render_loss(ctypes.byref(cfg), 4096, 4096, 4, 48, 4096, 4096, None, 4096, 4096, 4096, 4096,
+                               4096, 4096, 5 * 8, None) == -1
+
+
 def test_v21_gather_frame_needs_a_pose_or_a_camera(pkg):
     """A frame with neither c2w nor cam (ABI v21) is rejected before any launch."""
     L = pkg._lib.lib()
