@@ -1,5 +1,5 @@
 # Round 6 validation: the whole GPU suite + smoke, the default bench (all legs), a rocprofv3 kernel-stats
-# profile of the headline bench.  Copies the records into profiles/r06_*.
+# profile of the headline bench, under gpurun_out/TAG (copy the records to keep into profiles/r06_*).
 set -o pipefail
 TAG=${1:-r6final}; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread > $OUT/tests.log 2>&1 || { grep -E "FAILED|Error" $OUT/tests.log | head -20; tail -40 $OUT/tests.log; exit 1; }
